@@ -1,0 +1,93 @@
+"""CPU: pin the oracle against the reference's own outputs (tests/golden, made by
+tests/golden/make_golden.py from /root/reference).  Runs anywhere, no GPU."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden, golden_flags, rel_rms, tacotron2_config, weights_mod
+from oracle.griffin_lim_oracle import AudioOracle, mel_filters, stft, istft
+from oracle.tacotron2_oracle import Tacotron2Oracle
+
+T2_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2_*.npz")))
+
+
+@pytest.mark.parametrize("case", T2_CASES)
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_tacotron2_oracle_matches_reference(case, dtype):
+    z = golden(case)
+    fl = golden_flags(z)
+    sd = weights_mod().tacotron2_weights(0, location_attn=fl["location_attn"], trans_agent=fl["trans_agent"])
+    o = Tacotron2Oracle(sd, dtype=dtype, **fl)
+    enc = o.encoder(z["ids"])
+    assert rel_rms(enc, z["enc"]) < 1e-6
+    mel, stop, align = o.decoder(z["enc"])
+    # integer/index outputs: exact
+    assert mel.shape == z["mel"].shape, "frame count differs from the reference"
+    np.testing.assert_array_equal(align.argmax(1), z["align"].argmax(1))
+    np.testing.assert_array_equal(stop > 0.5, z["stop"] > 0.5)
+    # float outputs: fp32 reference vs restatement
+    assert rel_rms(mel, z["mel"]) < 1e-5
+    assert np.abs(align - z["align"]).max() < 1e-5
+    assert np.abs(stop - z["stop"]).max() < 1e-5
+    assert rel_rms(o.postnet(z["mel"]), z["mel_post"]) < 1e-5
+
+
+def test_stop_rule_frame_count_2L_plus_22():
+    """With the forward-attention mask (synthesize.py:86) the reference stops at 2L+22."""
+    for case in ("t2_fwdmask_L12", "t2_fwdmask_L40", "t2_fwdmask_L100"):
+        z = golden(case)
+        assert z["mel"].shape[0] == 2 * len(z["ids"]) + 22
+
+
+def test_forward_mask_wraparound_step0():
+    """Step-0 alignment is nonzero exactly at [0,1,2,3,L-1] (common_layers.py:207-213 wrap)."""
+    z = golden("t2_fwdmask_L40")
+    nz = np.nonzero(z["align"][0])[0].tolist()
+    assert nz == [0, 1, 2, 3, 39]
+
+
+@pytest.mark.parametrize("case", sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gl_*mel*.npz"))))
+def test_gl_oracle_matches_reference_glue(case, audio_cfg):
+    z = golden(case)
+    ap = AudioOracle(**{**audio_cfg, "griffin_lim_iters": int(z["iters"])})
+    np.random.seed(int(z["phase_seed"]))
+    pu = np.random.rand(1025, z["mel"].shape[1])
+    wav = ap.inv_mel_spectrogram(z["mel"], pu)
+    assert wav.dtype == np.float64 and wav.shape == z["wav"].shape
+    assert rel_rms(wav, z["wav"]) < 1e-12
+    if "S" in z:
+        assert rel_rms(ap.mel_magnitude(z["mel"]), z["S"]) < 1e-6
+
+
+def test_gl_linear_path(audio_cfg):
+    z = golden("gl_linear_it3")
+    ap = AudioOracle(**{**audio_cfg, "griffin_lim_iters": 3})
+    np.random.seed(int(z["phase_seed"]))
+    pu = np.random.rand(*z["spec"].shape)
+    assert rel_rms(ap.inv_spectrogram(z["spec"], pu), z["wav"]) < 1e-12
+
+
+def test_inverse_preemphasis_and_save_wav(audio_cfg):
+    ap = AudioOracle(**audio_cfg)
+    z = golden("preemph")
+    np.testing.assert_array_equal(ap.inv_preemphasis(z["x"]), z["y"])
+    z = golden("save_wav")
+    np.testing.assert_array_equal(AudioOracle.wav_to_int16(z["wav"]), z["pcm"])
+
+
+def test_librosa_restatement_properties(audio_cfg):
+    """Unpinned against librosa; check the published invariants instead."""
+    M = mel_filters(22050, 2048, 80, 0.0, 8000.0)
+    assert M.shape == (80, 1025) and (M >= 0).all()
+    # Slaney area norm: each filter integrates (over Hz) to ~1 -> sum * bin width ~ 1
+    bw = 22050 / 2048
+    assert np.allclose(M.sum(1) * bw, 1.0, atol=0.15)
+    # stft -> istft round trip reconstructs the signal (COLA with the sum-square normalisation)
+    rng = np.random.Generator(np.random.PCG64(0))
+    y = rng.standard_normal(275 * 40).astype(np.float32)
+    D = stft(y, 2048, 275, 1102)
+    assert D.dtype == np.complex64 and D.shape == (1025, 41)
+    y2 = istft(D, 275, 1102)
+    assert y2.shape == y.shape and rel_rms(y2, y) < 1e-5
