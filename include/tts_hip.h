@@ -1,0 +1,136 @@
+/*
+ * tts_hip.h — C-ABI of libtts_hip.so, the MI355X (gfx950) synthesis path of the
+ * prototypefund/your-voice-TTS drop-in.
+ *
+ * The reference has no FFI for this path: it is pure Python on stock PyTorch ops and librosa
+ * (SURVEY.md §0.1).  Each entry point below replaces one reference call site; the host package
+ * (your-voice-tts_amd/) binds them with ctypes and keeps the reference's Python signatures.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Pointers marked [dev] are device (HBM) pointers, [host]
+ *     are host pointers.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *   - Caller owns all input/output buffers; the library owns weights, workspace and graphs.
+ *   - Every call returns a tts_status; tts_last_error() gives the message of the last failure
+ *     on the calling thread.  No exceptions cross the ABI.
+ *   - A handle is not reentrant: one thread/stream per handle at a time (the reference decoder
+ *     keeps per-call state on the module and is not reentrant either, layers/tacotron2.py:161-177).
+ *   - All arithmetic is fp32 (fp64 for the inverse pre-emphasis, as scipy.signal.lfilter).
+ */
+#ifndef TTS_HIP_H
+#define TTS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int tts_status;
+#define TTS_OK 0
+#define TTS_ERR_INVALID 1     /* bad argument / shape / missing weight            */
+#define TTS_ERR_HIP 2         /* HIP runtime error (message in tts_last_error)    */
+#define TTS_ERR_UNSUPPORTED 3 /* configuration the path does not implement        */
+#define TTS_ERR_NOMEM 4
+
+typedef struct tts_decoder tts_decoder;
+typedef struct tts_postnet tts_postnet;
+typedef struct tts_gl tts_gl;
+
+/* One weight tensor in the reference's own state_dict layout (fp32, contiguous, [dev]). */
+typedef struct tts_tensor {
+    const char* key;   /* reference state_dict key, e.g. "decoder.attention_rnn.weight_ih" */
+    const float* data; /* [dev] fp32                                                        */
+    int64_t numel;
+} tts_tensor;
+
+/* Decoder flags: the arguments of layers/tacotron2.py:98-100 (Decoder.__init__) that change
+ * inference numerics, as mapped from the JSON config by utils/generic_utils.py:275-288. */
+typedef struct tts_decoder_config {
+    int r;                 /* frames per step (config "r")                                 */
+    int attn_norm;         /* 0 = softmax, 1 = sigmoid (common_layers.py:239-245)          */
+    int forward_attn;      /* use_forward_attn                                             */
+    int trans_agent;       /* transition_agent                                             */
+    int forward_attn_mask; /* forward_attn_mask (synthesize.py:86 forces 1)                */
+    int location_attn;     /* location_attn                                                */
+    int windowing;         /* windowing (attn_win), eval-only window (common_layers.py:184) */
+    int max_batch;         /* workspace capacity: sentences per call (<= 64)              */
+    int max_len;           /* workspace capacity: encoder length L (<= 1024)              */
+    int max_steps;         /* workspace capacity: decoder steps (max_decoder_steps)        */
+} tts_decoder_config;
+
+/* Replaces the construction + load_state_dict of layers/tacotron2.py:97-150 (Decoder).
+ * `tensors` must hold every decoder.* key of the reference state_dict for this config; they
+ * are repacked into the library's MFMA-fragment layout (the caller may free them after). */
+tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* tensors, int n_tensors,
+                              void* stream, tts_decoder** out);
+void tts_decoder_destroy(tts_decoder* d);
+
+/* Replaces Decoder.inference (layers/tacotron2.py:249-285) for a padded batch of sentences,
+ * with per-sentence semantics identical to the reference run alone at batch 1:
+ *   enc      [dev]  fp32 [B][Lmax][512] encoder outputs (rows >= lens[b] ignored)
+ *   lens     [host] int32 [B] encoder lengths L_b (2 <= L_b <= Lmax <= cfg.max_len)
+ *   max_steps        the reference's max_decoder_steps (<= cfg.max_steps)
+ *   mel      [dev]  fp32 [B][steps_cap*r][80]  mel frames (decoder_output, time-major)
+ *   stop     [dev]  fp32 [B][steps_cap]        sigmoid(stop token)
+ *   align    [dev]  fp32 [B][steps_cap][Lmax]  attention weights per step (may be NULL)
+ *   n_steps  [host] int32 [B] out: decoder steps taken by each sentence
+ * steps_cap must be >= max_steps + 20 (the reference can run up to 20 steps past the cap once
+ * every stop flag is set, layers/tacotron2.py:271-277).  Entries past n_steps[b] are left
+ * untouched.  Synchronises `stream` once per chunk of steps to read the stop flags. */
+tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
+                           int max_steps, int steps_cap, float* mel, float* stop, float* align,
+                           int32_t* n_steps, void* stream);
+
+/* Per-step timing of the last tts_decoder_run (ms of GPU time of the step loop, steps run). */
+tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run);
+
+/* Replaces Postnet (layers/tacotron2.py:30-45) + the residual add of models/tacotron2.py:69-70:
+ * out = mel + postnet(mel), per sentence at its own length (zero padding past T_b).
+ * `tensors` must hold the postnet.* keys. */
+tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_mel, void* stream,
+                              tts_postnet** out);
+void tts_postnet_destroy(tts_postnet* p);
+/*   mel [dev] fp32 [B][Tmax][n_mel] time-major; T [host] int32 [B]; out [dev] same shape. */
+tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, int B, int Tmax,
+                           float* out, void* stream);
+
+/* Audio parameters of AudioProcessor (utils/audio.py:12-54, 114-119). */
+typedef struct tts_audio_config {
+    int n_fft;          /* (num_freq-1)*2, must be 2048 */
+    int hop_length;     /* frame_shift_ms * sample_rate / 1000 */
+    int win_length;     /* frame_length_ms * sample_rate / 1000, <= n_fft */
+    int num_mels;
+    float min_level_db, ref_level_db, power, max_norm;
+    double preemphasis; /* lfilter coefficient, kept in double as the reference's Python float */
+    int signal_norm, symmetric_norm, clip_norm;
+} tts_audio_config;
+
+#define TTS_GL_FROM_MEL 0     /* AudioProcessor.inv_mel_spectrogram (utils/audio.py:164-172) */
+#define TTS_GL_FROM_LINEAR 1  /* AudioProcessor.inv_spectrogram     (utils/audio.py:154-162) */
+
+/* inv_mel_basis: [host] fp32 [n_fft/2+1][num_mels] = pinv(mel basis) (utils/audio.py:64-66);
+ * may be NULL when only the linear path is used. */
+tts_status tts_gl_create(const tts_audio_config* cfg, const float* inv_mel_basis, void* stream, tts_gl** out);
+void tts_gl_destroy(tts_gl* g);
+
+/* Batched Griffin-Lim vocoder: replaces inv_mel_spectrogram / inv_spectrogram, i.e.
+ * denormalise -> dB->amp -> [pinv mel->linear] -> ^power -> _griffin_lim (utils/audio.py:182-201,
+ * librosa 0.6.2 stft/istft) -> inverse pre-emphasis (lfilter, utils/audio.py:133-136).
+ *   spec    [dev]  fp32 [B][Fmax][n_in] frame-major (n_in = num_mels or n_fft/2+1 by mode)
+ *   F       [host] int32 [B] frames per sentence (>= 2)
+ *   phase_u [dev]  fp64 [B][n_fft/2+1][Fmax] initial phases as U[0,1) draws (the reference's
+ *                  np.random.rand(*S.shape)), or NULL: drawn on device from `seed`
+ *   wav     [dev]  fp64 [B][hop*(Fmax-1)]: sentence b fills its first hop*(F_b-1) samples */
+tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
+                      const double* phase_u, uint64_t seed, int iters, double* wav, void* stream);
+
+/* Time of the last tts_gl_run's iteration loop (ms, GPU) and kernel launches in it. */
+tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
+
+const char* tts_last_error(void);
+const char* tts_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TTS_HIP_H */

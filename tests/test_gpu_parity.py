@@ -1,0 +1,173 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden outputs and the
+oracle.  Tolerances (north_star: "alignments/stop-tokens bit-exact, mel and waveform within
+1e-4 RMS"): integer/index outputs — frame count, per-step attention argmax, stop decisions — are
+compared exactly; float outputs of a different fp32 reduction order cannot be bitwise equal, so
+alignments/stop tokens are held to max-abs 1e-4 and mel / waveform to relative RMS 1e-4
+(absolute RMS is vacuous here: the random-weight waveform has RMS ~1e-5)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden, golden_flags, load_pkg, rel_rms, weights_mod
+from oracle.griffin_lim_oracle import AudioOracle
+from oracle.tacotron2_oracle import Tacotron2Oracle
+
+pytestmark = pytest.mark.gpu
+
+T2_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2_*.npz")))
+MEL_RTOL = 1e-4
+ALIGN_ATOL = 1e-4
+WAV_RTOL = 1e-4
+
+
+def _model(fl, **kw):
+    t2 = load_pkg("tacotron2")
+    m = t2.Tacotron2(130, 0, r=1, attn_win=fl["attn_win"], attn_norm=fl["attn_norm"],
+                     forward_attn=fl["forward_attn"], trans_agent=fl["trans_agent"],
+                     forward_attn_mask=fl["forward_attn_mask"], location_attn=fl["location_attn"], **kw)
+    m.decoder.max_decoder_steps = fl["max_decoder_steps"]
+    return m.cuda().eval()
+
+
+def _check_decoder(out, b, z):
+    T = out["frames"][b]
+    assert T == z["mel"].shape[0], "frame count differs from the reference"
+    L = len(z["ids"])
+    al = out["align"][b, :T, :L].cpu().numpy()
+    np.testing.assert_array_equal(al.argmax(1), z["align"].argmax(1))
+    assert np.abs(al - z["align"]).max() < ALIGN_ATOL
+    st = out["stop"][b, :T].cpu().numpy()
+    np.testing.assert_array_equal(st > 0.5, z["stop"] > 0.5)
+    assert np.abs(st - z["stop"]).max() < ALIGN_ATOL
+    assert rel_rms(out["mel"][b, :T].cpu().numpy(), z["mel"]) < MEL_RTOL
+    assert rel_rms(out["mel_post"][b, :T].cpu().numpy(), z["mel_post"]) < MEL_RTOL
+
+
+@pytest.mark.parametrize("case", T2_CASES)
+def test_decoder_postnet_vs_reference(case):
+    """Decoder.inference + Postnet from the reference's own encoder outputs."""
+    z = golden(case)
+    m = _model(golden_flags(z))
+    enc = torch.from_numpy(z["enc"]).cuda()[None]
+    out = m.inference_batch(None, enc=enc, lens=[len(z["ids"])])
+    _check_decoder(out, 0, z)
+
+
+@pytest.mark.parametrize("case", ["t2_fwdmask_L12", "t2_fwdmask_L100", "t2_loc_fwd_ta_L24"])
+def test_full_inference_vs_reference(case):
+    """Tacotron2.inference(ids) end to end (encoder on the GPU, decoder + postnet in HIP)."""
+    z = golden(case)
+    m = _model(golden_flags(z))
+    mel, mel_post, align, stop = m.inference(torch.from_numpy(z["ids"])[None])
+    assert mel.shape == (1,) + z["mel"].shape and stop.shape == (1, z["mel"].shape[0], 1)
+    assert rel_rms(mel[0].cpu().numpy(), z["mel"]) < MEL_RTOL
+    assert rel_rms(mel_post[0].cpu().numpy(), z["mel_post"]) < MEL_RTOL
+    np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"].argmax(1))
+
+
+def test_batched_ragged_decoder_matches_batch1():
+    """A padded batch: every sentence gets exactly its batch-1 reference result."""
+    cases = ["t2_fwdmask_L40", "t2_fwdmask_L12", "t2_fwdmask_L100", "t2_fwdmask_L12", "t2_fwdmask_L40"]
+    zs = [golden(c) for c in cases]
+    m = _model(golden_flags(zs[0]))
+    Lmax = max(len(z["ids"]) for z in zs)
+    enc = torch.zeros(len(zs), Lmax, 512)
+    for b, z in enumerate(zs):
+        enc[b, :len(z["ids"])] = torch.from_numpy(z["enc"])
+    out = m.inference_batch(None, enc=enc.cuda(), lens=[len(z["ids"]) for z in zs])
+    for b, z in enumerate(zs):
+        _check_decoder(out, b, z)
+
+
+def test_batch64_lengths_property():
+    """Config-3 shape (B=64, L ~ U{60..160}): every sentence stops at 2L+22, oracle on two."""
+    w = weights_mod()
+    lens = w.synthetic_lengths(64, 2)
+    ids = [w.synthetic_ids(int(L), 100 + b) for b, L in enumerate(lens)]
+    fl = golden_flags(golden("t2_fwdmask_L100"))
+    m = _model(fl)
+    out = m.inference_batch(ids)
+    assert out["frames"] == [2 * int(L) + 22 for L in lens]
+    assert torch.isfinite(out["mel_post"]).all()
+    o = Tacotron2Oracle(w.tacotron2_weights(0), dtype=np.float32, **fl)
+    for b in (0, 37):
+        ref = o.inference(ids[b])
+        T = out["frames"][b]
+        assert T == ref["mel"].shape[0]
+        assert rel_rms(out["mel"][b, :T].cpu().numpy(), ref["mel"]) < MEL_RTOL
+        assert rel_rms(out["mel_post"][b, :T].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
+
+
+@pytest.mark.parametrize("case", sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gl_*mel*.npz"))))
+def test_griffin_lim_vs_reference_glue(case, audio_cfg):
+    """inv_mel_spectrogram with the reference's np.random phases (seeded) vs the reference's
+    AudioProcessor run on the librosa restatement."""
+    z = golden(case)
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": int(z["iters"])})
+    np.random.seed(int(z["phase_seed"]))
+    wav = ap.inv_mel_spectrogram(z["mel"])
+    assert wav.dtype == np.float64 and wav.shape == z["wav"].shape
+    assert rel_rms(wav, z["wav"]) < WAV_RTOL
+    pcm = load_pkg("synthesis").wav_to_int16(wav)
+    ref_pcm = AudioOracle.wav_to_int16(z["wav"])
+    assert np.abs(pcm.astype(np.int32) - ref_pcm).max() <= 2
+
+
+def test_griffin_lim_linear_path(audio_cfg):
+    z = golden("gl_linear_it3")
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 3})
+    np.random.seed(int(z["phase_seed"]))
+    assert rel_rms(ap.inv_spectrogram(z["spec"]), z["wav"]) < WAV_RTOL
+
+
+def test_griffin_lim_batched_ragged_60_iters(audio_cfg):
+    """Ragged batch at the metric's 60 iterations vs the oracle one sentence at a time."""
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**audio_cfg)  # griffin_lim_iters = 60
+    o = AudioOracle(**audio_cfg)
+    rng = np.random.Generator(np.random.PCG64(7))
+    Fs = [46, 13, 80, 2, 31]
+    Fmax = max(Fs)
+    mel = np.zeros((len(Fs), Fmax, 80), np.float32)
+    pu = np.zeros((len(Fs), 1025, Fmax))
+    for b, F in enumerate(Fs):
+        mel[b, :F] = rng.uniform(0, 1, size=(F, 80))
+        pu[b, :, :F] = rng.uniform(0, 1, size=(1025, F))
+    wav = ap.griffin_lim_batch(torch.from_numpy(mel).cuda(), Fs, phase_u=pu).cpu().numpy()
+    for b, F in enumerate(Fs):
+        ref = o.inv_mel_spectrogram(mel[b, :F].T, pu[b, :, :F])
+        n = ap.hop_length * (F - 1)
+        assert rel_rms(wav[b, :n], ref) < WAV_RTOL, (b, F)
+        assert np.all(wav[b, n:] == 0)
+
+
+def test_end_to_end_synthesis_vs_oracle(audio_cfg):
+    """ids -> wav through the whole HIP path vs the oracle chain (L=12, 60 GL iterations)."""
+    z = golden("t2_fwdmask_L12")
+    fl = golden_flags(z)
+    m = _model(fl)
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**audio_cfg)
+    np.random.seed(3)
+    wavs, info = load_pkg("synthesis").synthesize_batch(m, ap, [z["ids"]], phase="numpy")
+    np.random.seed(3)
+    ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(z["mel_post"].T)
+    assert info["frames"] == [z["mel"].shape[0]]
+    assert rel_rms(wavs[0], ref) < WAV_RTOL
+
+
+def test_native_errors_are_raised():
+    t2 = load_pkg("tacotron2")
+    m = t2.Tacotron2(130, 0, r=1, attn_norm="sigmoid", forward_attn=True, forward_attn_mask=True,
+                     location_attn=False).cuda()
+    with pytest.raises(ValueError):
+        m.inference_batch([[5]])  # L=1 has no alpha[n-2] in the reference
+    bad = m.state_dict()
+    bad["decoder.attention_rnn.weight_ih"] = torch.zeros(4096, 700)
+    with pytest.raises(RuntimeError):
+        m.load_state_dict(bad)

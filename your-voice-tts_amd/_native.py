@@ -1,0 +1,133 @@
+"""ctypes binding of libtts_hip.so (C-ABI in include/tts_hip.h).
+
+The library is loaded on first use.  If it is missing, fails to load, or no GPU is visible, the
+caller gets a RuntimeError: the product path has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TTS_HIP_LIB", os.path.join(_HERE, "libtts_hip.so"))
+
+TTS_GL_FROM_MEL = 0
+TTS_GL_FROM_LINEAR = 1
+
+# every symbol include/tts_hip.h declares
+EXPORTS = (
+    "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_last_timing",
+    "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
+    "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing",
+    "tts_last_error", "tts_version",
+)
+
+
+class TensorView(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
+class DecoderConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "r", "attn_norm", "forward_attn", "trans_agent", "forward_attn_mask", "location_attn",
+        "windowing", "max_batch", "max_len", "max_steps")]
+
+
+class AudioConfig(ctypes.Structure):
+    _fields_ = [("n_fft", ctypes.c_int), ("hop_length", ctypes.c_int), ("win_length", ctypes.c_int),
+                ("num_mels", ctypes.c_int), ("min_level_db", ctypes.c_float),
+                ("ref_level_db", ctypes.c_float), ("power", ctypes.c_float),
+                ("max_norm", ctypes.c_float), ("preemphasis", ctypes.c_double),
+                ("signal_norm", ctypes.c_int), ("symmetric_norm", ctypes.c_int), ("clip_norm", ctypes.c_int)]
+
+
+_lib = None
+_lock = threading.Lock()
+P = ctypes.c_void_p
+I32P = ctypes.POINTER(ctypes.c_int32)
+
+
+def _declare(lib):
+    vp = ctypes.c_void_p
+    lib.tts_decoder_create.argtypes = [ctypes.POINTER(DecoderConfig), ctypes.POINTER(TensorView), ctypes.c_int, vp,
+                                       ctypes.POINTER(vp)]
+    lib.tts_decoder_destroy.argtypes = [vp]
+    lib.tts_decoder_destroy.restype = None
+    lib.tts_decoder_run.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp,
+                                    I32P, vp]
+    lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    lib.tts_postnet_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    lib.tts_postnet_destroy.argtypes = [vp]
+    lib.tts_postnet_destroy.restype = None
+    lib.tts_postnet_run.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.tts_gl_create.argtypes = [ctypes.POINTER(AudioConfig), vp, vp, ctypes.POINTER(vp)]
+    lib.tts_gl_destroy.argtypes = [vp]
+    lib.tts_gl_destroy.restype = None
+    lib.tts_gl_run.argtypes = [vp, ctypes.c_int, vp, I32P, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64,
+                               ctypes.c_int, vp, vp]
+    lib.tts_gl_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    lib.tts_last_error.restype = ctypes.c_char_p
+    lib.tts_version.restype = ctypes.c_char_p
+    for name in EXPORTS:
+        fn = getattr(lib, name)
+        if fn.restype is ctypes.c_int or name.endswith(("_create", "_run", "_timing")):
+            fn.restype = ctypes.c_int
+
+
+def load_library(path: str = LIB_PATH):
+    """Load (once) and return the ctypes handle.  torch is imported first so that the HIP
+    runtime torch ships (SONAME libamdhip64.so.7) is the one the library binds to."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            import torch  # noqa: F401  (HIP runtime first)
+            if not os.path.exists(path):
+                raise RuntimeError(f"libtts_hip.so not found at {path}: build it with "
+                                   f"`make -C your-voice-tts_amd/csrc` (no CPU fallback exists)")
+            lib = ctypes.CDLL(path)
+            _declare(lib)
+            _lib = lib
+    return _lib
+
+
+def lib():
+    """Library handle for compute calls: requires a visible GPU."""
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("no GPU visible: the MI355X synthesis path has no CPU fallback")
+    return load_library()
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load_library().tts_last_error().decode(errors="replace")
+        if "attention norm" in msg:
+            raise RuntimeError("Unknown value for attention norm type")
+        raise RuntimeError(f"{what} failed (status {status}): {msg}")
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def tensor_views(tensors: dict):
+    """Build a TensorView array over CUDA tensors; returns (array, keepalive)."""
+    items = list(tensors.items())
+    arr = (TensorView * len(items))()
+    keep = []
+    for i, (k, t) in enumerate(items):
+        kb = k.encode()
+        keep.append(kb)
+        keep.append(t)
+        arr[i].key = kb
+        arr[i].data = t.data_ptr()
+        arr[i].numel = t.numel()
+    return arr, keep
+
+
+def i32_array(values):
+    vals = [int(v) for v in values]
+    return (ctypes.c_int32 * len(vals))(*vals)

@@ -1,0 +1,188 @@
+"""Drop-in for the inverse half of the reference ``AudioProcessor`` (utils/audio.py:11-201).
+
+``inv_mel_spectrogram`` / ``inv_spectrogram`` keep the reference signatures (numpy [n, T] in,
+numpy float64 waveform out) and run Griffin-Lim on the GPU through libtts_hip ``tts_gl_run``:
+denormalise -> dB->amp -> pinv(mel basis) -> ^power -> GL (librosa 0.6.2 stft/istft semantics)
+-> inverse pre-emphasis, all in HIP.  The initial phases are drawn on the host with
+``np.random.rand(*S.shape)`` exactly as utils/audio.py:183 does, so a caller that seeds numpy gets
+the same phases as the reference.  ``inv_mel_spectrogram_batch`` is the batched GPU-resident form
+(torch tensors in HBM, device-drawn phases) the batched/sharded synthesis uses.
+
+The mel filter bank is librosa 0.6.2 ``filters.mel`` (Slaney, area-normalised), restated in
+numpy because librosa is not installed; its pseudo-inverse is computed once in float64 on the
+host (utils/audio.py:64-66 recomputes it on every call).
+"""
+from __future__ import annotations
+
+import ctypes
+import io as _io
+
+import numpy as np
+import scipy.io.wavfile
+import scipy.signal
+import torch
+
+from . import _native
+
+
+def _hz_to_mel(f):
+    f = np.atleast_1d(np.asarray(f, dtype=np.float64))
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    mel = f / f_sp
+    hi = f >= min_log_hz
+    mel[hi] = min_log_mel + np.log(f[hi] / min_log_hz) / logstep
+    return mel
+
+
+def _mel_to_hz(m):
+    m = np.atleast_1d(np.asarray(m, dtype=np.float64))
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, np.log(6.4) / 27.0
+    f = f_sp * m
+    hi = m >= min_log_mel
+    f[hi] = min_log_hz * np.exp(logstep * (m[hi] - min_log_mel))
+    return f
+
+
+def mel_basis(sr, n_fft, n_mels, fmin=0.0, fmax=None):
+    """librosa 0.6.2 filters.mel(sr, n_fft, n_mels, fmin, fmax), htk=False, norm=1."""
+    fmax = float(sr) / 2 if fmax is None else fmax
+    bins = np.linspace(0, float(sr) / 2, 1 + n_fft // 2)
+    edges = _mel_to_hz(np.linspace(_hz_to_mel(fmin)[0], _hz_to_mel(fmax)[0], n_mels + 2))
+    lo, ce, hi = edges[:-2, None], edges[1:-1, None], edges[2:, None]
+    rise = (bins[None, :] - lo) / (ce - lo)
+    fall = (hi - bins[None, :]) / (hi - ce)
+    w = np.maximum(0.0, np.minimum(rise, fall))
+    return w * (2.0 / (edges[2:] - edges[:-2]))[:, None]
+
+
+class AudioProcessor:
+    def __init__(self, sample_rate=None, num_mels=None, min_level_db=None, frame_shift_ms=None,
+                 frame_length_ms=None, ref_level_db=None, num_freq=None, power=None, preemphasis=None,
+                 signal_norm=None, symmetric_norm=None, max_norm=None, mel_fmin=None, mel_fmax=None,
+                 clip_norm=True, griffin_lim_iters=None, do_trim_silence=False, **kwargs):
+        self.sample_rate = sample_rate
+        self.num_mels = num_mels
+        self.min_level_db = min_level_db
+        self.frame_shift_ms = frame_shift_ms
+        self.frame_length_ms = frame_length_ms
+        self.ref_level_db = ref_level_db
+        self.num_freq = num_freq
+        self.power = power
+        self.preemphasis = preemphasis
+        self.griffin_lim_iters = griffin_lim_iters
+        self.signal_norm = signal_norm
+        self.symmetric_norm = symmetric_norm
+        self.mel_fmin = 0 if mel_fmin is None else mel_fmin
+        self.mel_fmax = mel_fmax
+        self.max_norm = 1.0 if max_norm is None else float(max_norm)
+        self.clip_norm = clip_norm
+        self.do_trim_silence = do_trim_silence
+        self.n_fft, self.hop_length, self.win_length = self._stft_parameters()
+        self._gl = None
+
+    def _stft_parameters(self):  # utils/audio.py:114-119
+        n_fft = (self.num_freq - 1) * 2
+        hop_length = int(self.frame_shift_ms / 1000.0 * self.sample_rate)
+        win_length = int(self.frame_length_ms / 1000.0 * self.sample_rate)
+        return n_fft, hop_length, win_length
+
+    def _build_mel_basis(self):  # utils/audio.py:68-77
+        if self.mel_fmax is not None:
+            assert self.mel_fmax <= self.sample_rate // 2
+        return mel_basis(self.sample_rate, self.n_fft, self.num_mels, self.mel_fmin, self.mel_fmax)
+
+    # ---------------------------------------------------------------- host helpers (not hot)
+    def _denormalize(self, S):  # utils/audio.py:96-112
+        if not self.signal_norm:
+            return S
+        if self.symmetric_norm:
+            if self.clip_norm:
+                S = np.clip(S, -self.max_norm, self.max_norm)
+            return ((S + self.max_norm) * -self.min_level_db / (2 * self.max_norm)) + self.min_level_db
+        if self.clip_norm:
+            S = np.clip(S, 0, self.max_norm)
+        return (S * -self.min_level_db / self.max_norm) + self.min_level_db
+
+    def _db_to_amp(self, x):  # utils/audio.py:125-126
+        return np.power(10.0, x * 0.05)
+
+    def apply_inv_preemphasis(self, x):  # utils/audio.py:133-136
+        if self.preemphasis == 0:
+            raise RuntimeError(" !! Preemphasis is applied with factor 0.0. ")
+        return scipy.signal.lfilter([1], [1, -self.preemphasis], x)
+
+    def save_wav(self, wav, path):  # utils/audio.py:56-58
+        wav_norm = np.asarray(wav) * (32767 / max(0.01, np.max(np.abs(wav))))
+        scipy.io.wavfile.write(path, self.sample_rate, wav_norm.astype(np.int16))
+
+    # ---------------------------------------------------------------- GPU Griffin-Lim
+    def _handle(self):
+        if self._gl is None:
+            lib = _native.lib()
+            cfg = _native.AudioConfig(
+                n_fft=self.n_fft, hop_length=self.hop_length, win_length=self.win_length,
+                num_mels=self.num_mels, min_level_db=self.min_level_db, ref_level_db=self.ref_level_db,
+                power=self.power, max_norm=self.max_norm, preemphasis=float(self.preemphasis),
+                signal_norm=int(bool(self.signal_norm)), symmetric_norm=int(bool(self.symmetric_norm)),
+                clip_norm=int(bool(self.clip_norm)))
+            pinv = np.ascontiguousarray(np.linalg.pinv(self._build_mel_basis()), dtype=np.float32)
+            h = ctypes.c_void_p()
+            _native.check(lib.tts_gl_create(ctypes.byref(cfg), pinv.ctypes.data_as(ctypes.c_void_p),
+                                            _native.stream_handle(), ctypes.byref(h)), "tts_gl_create")
+            self._gl = (lib, h)
+        return self._gl
+
+    def __del__(self):
+        try:
+            if self._gl is not None:
+                self._gl[0].tts_gl_destroy(self._gl[1])
+        except Exception:
+            pass
+
+    def griffin_lim_batch(self, spec, frames, mode=_native.TTS_GL_FROM_MEL, phase_u=None, seed=0, iters=None):
+        """spec: CUDA fp32 [B, Fmax, n] (frame-major); frames: list of F_b.  Returns CUDA fp64
+        [B, hop*(Fmax-1)]; sentence b's waveform is the first hop*(F_b-1) samples."""
+        lib, h = self._handle()
+        iters = self.griffin_lim_iters if iters is None else iters
+        spec = spec.float().contiguous()
+        B, Fmax = spec.shape[0], spec.shape[1]
+        wav = torch.zeros(B, self.hop_length * (Fmax - 1), dtype=torch.float64, device=spec.device)
+        pu = None
+        if phase_u is not None:
+            pu = torch.as_tensor(phase_u, dtype=torch.float64).to(spec.device).contiguous()
+        _native.check(lib.tts_gl_run(h, mode, ctypes.c_void_p(spec.data_ptr()), _native.i32_array(frames), B, Fmax,
+                                     ctypes.c_void_p(pu.data_ptr()) if pu is not None else None, int(seed), int(iters),
+                                     ctypes.c_void_p(wav.data_ptr()), _native.stream_handle()), "tts_gl_run")
+        return wav
+
+    def inv_mel_spectrogram_batch(self, mel, frames, seed=0, phase_u=None):
+        return self.griffin_lim_batch(mel, frames, _native.TTS_GL_FROM_MEL, phase_u, seed)
+
+    def last_gl_timing(self):
+        lib, h = self._handle()
+        ms, n = ctypes.c_float(), ctypes.c_int()
+        lib.tts_gl_last_timing(h, ctypes.byref(ms), ctypes.byref(n))
+        return dict(gl_loop_ms=ms.value, gl_iterations=n.value)
+
+    def _single(self, spec_nT, mode):
+        self._handle()  # raises without a GPU / library: no CPU fallback
+        spec_nT = np.asarray(spec_nT, dtype=np.float32)
+        T = spec_nT.shape[1]
+        phase_u = np.random.rand(self.n_fft // 2 + 1, T)  # utils/audio.py:183 (unseeded, numpy global RNG)
+        spec = torch.from_numpy(np.ascontiguousarray(spec_nT.T)).cuda()[None]
+        wav = self.griffin_lim_batch(spec, [T], mode, phase_u[None])
+        return wav[0].cpu().numpy()
+
+    def inv_mel_spectrogram(self, mel_spectrogram):  # utils/audio.py:164-172
+        return self._single(mel_spectrogram, _native.TTS_GL_FROM_MEL)
+
+    def inv_spectrogram(self, spectrogram):  # utils/audio.py:154-162
+        return self._single(spectrogram, _native.TTS_GL_FROM_LINEAR)
+
+
+def wav_bytes(ap: AudioProcessor, wav) -> _io.BytesIO:
+    out = _io.BytesIO()
+    ap.save_wav(np.asarray(wav), out)
+    return out

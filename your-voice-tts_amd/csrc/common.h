@@ -1,0 +1,94 @@
+// Shared device/host helpers for libtts_hip (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/tts_hip.h"
+
+namespace tts {
+
+void set_error(const std::string& msg);
+tts_status hip_fail(hipError_t e, const char* what, const char* file, int line);
+
+#define TTS_HIP(call)                                                        \
+    do {                                                                     \
+        hipError_t _e = (call);                                              \
+        if (_e != hipSuccess) return ::tts::hip_fail(_e, #call, __FILE__, __LINE__); \
+    } while (0)
+
+#define TTS_CHECK(cond, code, msg)           \
+    do {                                             \
+        if (!(cond)) {                               \
+            ::tts::set_error(msg);                   \
+            return code;                             \
+        }                                            \
+    } while (0)
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int WAVE = 64;
+
+// v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];
+// D lane l holds C[(l>>4)*4 + r][l&15], r = 0..3.  Exact f32 fma chain.
+__device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+// (value, index) max with first-index tie break (torch.argmax / max(dim) semantics).
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float ov = __shfl_xor(v, o, 64);
+        int oi = __shfl_xor(i, o, 64);
+        if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+    }
+}
+
+// Block reductions; `scratch` must hold >= 2*nwaves entries; all threads get the result.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) scratch[w] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int k = 0; k < nw; ++k) s += scratch[k];  // fixed order: deterministic
+    return s;
+}
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    v = wave_max(v);
+    __syncthreads();
+    if (lane == 0) scratch[w] = v;
+    __syncthreads();
+    float s = scratch[0];
+    for (int k = 1; k < nw; ++k) s = fmaxf(s, scratch[k]);
+    return s;
+}
+__device__ __forceinline__ int block_argmax(float v, int i, float* scratch, int* iscratch) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    wave_argmax(v, i);
+    __syncthreads();
+    if (lane == 0) { scratch[w] = v; iscratch[w] = i; }
+    __syncthreads();
+    float bv = scratch[0];
+    int bi = iscratch[0];
+    for (int k = 1; k < nw; ++k)
+        if (scratch[k] > bv || (scratch[k] == bv && iscratch[k] < bi)) { bv = scratch[k]; bi = iscratch[k]; }
+    return bi;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+}  // namespace tts

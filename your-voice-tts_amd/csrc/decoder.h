@@ -1,0 +1,99 @@
+// Decoder-step state and the non-GEMM kernels of the step (attention, stop rule).
+#pragma once
+#include "common.h"
+
+namespace tts {
+
+constexpr int ENC = 512;   // encoder embedding dim (layers/tacotron2.py:104)
+constexpr int HATT = 1024; // attention_rnn_dim
+constexpr int HDEC = 1024; // decoder_rnn_dim
+constexpr int PRE = 256;   // prenet_dim
+constexpr int ADIM = 128;  // attention_dim
+constexpr int NLOC = 32;   // location filters
+constexpr int KLOC = 31;   // location kernel
+constexpr int XA = PRE + ENC;  // [prenet | ctx] row of the attention-LSTM input
+constexpr int ATT_THREADS = 512;
+
+// Flags (tts_decoder_config) + weights + device state pointers, passed by value.
+struct AttnArgs {
+    int attn_norm, forward_attn, trans_agent, forward_attn_mask, location_attn, windowing;
+    int Lcap;  // row stride of per-position arrays
+    int B;
+    // weights (reference layout)
+    const float* v;        // [128]
+    const float* v_b;      // [1]
+    const float* ta_w;     // [1536] = [ctx(512) | h_att(1024)]
+    const float* ta_b;     // [1]
+    const float* loc_conv; // [32][2][31]
+    const float* loc_dense;// [128][32]
+    // inputs
+    const float* q;        // [B][128] processed query
+    const float* Pt;       // [B][128][Lcap] processed inputs, transposed
+    const float* enc;      // [B][Lcap][512]
+    const int* lens;       // [B]
+    const float* h_att;    // ping-pong base [2][B][1024] (row of step parity)
+    int64_t h_pstride;
+    // state
+    float* alpha;          // [B][Lcap]
+    float* att_w;          // [B][Lcap]
+    float* att_cum;        // [B][Lcap]
+    float* u;              // [B]
+    int* win_idx;          // [B]
+    float* tail;           // [B] att_w[L-2] + att_w[L-1]
+    // outputs
+    float* xa;             // ping-pong base [2][B][768]; ctx goes to xa[(t+1)&1][b][256:]
+    int64_t xa_pstride;
+    float* align_hist;     // [B][hist_cap][Lalign] or null
+    int64_t align_ldb;     // stride per sentence
+    int Lalign;
+    int hist_cap;
+    const int* step;
+    const int* done;
+    const int* n_active;
+};
+
+struct StopArgs {
+    const float* w;      // stopnet weight [1024 + 80r]
+    const float* b;      // [1]
+    int nmel;            // 80*r
+    const float* h_dec;  // ping-pong base [2][B][1024]
+    int64_t h_pstride;
+    const float* mem;    // [B][nmel] this step's mel frame(s)
+    const int* lens;
+    const float* tail;
+    float* stop_hist;    // [B][hist_cap]
+    int64_t stop_ldb;
+    int hist_cap;
+    int max_steps;
+    int B;
+    int* flag1;
+    int* count;
+    int* done;
+    int* n_steps;
+    int* step;
+    int* n_active;
+};
+
+struct InitArgs {
+    int B, Lcap, nmel;
+    const int* lens;
+    const float* att_init;  // [1024]
+    const float* dec_init;  // [1024]
+    const float* go;        // [nmel]
+    float* h_att; int64_t h_pstride;
+    float* c_att;
+    float* h_dec;
+    float* c_dec;
+    float* xa; int64_t xa_pstride;
+    float* mem;
+    float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; float* tail;
+    int* flag1; int* count; int* done; int* n_steps; int* step; int* n_active;
+};
+
+hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
+hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s);
+hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
+hipError_t launch_stop(const StopArgs& a, hipStream_t s);
+size_t attention_smem_bytes(int Lcap, int location);
+
+}  // namespace tts

@@ -1,0 +1,472 @@
+// Host runtime of the decoder: weight repacking, workspace, hipGraph-captured step loop.
+//
+// One decoder step = 8 launches on the library's own stream (captured once per (B, Lmax)):
+//   prenet L1 (sgemm relu) -> prenet L2 (sgemm relu) -> attention LSTM (sgemm + LSTM epilogue)
+//   -> query (sgemm) -> attention (1 WG / sentence) -> decoder LSTM (sgemm + LSTM epilogue)
+//   -> mel projection (sgemm) -> stopnet + stop rule (1 WG).
+// The step index lives in device memory (advanced by the stop kernel), so the same graph is
+// replayed for every step; ping-pong activation buffers are selected by its parity.
+// The host synchronises only at chunk boundaries: the first chunk is the reference's lower
+// bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "decoder.h"
+#include "sgemm.h"
+
+using namespace tts;
+
+namespace {
+struct Graphs {
+    hipGraphExec_t one = nullptr, chunk = nullptr;
+};
+constexpr int CHUNK = 8;
+}  // namespace
+
+struct tts_decoder {
+    tts_decoder_config cfg{};
+    int nmel = 80;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+    std::vector<void*> allocs;
+    // packed GEMM weights + logical biases
+    float *W_pre1 = nullptr, *W_pre2 = nullptr, *W_att = nullptr, *b_att = nullptr, *W_q = nullptr;
+    float *W_dec = nullptr, *b_dec = nullptr, *W_mel = nullptr, *b_mel = nullptr;
+    // reference-layout small weights
+    float *v = nullptr, *v_b = nullptr, *ta_w = nullptr, *ta_b = nullptr, *loc_conv = nullptr, *loc_dense = nullptr;
+    float *W_in = nullptr, *stop_w = nullptr, *stop_b = nullptr, *att_init = nullptr, *dec_init = nullptr, *go = nullptr;
+    // workspace
+    int Lcap = 0, Bcap = 0, hist_cap = 0;
+    float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
+    float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr;
+    float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
+    int *lens = nullptr, *win_idx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
+    int *n_steps = nullptr, *step = nullptr, *n_active = nullptr;
+    float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
+    int align_L = 0;  // Lmax the align history is currently laid out for
+    int* host_flags = nullptr;  // pinned: [n_active, step]
+    std::map<std::pair<int, int>, Graphs> graphs;
+    float last_ms = 0.f;
+    int last_steps = 0;
+};
+
+namespace {
+
+template <typename T>
+tts_status dmalloc(tts_decoder* d, T** p, size_t n) {
+    void* q = nullptr;
+    TTS_HIP(hipMalloc(&q, n * sizeof(T) + 16));
+    d->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return TTS_OK;
+}
+
+struct WeightMap {
+    std::unordered_map<std::string, std::pair<const float*, int64_t>> m;
+    const float* get(const std::string& k, int64_t numel) const {
+        auto it = m.find(k);
+        if (it == m.end()) { set_error("missing weight " + k); return nullptr; }
+        if (it->second.second != numel) {
+            set_error("weight " + k + " has " + std::to_string(it->second.second) + " elements, expected " +
+                      std::to_string(numel));
+            return nullptr;
+        }
+        return it->second.first;
+    }
+};
+
+#define GETW(var, key, n)                                   \
+    const float* var = wm.get(key, n);                     \
+    if (!var) return TTS_ERR_INVALID;
+
+tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, hipStream_t s) {
+    tts_status st = dmalloc(d, dst, n);
+    if (st) return st;
+    TTS_HIP(hipMemcpyAsync(*dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    return TTS_OK;
+}
+
+tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
+    const int nmel = d->nmel;
+    const int64_t hps = (int64_t)d->Bcap * HATT;   // ping-pong stride of h buffers
+    const int64_t xps = (int64_t)d->Bcap * XA;
+    SGemmArgs g{};
+    g.B = B;
+    g.step = d->step;
+    g.done = d->done;
+    g.n_active = d->n_active;
+    g.out_par = -1;
+    // 1) prenet layer 1: relu(W1 . memory)   (common_layers.py:77-83; dropout off in eval)
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->mem, 0, -1, nmel, nmel};
+        a.nseg = 1;
+        a.W = d->W_pre1; a.K = nmel; a.N = PRE; a.act = ACT_RELU;
+        a.out = d->pre1; a.ldo = PRE;
+        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+    }
+    // 2) prenet layer 2 -> xa[t&1][b][0:256]
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->pre1, 0, -1, PRE, PRE};
+        a.nseg = 1;
+        a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
+        a.out = d->xa; a.out_pstride = xps; a.out_par = 0; a.ldo = XA;
+        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+    }
+    // 3) attention LSTM: x = [prenet | ctx_{t-1}] (xa[t&1]), h = h_att[(t+1)&1]  (tacotron2.py:195-197)
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->xa, xps, 0, XA, XA};
+        a.seg[1] = Seg{d->h_att, hps, 1, HATT, HATT};
+        a.nseg = 2;
+        a.W = d->W_att; a.K = XA + HATT; a.N = 4 * HATT; a.bias = d->b_att;
+        a.out = d->h_att; a.out_pstride = hps; a.out_par = 0; a.ldo = HATT;
+        a.cell = d->c_att; a.ldc = HATT;
+        TTS_HIP(sgemm_launch(a, EPI_LSTM, s));
+    }
+    // 4) processed query = query_layer(h_att)   (common_layers.py:170/179)
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->h_att, hps, 0, HATT, HATT};
+        a.nseg = 1;
+        a.W = d->W_q; a.K = HATT; a.N = ADIM;
+        a.out = d->q; a.ldo = ADIM;
+        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+    }
+    // 5) attention (energies, norm, forward attention, context)
+    {
+        AttnArgs a{};
+        const tts_decoder_config& c = d->cfg;
+        a.attn_norm = c.attn_norm; a.forward_attn = c.forward_attn; a.trans_agent = c.trans_agent;
+        a.forward_attn_mask = c.forward_attn_mask; a.location_attn = c.location_attn; a.windowing = c.windowing;
+        a.Lcap = d->Lcap; a.B = B;
+        a.v = d->v; a.v_b = d->v_b; a.ta_w = d->ta_w; a.ta_b = d->ta_b;
+        a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
+        a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
+        a.h_att = d->h_att; a.h_pstride = hps;
+        a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
+        a.tail = d->tail;
+        a.xa = d->xa; a.xa_pstride = xps;
+        a.align_hist = d->align_hist; a.align_ldb = (int64_t)d->hist_cap * Lmax; a.Lalign = Lmax;
+        a.hist_cap = d->hist_cap;
+        a.step = d->step; a.done = d->done; a.n_active = d->n_active;
+        TTS_HIP(launch_attention(a, s));
+    }
+    // 6) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec[(t+1)&1]   (tacotron2.py:206-208)
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->h_att, hps, 0, HATT, HATT};
+        a.seg[1] = Seg{d->xa + PRE, xps, 1, XA, ENC};
+        a.seg[2] = Seg{d->h_dec, hps, 1, HDEC, HDEC};
+        a.nseg = 3;
+        a.W = d->W_dec; a.K = HATT + ENC + HDEC; a.N = 4 * HDEC; a.bias = d->b_dec;
+        a.out = d->h_dec; a.out_pstride = hps; a.out_par = 0; a.ldo = HDEC;
+        a.cell = d->c_dec; a.ldc = HDEC;
+        TTS_HIP(sgemm_launch(a, EPI_LSTM, s));
+    }
+    // 7) mel = linear_projection([h_dec | ctx]) -> memory + history   (tacotron2.py:214-217)
+    {
+        SGemmArgs a = g;
+        a.seg[0] = Seg{d->h_dec, hps, 0, HDEC, HDEC};
+        a.seg[1] = Seg{d->xa + PRE, xps, 1, XA, ENC};
+        a.nseg = 2;
+        a.W = d->W_mel; a.K = HDEC + ENC; a.N = nmel; a.bias = d->b_mel;
+        a.out = d->mem; a.ldo = nmel;
+        a.hist = d->mel_hist; a.ldh = (int64_t)d->hist_cap * nmel; a.hist_cap = d->hist_cap;
+        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+    }
+    // 8) stopnet + stop rule + step advance
+    {
+        StopArgs a{};
+        a.w = d->stop_w; a.b = d->stop_b; a.nmel = nmel;
+        a.h_dec = d->h_dec; a.h_pstride = hps; a.mem = d->mem; a.lens = d->lens; a.tail = d->tail;
+        a.stop_hist = d->stop_hist; a.stop_ldb = d->hist_cap; a.hist_cap = d->hist_cap;
+        a.max_steps = 0;  // patched below through the device copy of the cap
+        a.B = B;
+        a.flag1 = d->flag1; a.count = d->count; a.done = d->done; a.n_steps = d->n_steps;
+        a.step = d->step; a.n_active = d->n_active;
+        a.max_steps = d->cfg.max_steps;  // replaced per run via graph key (see below)
+        TTS_HIP(launch_stop(a, s));
+    }
+    return TTS_OK;
+}
+
+tts_status build_graph(tts_decoder* d, int B, int Lmax, int steps, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    TTS_HIP(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+    tts_status st = TTS_OK;
+    for (int i = 0; i < steps && st == TTS_OK; ++i) st = enqueue_step(d, B, Lmax, d->stream);
+    hipError_t e = hipStreamEndCapture(d->stream, &g);
+    if (st) return st;
+    TTS_HIP(e);
+    TTS_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    TTS_HIP(hipGraphDestroy(g));
+    return TTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* tensors, int n_tensors, void* stream,
+                              tts_decoder** out) {
+    TTS_CHECK(cfg && out && (tensors || n_tensors == 0), TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(cfg->r >= 1 && cfg->r <= 8, TTS_ERR_INVALID, "r must be in [1, 8]");
+    TTS_CHECK(cfg->max_batch >= 1 && cfg->max_batch <= 64, TTS_ERR_UNSUPPORTED, "max_batch must be in [1, 64]");
+    TTS_CHECK(cfg->max_len >= 2 && cfg->max_len <= (cfg->location_attn ? 512 : 1024), TTS_ERR_UNSUPPORTED,
+              "max_len must be in [2, 1024] (512 with location attention)");
+    TTS_CHECK(cfg->max_steps >= 1, TTS_ERR_INVALID, "max_steps must be >= 1");
+    TTS_CHECK(cfg->attn_norm == 0 || cfg->attn_norm == 1, TTS_ERR_INVALID, "Unknown value for attention norm type");
+    auto* d = new tts_decoder();
+    d->cfg = *cfg;
+    d->nmel = 80 * cfg->r;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    tts_status st = TTS_OK;
+    auto fail = [&](tts_status code) { tts_decoder_destroy(d); return code; };
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_out, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&d->ev_t0) != hipSuccess || hipEventCreate(&d->ev_t1) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), 4 * sizeof(int)) != hipSuccess) {
+        set_error("stream/event creation failed");
+        return fail(TTS_ERR_HIP);
+    }
+    WeightMap wm;
+    for (int i = 0; i < n_tensors; ++i) wm.m[tensors[i].key] = {tensors[i].data, tensors[i].numel};
+    const int nmel = d->nmel;
+#define GW(var, key, n)                        \
+    const float* var = wm.get(key, n);         \
+    if (!var) return fail(TTS_ERR_INVALID);
+    GW(pre0, "decoder.prenet.layers.0.linear_layer.weight", (int64_t)PRE * nmel);
+    GW(pre1, "decoder.prenet.layers.1.linear_layer.weight", (int64_t)PRE * PRE);
+    GW(a_wih, "decoder.attention_rnn.weight_ih", (int64_t)4 * HATT * XA);
+    GW(a_whh, "decoder.attention_rnn.weight_hh", (int64_t)4 * HATT * HATT);
+    GW(a_bih, "decoder.attention_rnn.bias_ih", 4 * HATT);
+    GW(a_bhh, "decoder.attention_rnn.bias_hh", 4 * HATT);
+    GW(wq, "decoder.attention_layer.query_layer.linear_layer.weight", (int64_t)ADIM * HATT);
+    GW(win, "decoder.attention_layer.inputs_layer.linear_layer.weight", (int64_t)ADIM * ENC);
+    GW(vw, "decoder.attention_layer.v.linear_layer.weight", ADIM);
+    GW(vb, "decoder.attention_layer.v.linear_layer.bias", 1);
+    GW(d_wih, "decoder.decoder_rnn.weight_ih", (int64_t)4 * HDEC * (HATT + ENC));
+    GW(d_whh, "decoder.decoder_rnn.weight_hh", (int64_t)4 * HDEC * HDEC);
+    GW(d_bih, "decoder.decoder_rnn.bias_ih", 4 * HDEC);
+    GW(d_bhh, "decoder.decoder_rnn.bias_hh", 4 * HDEC);
+    GW(pw, "decoder.linear_projection.linear_layer.weight", (int64_t)nmel * (HDEC + ENC));
+    GW(pb, "decoder.linear_projection.linear_layer.bias", nmel);
+    GW(sw, "decoder.stopnet.1.linear_layer.weight", HDEC + nmel);
+    GW(sb, "decoder.stopnet.1.linear_layer.bias", 1);
+    GW(ainit, "decoder.attention_rnn_init.weight", HATT);
+    GW(goinit, "decoder.go_frame_init.weight", nmel);
+    GW(dinit, "decoder.decoder_rnn_inits.weight", HDEC);
+    const float *taw = nullptr, *tab = nullptr, *lcw = nullptr, *ldw = nullptr;
+    if (cfg->trans_agent) {
+        TTS_CHECK(cfg->forward_attn, TTS_ERR_INVALID, "trans_agent requires forward_attn");
+        taw = wm.get("decoder.attention_layer.ta.weight", HATT + ENC);
+        tab = wm.get("decoder.attention_layer.ta.bias", 1);
+        if (!taw || !tab) return fail(TTS_ERR_INVALID);
+    }
+    if (cfg->location_attn) {
+        lcw = wm.get("decoder.attention_layer.location_layer.location_conv.weight", NLOC * 2 * KLOC);
+        ldw = wm.get("decoder.attention_layer.location_layer.location_dense.linear_layer.weight", ADIM * NLOC);
+        if (!lcw || !ldw) return fail(TTS_ERR_INVALID);
+    }
+#undef GW
+#define CK(x)                              \
+    do {                                   \
+        st = (x);                          \
+        if (st) return fail(st);           \
+    } while (0)
+#define HK(x)                                                            \
+    do {                                                                 \
+        hipError_t _e = (x);                                             \
+        if (_e != hipSuccess) return fail(hip_fail(_e, #x, __FILE__, __LINE__)); \
+    } while (0)
+    // packed GEMM weights
+    CK(dmalloc(d, &d->W_pre1, sgemm_packed_floats(PRE, nmel)));
+    HK(sgemm_pack(pre0, nmel, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre1, s));
+    CK(dmalloc(d, &d->W_pre2, sgemm_packed_floats(PRE, PRE)));
+    HK(sgemm_pack(pre1, PRE, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre2, s));
+    CK(dmalloc(d, &d->W_att, sgemm_packed_floats(4 * HATT, XA + HATT)));
+    HK(sgemm_pack(a_wih, XA, a_whh, HATT, 4 * HATT, ROWMAP_LSTM, HATT, d->W_att, s));
+    CK(dmalloc(d, &d->b_att, 4 * HATT));
+    HK(sgemm_pack_bias(a_bih, a_bhh, 4 * HATT, ROWMAP_LSTM, HATT, d->b_att, s));
+    CK(dmalloc(d, &d->W_q, sgemm_packed_floats(ADIM, HATT)));
+    HK(sgemm_pack(wq, HATT, nullptr, 0, ADIM, ROWMAP_IDENTITY, 0, d->W_q, s));
+    CK(dmalloc(d, &d->W_dec, sgemm_packed_floats(4 * HDEC, HATT + ENC + HDEC)));
+    HK(sgemm_pack(d_wih, HATT + ENC, d_whh, HDEC, 4 * HDEC, ROWMAP_LSTM, HDEC, d->W_dec, s));
+    CK(dmalloc(d, &d->b_dec, 4 * HDEC));
+    HK(sgemm_pack_bias(d_bih, d_bhh, 4 * HDEC, ROWMAP_LSTM, HDEC, d->b_dec, s));
+    CK(dmalloc(d, &d->W_mel, sgemm_packed_floats(nmel, HDEC + ENC)));
+    HK(sgemm_pack(pw, HDEC + ENC, nullptr, 0, nmel, ROWMAP_IDENTITY, 0, d->W_mel, s));
+    CK(dmalloc(d, &d->b_mel, (nmel + 15) / 16 * 16));
+    HK(sgemm_pack_bias(pb, nullptr, nmel, ROWMAP_IDENTITY, 0, d->b_mel, s));
+    // small weights in reference layout
+    CK(copy_weight(d, &d->v, vw, ADIM, s));
+    CK(copy_weight(d, &d->v_b, vb, 1, s));
+    CK(copy_weight(d, &d->W_in, win, (size_t)ADIM * ENC, s));
+    CK(copy_weight(d, &d->stop_w, sw, HDEC + nmel, s));
+    CK(copy_weight(d, &d->stop_b, sb, 1, s));
+    CK(copy_weight(d, &d->att_init, ainit, HATT, s));
+    CK(copy_weight(d, &d->dec_init, dinit, HDEC, s));
+    CK(copy_weight(d, &d->go, goinit, nmel, s));
+    if (taw) {
+        CK(copy_weight(d, &d->ta_w, taw, HATT + ENC, s));
+        CK(copy_weight(d, &d->ta_b, tab, 1, s));
+    }
+    if (lcw) {
+        CK(copy_weight(d, &d->loc_conv, lcw, NLOC * 2 * KLOC, s));
+        CK(copy_weight(d, &d->loc_dense, ldw, ADIM * NLOC, s));
+    }
+    // workspace
+    const int Bc = cfg->max_batch, Lc = (cfg->max_len + 3) / 4 * 4;
+    d->Bcap = Bc;
+    d->Lcap = Lc;
+    d->hist_cap = cfg->max_steps + 21;
+    CK(dmalloc(d, &d->enc, (size_t)Bc * Lc * ENC));
+    CK(dmalloc(d, &d->Pt, (size_t)Bc * ADIM * Lc));
+    CK(dmalloc(d, &d->h_att, (size_t)2 * Bc * HATT));
+    CK(dmalloc(d, &d->c_att, (size_t)Bc * HATT));
+    CK(dmalloc(d, &d->h_dec, (size_t)2 * Bc * HDEC));
+    CK(dmalloc(d, &d->c_dec, (size_t)Bc * HDEC));
+    CK(dmalloc(d, &d->xa, (size_t)2 * Bc * XA));
+    CK(dmalloc(d, &d->mem, (size_t)Bc * nmel));
+    CK(dmalloc(d, &d->pre1, (size_t)Bc * PRE));
+    CK(dmalloc(d, &d->q, (size_t)Bc * ADIM));
+    CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
+    CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
+    CK(dmalloc(d, &d->att_cum, (size_t)Bc * Lc));
+    CK(dmalloc(d, &d->u, Bc));
+    CK(dmalloc(d, &d->tail, Bc));
+    CK(dmalloc(d, &d->lens, Bc));
+    CK(dmalloc(d, &d->win_idx, Bc));
+    CK(dmalloc(d, &d->flag1, Bc));
+    CK(dmalloc(d, &d->count, Bc));
+    CK(dmalloc(d, &d->done, Bc));
+    CK(dmalloc(d, &d->n_steps, Bc));
+    CK(dmalloc(d, &d->step, 4));
+    CK(dmalloc(d, &d->n_active, 4));
+    CK(dmalloc(d, &d->mel_hist, (size_t)Bc * d->hist_cap * nmel));
+    CK(dmalloc(d, &d->stop_hist, (size_t)Bc * d->hist_cap));
+    CK(dmalloc(d, &d->align_hist, (size_t)Bc * d->hist_cap * Lc));
+    HK(hipMemsetAsync(d->xa, 0, sizeof(float) * 2 * Bc * XA, s));
+    HK(hipMemsetAsync(d->h_att, 0, sizeof(float) * 2 * Bc * HATT, s));
+    HK(hipMemsetAsync(d->h_dec, 0, sizeof(float) * 2 * Bc * HDEC, s));
+    HK(hipMemsetAsync(d->mem, 0, sizeof(float) * Bc * nmel, s));
+    HK(hipMemsetAsync(d->enc, 0, sizeof(float) * Bc * Lc * ENC, s));
+    HK(hipMemsetAsync(d->Pt, 0, sizeof(float) * Bc * ADIM * Lc, s));
+    HK(hipStreamSynchronize(s));
+#undef CK
+#undef HK
+    *out = d;
+    return TTS_OK;
+}
+
+void tts_decoder_destroy(tts_decoder* d) {
+    if (!d) return;
+    if (d->stream) (void)hipStreamSynchronize(d->stream);
+    for (auto& kv : d->graphs) {
+        if (kv.second.one) (void)hipGraphExecDestroy(kv.second.one);
+        if (kv.second.chunk) (void)hipGraphExecDestroy(kv.second.chunk);
+    }
+    for (void* p : d->allocs) (void)hipFree(p);
+    if (d->host_flags) (void)hipHostFree(d->host_flags);
+    if (d->ev_in) (void)hipEventDestroy(d->ev_in);
+    if (d->ev_out) (void)hipEventDestroy(d->ev_out);
+    if (d->ev_t0) (void)hipEventDestroy(d->ev_t0);
+    if (d->ev_t1) (void)hipEventDestroy(d->ev_t1);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax, int max_steps,
+                           int steps_cap, float* mel, float* stop, float* align, int32_t* n_steps, void* stream) {
+    TTS_CHECK(d && enc && lens && mel && stop && n_steps, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(B >= 1 && B <= d->Bcap, TTS_ERR_INVALID, "batch exceeds decoder capacity");
+    TTS_CHECK(Lmax >= 2 && Lmax <= d->Lcap, TTS_ERR_INVALID, "Lmax exceeds decoder capacity");
+    TTS_CHECK(max_steps >= 1 && max_steps <= d->cfg.max_steps, TTS_ERR_INVALID, "max_steps exceeds decoder capacity");
+    TTS_CHECK(steps_cap >= max_steps + 20, TTS_ERR_INVALID, "steps_cap must be >= max_steps + 20");
+    int first = 0;
+    for (int b = 0; b < B; ++b) {
+        TTS_CHECK(lens[b] >= 2 && lens[b] <= Lmax, TTS_ERR_INVALID, "encoder length out of range [2, Lmax]");
+        const int lb = std::min(2 * lens[b] + 22, max_steps);
+        first = std::max(first, lb);
+    }
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t s = d->stream;
+    TTS_HIP(hipEventRecord(d->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(s, d->ev_in, 0));
+    TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4, B,
+                             hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    TTS_HIP(launch_project_inputs(d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
+    InitArgs ia{};
+    ia.B = B; ia.Lcap = d->Lcap; ia.nmel = d->nmel; ia.lens = d->lens;
+    ia.att_init = d->att_init; ia.dec_init = d->dec_init; ia.go = d->go;
+    ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
+    ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
+    ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
+    ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
+    ia.step = d->step; ia.n_active = d->n_active;
+    TTS_HIP(launch_decoder_init(ia, s));
+    // graphs for this (B, Lmax); max_steps is baked into the stop kernel args -> part of the key
+    const int saved_cap = d->cfg.max_steps;
+    d->cfg.max_steps = max_steps;
+    auto key = std::make_pair(B * 1000003 + max_steps, Lmax);
+    auto it = d->graphs.find(key);
+    if (it == d->graphs.end()) {
+        Graphs g;
+        tts_status st = build_graph(d, B, Lmax, 1, &g.one);
+        if (!st) st = build_graph(d, B, Lmax, CHUNK, &g.chunk);
+        if (st) { d->cfg.max_steps = saved_cap; return st; }
+        it = d->graphs.emplace(key, g).first;
+    }
+    d->cfg.max_steps = saved_cap;
+    const Graphs& g = it->second;
+    TTS_HIP(hipEventRecord(d->ev_t0, s));
+    int run = 0;
+    auto launch_steps = [&](int n) -> tts_status {
+        for (; n >= CHUNK; n -= CHUNK, run += CHUNK) TTS_HIP(hipGraphLaunch(g.chunk, s));
+        for (; n > 0; --n, ++run) TTS_HIP(hipGraphLaunch(g.one, s));
+        return TTS_OK;
+    };
+    tts_status st = launch_steps(first);
+    if (st) return st;
+    for (;;) {
+        TTS_HIP(hipMemcpyAsync(d->host_flags, d->n_active, sizeof(int), hipMemcpyDeviceToHost, s));
+        TTS_HIP(hipStreamSynchronize(s));
+        if (d->host_flags[0] == 0) break;
+        TTS_CHECK(run < max_steps + 20, TTS_ERR_HIP, "decoder did not stop within max_steps + 20 (internal error)");
+        st = launch_steps(CHUNK);
+        if (st) return st;
+    }
+    TTS_HIP(hipEventRecord(d->ev_t1, s));
+    TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipStreamSynchronize(s));
+    int nmax = 0;
+    for (int b = 0; b < B; ++b) nmax = std::max(nmax, (int)n_steps[b]);
+    const size_t nm = d->nmel;
+    TTS_HIP(hipMemcpy2DAsync(mel, (size_t)steps_cap * nm * 4, d->mel_hist, (size_t)d->hist_cap * nm * 4,
+                             (size_t)nmax * nm * 4, B, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipMemcpy2DAsync(stop, (size_t)steps_cap * 4, d->stop_hist, (size_t)d->hist_cap * 4, (size_t)nmax * 4, B,
+                             hipMemcpyDeviceToDevice, s));
+    if (align)
+        TTS_HIP(hipMemcpy2DAsync(align, (size_t)steps_cap * Lmax * 4, d->align_hist, (size_t)d->hist_cap * Lmax * 4,
+                                 (size_t)nmax * Lmax * 4, B, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipEventRecord(d->ev_out, s));
+    TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
+    TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
+    d->last_steps = run;
+    return TTS_OK;
+}
+
+tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run) {
+    TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
+    *loop_ms = d->last_ms;
+    *steps_run = d->last_steps;
+    return TTS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+"""Callers of the synthesis path: ``synthesis`` (utils/synthesis.py:78-124), ``tts``
+(synthesize.py:15-38) and ``Synthesizer`` (server/synthesizer.py:22-162), plus the batched
+GPU-resident pipeline they share.
+
+The text front-end (phonemizer/espeak, utils/text/) is outside the MI355X path and its
+dependencies are not installed here: callers pass character/phoneme ids, or give
+``Synthesizer`` an ``input_adapter`` (the reference builds one at server/synthesizer.py:51-54).
+"""
+from __future__ import annotations
+
+import io
+import re
+import time
+
+import numpy as np
+import torch
+
+from .audio import AudioProcessor
+
+# ------------------------------------------------------------------ sentence splitting
+# server/synthesizer.py:12-17, 102-126 (regex pipeline restated)
+_ALPHA = "([A-Za-z])"
+_PREFIXES = "(Mr|St|Mrs|Ms|Dr)[.]"
+_SUFFIXES = "(Inc|Ltd|Jr|Sr|Co)"
+_STARTERS = r"(Mr|Mrs|Ms|Dr|He\s|She\s|It\s|They\s|Their\s|Our\s|We\s|But\s|However\s|That\s|This\s|Wherever)"
+_ACRONYMS = "([A-Z][.][A-Z][.](?:[A-Z][.])?)"
+_WEBSITES = "[.](com|net|org|io|gov)"
+
+
+def split_into_sentences(text: str):
+    t = " " + text + "  "
+    t = t.replace("\n", " ")
+    t = re.sub(_PREFIXES, "\\1<prd>", t)
+    t = re.sub(_WEBSITES, "<prd>\\1", t)
+    if "Ph.D" in t:
+        t = t.replace("Ph.D.", "Ph<prd>D<prd>")
+    t = re.sub(r"\s" + _ALPHA + "[.] ", " \\1<prd> ", t)
+    t = re.sub(_ACRONYMS + " " + _STARTERS, "\\1<stop> \\2", t)
+    t = re.sub(_ALPHA + "[.]" + _ALPHA + "[.]" + _ALPHA + "[.]", "\\1<prd>\\2<prd>\\3<prd>", t)
+    t = re.sub(_ALPHA + "[.]" + _ALPHA + "[.]", "\\1<prd>\\2<prd>", t)
+    t = re.sub(" " + _SUFFIXES + "[.] " + _STARTERS, " \\1<stop> \\2", t)
+    t = re.sub(" " + _SUFFIXES + "[.]", " \\1<prd>", t)
+    t = re.sub(" " + _ALPHA + "[.]", " \\1<prd>", t)
+    if "”" in t:
+        t = t.replace(".”", "”.")
+    if '"' in t:
+        t = t.replace('."', '".')
+    if "!" in t:
+        t = t.replace('!"', '"!')
+    if "?" in t:
+        t = t.replace('?"', '"?')
+    t = t.replace(".", ".<stop>").replace("?", "?<stop>").replace("!", "!<stop>").replace("<prd>", ".")
+    return [s.strip() for s in t.split("<stop>")[:-1]]
+
+
+def wav_to_int16(wav):
+    """save_wav's conversion (utils/audio.py:56-58): peak-normalise to 32767, truncate to int16."""
+    wav = np.asarray(wav)
+    return (wav * (32767 / max(0.01, np.max(np.abs(wav))))).astype(np.int16)
+
+
+# ------------------------------------------------------------------ batched pipeline
+@torch.no_grad()
+def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed=0, phase="device",
+                     iters=None, keep_outputs=False):
+    """ids -> encoder -> HIP decoder -> HIP postnet -> HIP Griffin-Lim for a ragged batch.
+
+    phase: "device" draws the initial GL phases on the GPU from ``seed``; "numpy" draws them
+    sentence by sentence with np.random.rand(1025, T_b) in batch order, as the reference does
+    when it synthesises the sentences one after another.  Returns (wavs: list of float64 numpy
+    arrays, info dict)."""
+    out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
+    frames = out["frames"]
+    mel_post = out["mel_post"]
+    phase_u = None
+    if phase == "numpy":
+        Fmax = mel_post.shape[1]
+        phase_u = np.zeros((len(frames), ap.n_fft // 2 + 1, Fmax))
+        for b, T in enumerate(frames):
+            phase_u[b, :, :T] = np.random.rand(ap.n_fft // 2 + 1, T)
+    wav = ap.griffin_lim_batch(mel_post, frames, phase_u=phase_u, seed=seed, iters=iters)
+    lens = [ap.hop_length * (T - 1) for T in frames]
+    info = dict(frames=frames, steps=out["steps"], samples=lens, **model.last_timing, **ap.last_gl_timing())
+    if keep_outputs:
+        info.update(out)
+        info["wav_dev"] = wav
+    wav_h = wav.cpu().numpy()
+    return [wav_h[b, :n] for b, n in enumerate(lens)], info
+
+
+# ------------------------------------------------------------------ reference call sites
+def _ids_tensor(text, CONFIG):
+    if isinstance(text, str):
+        raise NotImplementedError(
+            "text front-end (phonemizer/espeak, utils/text) is outside the MI355X path: pass ids "
+            "(e.g. from the reference's phoneme_to_sequence) instead of a string")
+    return torch.as_tensor(np.asarray(text), dtype=torch.long).view(1, -1)
+
+
+def synthesis(model, text, CONFIG, use_cuda, ap, speaker_id=None, style_wav=None, truncated=False,
+              enable_eos_bos_chars=False, trim_silence=False):
+    """utils/synthesis.py:78-124 (Tacotron2 path): returns
+    (wav, alignment [T,L], decoder_output [T,80], postnet_output [T,80], stop_tokens [1,T,1])."""
+    if truncated:
+        return model.inference_truncated(_ids_tensor(text, CONFIG))
+    if style_wav is not None and CONFIG.model == "TacotronGST":
+        raise NotImplementedError("TacotronGST (SURVEY config 5) is not yet on the MI355X path")
+    inputs = _ids_tensor(text, CONFIG)
+    sid = None if speaker_id is None or speaker_id is False else torch.as_tensor([speaker_id])
+    decoder_output, postnet_output, alignments, stop_tokens = model.inference(inputs, speaker_ids=sid)
+    postnet_output = postnet_output[0].cpu().numpy()  # parse_outputs (utils/synthesis.py:52-56)
+    decoder_output = decoder_output[0].cpu().numpy()
+    alignment = alignments[0].cpu().numpy()
+    if CONFIG.model in ("Tacotron", "TacotronGST"):
+        wav = ap.inv_spectrogram(postnet_output.T)
+    else:
+        wav = ap.inv_mel_spectrogram(postnet_output.T)
+    if trim_silence:
+        raise NotImplementedError("trim_silence needs AudioProcessor.find_endpoint (not on the path)")
+    return wav, alignment, decoder_output, postnet_output, stop_tokens
+
+
+def tts(model, vocoder_model, C, VC, text, ap, use_cuda, batched_vocoder, figures=False):
+    """synthesize.py:15-38 with the GL vocoder (WaveRNN is an external repo, not vendored)."""
+    if vocoder_model is not None:
+        raise NotImplementedError("WaveRNN vocoder is not part of the reference tree")
+    t_1 = time.time()
+    waveform, alignment, decoder_outputs, postnet_output, stop_tokens = synthesis(
+        model, text, C, use_cuda, ap, None, None, False, C.enable_eos_bos_chars)
+    print(" >  Run-time: {}".format(time.time() - t_1))
+    return alignment, postnet_output, stop_tokens, waveform
+
+
+class Synthesizer:
+    """server/synthesizer.py:22-162 without file loading: give it a built model, an
+    AudioProcessor, the tts config and an input_adapter (sentence -> ids).  All sentences of a
+    request are synthesised as one GPU batch instead of one after another."""
+
+    def __init__(self, tts_model, ap, tts_config, input_adapter=None, seed=0):
+        self.tts_model = tts_model
+        self.ap = ap
+        self.tts_config = tts_config
+        self.input_adapter = input_adapter
+        self.seed = seed
+        self.tts_model.eval()
+        self.tts_model.decoder.max_decoder_steps = 3000  # server/synthesizer.py:66
+
+    def split_into_sentences(self, text):
+        return split_into_sentences(text)
+
+    def save_wav(self, wav, path):
+        self.ap.save_wav(np.array(wav), path)
+
+    def tts(self, text):
+        sens = self.split_into_sentences(text)
+        if len(sens) == 0:
+            sens = [text + "."]
+        sens = [s.strip() for s in sens if len(s) >= 3]  # server/synthesizer.py:134-136
+        if self.input_adapter is None:
+            raise NotImplementedError("Synthesizer needs an input_adapter (text front-end is off the path)")
+        ids = [np.asarray(self.input_adapter(s)) for s in sens]
+        wavs = []
+        if ids:
+            outs, _ = synthesize_batch(self.tts_model, self.ap, ids, seed=self.seed, phase="numpy")
+            for w in outs:
+                wavs += list(w)
+                wavs += [0] * 10000  # server/synthesizer.py:158
+        out = io.BytesIO()
+        self.save_wav(wavs, out)
+        return out

@@ -1,0 +1,268 @@
+"""Drop-in for the reference ``Tacotron2`` (models/tacotron2.py:11-100) on MI355X.
+
+Same constructor arguments, same ``state_dict`` keys and shapes (so reference checkpoints load
+with ``load_state_dict(cp['model'])``), same ``inference(text, speaker_ids)`` return tuple
+``(mel [B,T,80], mel_post [B,T,80], align [B,T,L], stop [B,T,1])``.
+
+Where the compute runs:
+  * decoder loop (``Decoder.inference``, layers/tacotron2.py:249-285): libtts_hip
+    ``tts_decoder_run`` — HIP kernels, hipGraph-replayed steps;
+  * Postnet + residual (layers/tacotron2.py:30-45, models/tacotron2.py:69-70): libtts_hip
+    ``tts_postnet_run`` — fp32 MFMA implicit-GEMM convolutions;
+  * embedding + encoder (layers/tacotron2.py:78-83): PyTorch-ROCm ops on the GPU for now
+    (SURVEY 8(f) row 1 moves it to HIP).
+There is no CPU path: without a GPU or without libtts_hip.so, ``inference`` raises.
+
+Batches: the reference decoder is batch-1 (its stop rule reads item 0,
+layers/tacotron2.py:268).  Here every sentence of a batch gets exactly the outputs it would get
+alone; ``inference_batch`` takes ragged id lists, ``inference`` a [B, L] tensor.
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _native, weights
+
+
+class _DecoderAttrs:
+    """Mutable attributes callers set on ``model.decoder`` (e.g. server/synthesizer.py:66)."""
+
+    def __init__(self, r):
+        self.max_decoder_steps = 1000  # layers/tacotron2.py:109
+        self.r = r
+
+
+class Tacotron2:
+    def __init__(self, num_chars, num_speakers=0, r=1, attn_win=False, attn_norm="softmax",
+                 prenet_type="original", prenet_dropout=True, forward_attn=False, trans_agent=False,
+                 forward_attn_mask=False, location_attn=True, separate_stopnet=True,
+                 max_batch=64, max_len=256, seed=0):
+        if prenet_type != "original":
+            raise NotImplementedError("prenet_type 'bn' is not on the MI355X path (no BASELINE config uses it)")
+        if attn_norm not in ("softmax", "sigmoid"):
+            raise RuntimeError("Unknown value for attention norm type")
+        self.num_chars = num_chars
+        self.num_speakers = num_speakers
+        self.n_mel_channels = 80
+        self.n_frames_per_step = r
+        self.flags = dict(r=r, attn_norm=attn_norm, forward_attn=bool(forward_attn),
+                          trans_agent=bool(trans_agent), forward_attn_mask=bool(forward_attn_mask),
+                          location_attn=bool(location_attn), attn_win=bool(attn_win))
+        self.separate_stopnet = separate_stopnet  # training-only flag (stopnet input detach)
+        self.decoder = _DecoderAttrs(r)
+        self.max_batch = max_batch
+        self.max_len = max_len
+        self.training = False
+        self.device = torch.device("cpu")
+        self._spec = weights.tacotron2_spec(num_chars, num_speakers, r, location_attn, trans_agent)
+        self._params = OrderedDict(
+            (k, torch.from_numpy(v)) for k, v in weights.generate(self._spec, seed).items())
+        self._native = None  # (decoder handle, postnet handle, key)
+        self.last_lengths = None
+        self.last_timing = {}
+
+    # ------------------------------------------------------------------ module-like surface
+    def state_dict(self):
+        return OrderedDict((k, v) for k, v in self._params.items())
+
+    def load_state_dict(self, sd, strict=True):
+        want = {k: tuple(s) for k, s, _ in self._spec}
+        missing = [k for k in want if k not in sd]
+        unexpected = [k for k in sd if k not in want]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Error(s) in loading state_dict for Tacotron2: missing {missing}, "
+                               f"unexpected {unexpected}")
+        for k in want:
+            if k not in sd:
+                continue
+            v = sd[k]
+            v = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            if tuple(v.shape) != want[k]:
+                raise RuntimeError(f"size mismatch for {k}: copying a param with shape {tuple(v.shape)}, "
+                                   f"the shape in current model is {want[k]}")
+            self._params[k] = v.detach().to(self.device, dtype=self._params[k].dtype).contiguous()
+        self._drop_native()
+        return self
+
+    def parameters(self):
+        return [v for k, v in self._params.items() if v.is_floating_point()]
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("training is out of scope for the MI355X synthesis path")
+        return self.eval()
+
+    def to(self, device):
+        self.device = torch.device(device)
+        self._params = OrderedDict((k, v.to(self.device)) for k, v in self._params.items())
+        self._drop_native()
+        return self
+
+    def cuda(self):
+        return self.to("cuda")
+
+    def cpu(self):
+        return self.to("cpu")
+
+    def _drop_native(self):
+        self._lstm = None
+        if self._native is not None:
+            lib = _native.load_library()
+            lib.tts_decoder_destroy(self._native[0])
+            lib.tts_postnet_destroy(self._native[1])
+            self._native = None
+
+    def __del__(self):
+        try:
+            self._drop_native()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ native handles
+    def _handles(self, Lmax, B):
+        lib = _native.lib()
+        if self.device.type != "cuda":
+            self.cuda()
+        max_steps = int(self.decoder.max_decoder_steps)
+        key = (max_steps, max(self.max_len, Lmax), max(self.max_batch, B))
+        if self._native is not None and (self._native[2][0] != max_steps or self._native[2][1] < Lmax
+                                         or self._native[2][2] < B):
+            self._drop_native()
+        if self._native is None:
+            f = self.flags
+            cfg = _native.DecoderConfig(r=f["r"], attn_norm=0 if f["attn_norm"] == "softmax" else 1,
+                                        forward_attn=int(f["forward_attn"]), trans_agent=int(f["trans_agent"]),
+                                        forward_attn_mask=int(f["forward_attn_mask"]),
+                                        location_attn=int(f["location_attn"]), windowing=int(f["attn_win"]),
+                                        max_batch=key[2], max_len=key[1], max_steps=max_steps)
+            stream = _native.stream_handle()
+            dec_w = {k: v.float().contiguous() for k, v in self._params.items() if k.startswith("decoder.")}
+            arr, keep = _native.tensor_views(dec_w)
+            h = ctypes.c_void_p()
+            _native.check(lib.tts_decoder_create(ctypes.byref(cfg), arr, len(dec_w), stream, ctypes.byref(h)),
+                          "tts_decoder_create")
+            post_w = {k: v.float().contiguous() for k, v in self._params.items()
+                      if k.startswith("postnet.") and v.is_floating_point()}
+            arr2, keep2 = _native.tensor_views(post_w)
+            p = ctypes.c_void_p()
+            _native.check(lib.tts_postnet_create(arr2, len(post_w), 80, stream, ctypes.byref(p)), "tts_postnet_create")
+            self._native = (h, p, key)
+        return lib, self._native[0], self._native[1]
+
+    # ------------------------------------------------------------------ encoder (PyTorch-ROCm)
+    def _encoder_lstm(self):
+        if getattr(self, "_lstm", None) is None:
+            lstm = torch.nn.LSTM(512, 256, num_layers=1, batch_first=True, bidirectional=True).to(self.device)
+            with torch.no_grad():
+                for name, prm in lstm.named_parameters():
+                    prm.copy_(self._params["encoder.lstm." + name])
+            lstm.eval()
+            self._lstm = lstm
+        return self._lstm
+
+    def encode(self, ids: torch.Tensor, lens, speaker_ids=None):
+        """Embedding + Encoder.inference (models/tacotron2.py:63-66, layers/tacotron2.py:78-83)
+        on a padded batch; every sentence sees zero padding past its own length, as alone."""
+        p = self._params
+        B, Lmax = ids.shape
+        lens_t = torch.as_tensor(lens, device=ids.device)
+        valid = (torch.arange(Lmax, device=ids.device)[None, :] < lens_t[:, None]).float()  # [B, L]
+        x = F.embedding(ids, p["embedding.weight"]).transpose(1, 2)  # [B, 512, L]
+        for i in range(3):
+            pre = f"encoder.convolutions.{i}.net."
+            x = x * valid[:, None, :]
+            x = F.conv1d(x, p[pre + "0.weight"], p[pre + "0.bias"], padding=2)
+            x = F.batch_norm(x, p[pre + "1.running_mean"], p[pre + "1.running_var"], p[pre + "1.weight"],
+                             p[pre + "1.bias"], training=False, eps=1e-5)
+            x = F.relu(x)
+        x = x.transpose(1, 2).contiguous()  # [B, L, 512]
+        lstm = self._encoder_lstm()
+        if B == 1 or min(lens) == Lmax:
+            out, _ = lstm(x)
+        else:  # each sentence's reverse direction starts at its own last position
+            packed = torch.nn.utils.rnn.pack_padded_sequence(x, torch.as_tensor(lens), batch_first=True,
+                                                             enforce_sorted=False)
+            out, _ = lstm(packed)
+            out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, batch_first=True, total_length=Lmax)
+        if speaker_ids is not None and "speaker_embedding.weight" in p:
+            out = out + F.embedding(torch.as_tensor(speaker_ids, device=ids.device).view(-1),
+                                    p["speaker_embedding.weight"])[:, None, :]
+        return out
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def inference_batch(self, ids_list, speaker_ids=None, enc=None, lens=None):
+        """Ragged batch: ids_list = list of 1-D id sequences.  Returns a dict of padded CUDA
+        tensors (mel, mel_post [B,T,80]; align [B,Tsteps,L]; stop [B,Tsteps]) plus per-sentence
+        ``frames`` (n_steps*r) and ``steps``."""
+        _native.lib()  # raises without a GPU / library: no CPU fallback
+        if enc is None:
+            lens = [len(x) for x in ids_list]
+            B, Lmax = len(lens), max(lens)
+            ids = torch.zeros(B, Lmax, dtype=torch.long)
+            for b, x in enumerate(ids_list):
+                ids[b, :lens[b]] = torch.as_tensor(np.asarray(x), dtype=torch.long)
+            if self.device.type != "cuda":
+                self.cuda()
+            enc = self.encode(ids.to(self.device), lens, speaker_ids)
+        else:
+            B, Lmax = enc.shape[0], enc.shape[1]
+            lens = list(lens) if lens is not None else [Lmax] * B
+        if min(lens) < 2:
+            raise ValueError("encoder length must be >= 2 (the reference's forward-attention mask "
+                             "indexes alpha[n-2], common_layers.py:213)")
+        lib, hdec, hpost = self._handles(Lmax, B)
+        r = self.n_frames_per_step
+        max_steps = int(self.decoder.max_decoder_steps)
+        cap = max_steps + 21
+        dev = self.device
+        enc = enc.float().contiguous()
+        mel = torch.zeros(B, cap * r, 80, device=dev)
+        stop = torch.zeros(B, cap, device=dev)
+        align = torch.zeros(B, cap, Lmax, device=dev)
+        n_steps = (ctypes.c_int32 * B)()
+        stream = _native.stream_handle()
+        _native.check(lib.tts_decoder_run(hdec, ctypes.c_void_p(enc.data_ptr()), _native.i32_array(lens), B, Lmax,
+                                          max_steps, cap, ctypes.c_void_p(mel.data_ptr()),
+                                          ctypes.c_void_p(stop.data_ptr()), ctypes.c_void_p(align.data_ptr()),
+                                          n_steps, stream), "tts_decoder_run")
+        steps = [int(n_steps[b]) for b in range(B)]
+        for s in steps:
+            if s >= max_steps:
+                print("   | > Decoder stopped with 'max_decoder_steps")  # layers/tacotron2.py:276
+                break
+        frames = [s * r for s in steps]
+        mel_post = torch.zeros_like(mel)
+        _native.check(lib.tts_postnet_run(hpost, ctypes.c_void_p(mel.data_ptr()), _native.i32_array(frames), B,
+                                          cap * r, ctypes.c_void_p(mel_post.data_ptr()), stream), "tts_postnet_run")
+        T, S = max(frames), max(steps)
+        ms = ctypes.c_float()
+        ns = ctypes.c_int()
+        lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
+        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value)
+        self.last_lengths = frames
+        return dict(mel=mel[:, :T], mel_post=mel_post[:, :T], align=align[:, :S], stop=stop[:, :S],
+                    frames=frames, steps=steps, lens=lens)
+
+    @torch.no_grad()
+    def inference(self, text, speaker_ids=None):
+        """models/tacotron2.py:62-73.  text: LongTensor [B, L] (all rows length L)."""
+        text = torch.as_tensor(text)
+        if text.dim() == 1:
+            text = text.unsqueeze(0)
+        out = self.inference_batch([row for row in text.cpu().numpy()], speaker_ids=speaker_ids)
+        return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
+
+    def inference_truncated(self, text, speaker_ids=None):
+        raise NotImplementedError("inference_truncated (continuous mode) is SURVEY 8(f) row 4, not yet built")
+
+    __call__ = inference
