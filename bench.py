@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Headline benchmark: mel-frames/s and RTF of Tacotron2 + 60-iteration Griffin-Lim on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--L 100] [--iters 60]
+
+A step = one pass of the synthesis hot path over one batch of synthetic sentences per rank:
+ids (already in HBM) -> encoder -> HIP decoder loop -> HIP postnet -> HIP Griffin-Lim (60 iters,
+inverse pre-emphasis) -> waveforms in HBM; with N > 1 ranks the finished waveforms are gathered to
+rank 0 over RCCL (the only collective: sentences are independent).  Weak scaling:
+every rank synthesises --batch sentences per step.
+
+Default workload = BASELINE.json configs[1]: one LJSpeech-length sentence (L=100 ids, seed 1,
+-> 222 frames), config_tacotron2.json + forward_attn_mask (synthesize.py:86), random-init weights
+from the deterministic generator (seed 0), GL 60 iterations.
+
+Prints ONE JSON line on rank 0 (keys per the driver contract, plus roofline / cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+pkg = importlib.import_module("your-voice-tts_amd")
+t2mod = importlib.import_module("your-voice-tts_amd.tacotron2")
+audiomod = importlib.import_module("your-voice-tts_amd.audio")
+weights = importlib.import_module("your-voice-tts_amd.weights")
+gu = importlib.import_module("your-voice-tts_amd.generic_utils")
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA peak (same table)
+POSTNET_FLOP_PER_FRAME = 2 * 5 * (80 * 512 + 3 * 512 * 512 + 512 * 80)
+GL_BYTES_PER_FRAME_ITER = 4 * 1025 + 2 * 4 * 275                        # 6300 B
+
+
+def kernel_algorithmic(name, B, L, frames_total, r=1):
+    """(kind, algorithmic bytes or flops per launch) for each timed kernel."""
+    nm = 80 * r
+    by = {
+        "prenet1": 4 * (256 * nm + B * (nm + 256)),
+        "prenet2": 4 * (256 * 256 + B * (256 + 256)),
+        "att_lstm": 4 * (4096 * 1792 + B * (1792 + 3 * 1024)),
+        "query": 4 * (128 * 1024 + B * (1024 + 128)),
+        "attention": 4 * B * (L * 640 + 2 * L + 128 + 512),
+        "dec_lstm": 4 * (4096 * 2560 + B * (2560 + 3 * 1024)),
+        "mel_proj": 4 * (nm * 1536 + B * (1536 + 2 * nm)),
+        "stop": 4 * ((1024 + nm) + B * (1024 + nm + 1)),
+        "gl_iter": GL_BYTES_PER_FRAME_ITER * frames_total,
+    }
+    return ("hbm", by[name])
+
+
+def build(args, device):
+    cfg = gu.default_config("config_tacotron2.json")
+    cfg.forward_attn_mask = True  # synthesize.py:86
+    model = gu.setup_model(130, cfg, max_batch=max(args.batch, 1), max_len=max(args.L, 256))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in weights.tacotron2_weights(0).items()})
+    model.cuda().eval()
+    audio = dict(cfg.audio)
+    audio["griffin_lim_iters"] = args.iters
+    ap = audiomod.AudioProcessor(**audio)
+    return cfg, model, ap
+
+
+def make_ids(args, rank):
+    if args.lengths == "fixed":
+        return [weights.synthetic_ids(args.L, 1) for _ in range(args.batch)]  # configs[1]: L=100, seed 1
+    lens = weights.synthetic_lengths(args.batch, 2 + rank)  # configs[2]/[3]: L ~ U{60..160}
+    return [weights.synthetic_ids(int(L), 1000 * rank + b) for b, L in enumerate(lens)]
+
+
+@torch.no_grad()
+def run_step(model, ap, ids, world, seed, gather_buf=None):
+    out = model.inference_batch(ids)
+    wav = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=seed)
+    if world > 1:
+        n = gather_buf[0].shape[-1]
+        local = torch.zeros(wav.shape[0], n, dtype=wav.dtype, device=wav.device)
+        local[:, :wav.shape[1]] = wav
+        dist.all_gather_into_tensor(gather_buf[1], local)  # RCCL over xGMI: finished waveforms only
+    return out["frames"], wav
+
+
+def cpu_baseline(args, seconds_target=12.0):
+    """Oracle (numpy restatement of the reference path) on the host: decoder + postnet + GL."""
+    from oracle.griffin_lim_oracle import AudioOracle
+    from oracle.tacotron2_oracle import Tacotron2Oracle
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    cfg = gu.default_config("config_tacotron2.json")
+    o = Tacotron2Oracle(weights.tacotron2_weights(0), dtype=np.float32, attn_norm=cfg.attention_norm,
+                        forward_attn=cfg.use_forward_attn, trans_agent=cfg.transition_agent,
+                        forward_attn_mask=True, location_attn=cfg.location_attn, attn_win=cfg.windowing)
+    ap = AudioOracle(**{**cfg.audio, "griffin_lim_iters": args.iters})
+    ids = weights.synthetic_ids(args.L, 1)
+    frames = 0
+    n = 0
+    t0 = time.time()
+    while True:
+        res = o.inference(ids)
+        np.random.seed(n)
+        ap.inv_mel_spectrogram(res["mel_post"].T)
+        frames += res["mel"].shape[0]
+        n += 1
+        if time.time() - t0 >= seconds_target or n >= 8:
+            break
+    dt = time.time() - t0
+    return dict(value=frames / dt, unit="mel-frames/s", cores=int(threads), kind="port",
+                sample=f"{n} x one L={args.L} sentence ({res['mel'].shape[0]} frames): numpy oracle decoder+postnet "
+                       f"(fp32) + GL {args.iters} iters (fp64, scipy.fftpack) on the host, {dt:.1f} s",
+                rtf=dt / (n * 275 * (res["mel"].shape[0] - 1) / 22050.0))
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_*.json), or None."""
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if kernel in d.get("per_launch_hbm_bytes", {}):
+            return d["per_launch_hbm_bytes"][kernel]
+    return None
+
+
+def main():
+    ap_ = argparse.ArgumentParser()
+    ap_.add_argument("--gpus", type=int, default=1)
+    ap_.add_argument("--steps", type=int, default=10)
+    ap_.add_argument("--warmup", type=int, default=3)
+    ap_.add_argument("--batch", type=int, default=1)
+    ap_.add_argument("--L", type=int, default=100)
+    ap_.add_argument("--lengths", choices=["fixed", "uniform"], default="fixed")
+    ap_.add_argument("--iters", type=int, default=60)
+    ap_.add_argument("--no-cpu-baseline", action="store_true")
+    ap_.add_argument("--no-profile", action="store_true")
+    args = ap_.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    cfg, model, ap = build(args, device)
+    ids = make_ids(args, rank)
+    gather_buf = None
+    if world > 1:
+        # waveform capacity per sentence: 275 * (max frames - 1) with frames <= 2*Lmax+22 under the mask
+        cap = ap.hop_length * (model.decoder.max_decoder_steps + 20)
+        gather_buf = (torch.zeros(args.batch, cap, dtype=torch.float64, device=device),
+                      torch.zeros(world * args.batch, cap, dtype=torch.float64, device=device))
+
+    for w in range(args.warmup):
+        run_step(model, ap, ids, world, seed=w, gather_buf=gather_buf)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    frames = None
+    for k in range(args.steps):
+        frames, _ = run_step(model, ap, ids, world, seed=1000 + k, gather_buf=gather_buf)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    nfr = torch.tensor([float(sum(frames))], dtype=torch.float64, device=device)
+    aud = torch.tensor([sum(ap.hop_length * (f - 1) for f in frames) / ap.sample_rate], dtype=torch.float64,
+                       device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(nfr)
+        dist.all_reduce(aud)
+    elapsed = float(t.item())
+    frames_per_step = float(nfr.item())
+    audio_s_per_step = float(aud.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = frames_per_step * args.steps / elapsed
+    rtf = (elapsed / args.steps) / audio_s_per_step
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---- per-stage wall times (rank 0, one extra untimed step) and per-kernel profile
+    torch.cuda.synchronize()
+    s0 = time.perf_counter()
+    out = model.inference_batch(ids)
+    torch.cuda.synchronize()
+    s1 = time.perf_counter()
+    ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=7)
+    torch.cuda.synchronize()
+    s2 = time.perf_counter()
+    dec_ms = model.last_timing.get("decoder_loop_ms", 0.0)
+    gl_ms = ap.last_gl_timing()["gl_loop_ms"]
+    stages = dict(tacotron2_ms=1000 * (s1 - s0), decoder_loop_ms=dec_ms, griffin_lim_ms=1000 * (s2 - s1),
+                  gl_iteration_loop_ms=gl_ms)
+    roofline = None
+    kernels = {}
+    if not args.no_profile:
+        B = len(ids)
+        Lmean = float(np.mean([len(x) for x in ids]))
+        steps = max(out["steps"])
+        frames_total = sum(out["frames"])
+        kd = model.profile_step_kernels(reps=50)
+        kg = ap.profile_gl_kernels(reps=20)
+        launches = {k: steps for k in kd}
+        launches["gl_iter"] = args.iters
+        allk = {**kd, "gl_iter": kg["gl_iter"]}
+        for k, ms in allk.items():
+            kind, alg = kernel_algorithmic(k, B, Lmean, frames_total)
+            kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],
+                              algorithmic_bytes=alg, achieved_gbs=alg / (ms * 1e-3) / 1e9 if ms > 0 else None)
+        dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+        kdom = kernels[dom]
+        traffic = load_traffic(dom)
+        roofline = dict(bound="hbm", kernel=dom, achieved=kdom["achieved_gbs"], peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=kdom["achieved_gbs"] / HBM_PEAK_GBS, traffic=traffic,
+                        algorithmic_bytes_per_launch=kdom["algorithmic_bytes"], mean_launch_ms=kdom["mean_ms"])
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+
+    rec = {
+        "metric": "mel-frames/sec + RTF, Tacotron2 + 60-iter Griffin-Lim, LJSpeech",
+        "value": value,
+        "unit": "mel-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic ids, random-init weights (deterministic generator, seed 0)",
+        "config": {"workload": ("configs[1]: Tacotron2 single sentence, HIP decoder loop + HIP Griffin-Lim "
+                                f"{args.iters} iters" if args.batch == 1 else
+                                f"Tacotron2 batch={args.batch} per GPU, {args.lengths} lengths"),
+                   "sentences_per_gpu": args.batch, "L": args.L if args.lengths == "fixed" else "U{60..160}",
+                   "frames_per_step": frames_per_step, "gl_iters": args.iters,
+                   "model_config": "config_tacotron2.json + forward_attn_mask (synthesize.py:86)",
+                   "parallelism": f"sentence-sharded x{world}, RCCL waveform gather" if world > 1 else "single GPU"},
+        "rtf": rtf,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "stages_rank0": stages,
+        "kernels_rank0": kernels,
+    }
+    print(json.dumps(rec))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

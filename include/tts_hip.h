@@ -84,6 +84,14 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
 /* Per-step timing of the last tts_decoder_run (ms of GPU time of the step loop, steps run). */
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run);
 
+/* Measurement only (no reference counterpart): re-runs up to `reps` steps of the last
+ * tts_decoder_run's batch eagerly, with a HIP event before/after every kernel on the stream it
+ * is launched on, and returns the mean duration (ms) of each step kernel, in launch order:
+ * prenet1, prenet2, attention-LSTM, query, attention, decoder-LSTM, mel projection, stop.
+ * Leaves the decoder state mid-sentence (the next tts_decoder_run re-initialises it). */
+#define TTS_DECODER_STEP_KERNELS 8
+tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n_kernels);
+
 /* Replaces Postnet (layers/tacotron2.py:30-45) + the residual add of models/tacotron2.py:69-70:
  * out = mel + postnet(mel), per sentence at its own length (zero padding past T_b).
  * `tensors` must hold the postnet.* keys. */
@@ -126,6 +134,12 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
 
 /* Time of the last tts_gl_run's iteration loop (ms, GPU) and kernel launches in it. */
 tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
+
+/* Measurement only: re-runs `reps` GL iterations of the last tts_gl_run's batch eagerly with
+ * HIP events around each kernel on its stream; returns mean ms of [iteration kernel, final
+ * overlap-add kernel].  Clobbers the internal frame buffers (not the caller's outputs). */
+#define TTS_GL_KERNELS 2
+tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels);
 
 const char* tts_last_error(void);
 const char* tts_version(void);

@@ -14,12 +14,15 @@ LIB_PATH = os.environ.get("TTS_HIP_LIB", os.path.join(_HERE, "libtts_hip.so"))
 
 TTS_GL_FROM_MEL = 0
 TTS_GL_FROM_LINEAR = 1
+DECODER_STEP_KERNELS = ("prenet1", "prenet2", "att_lstm", "query", "attention", "dec_lstm", "mel_proj", "stop")
+GL_KERNELS = ("gl_iter", "gl_ola")
 
 # every symbol include/tts_hip.h declares
 EXPORTS = (
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_last_timing",
+    "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
-    "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing",
+    "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
     "tts_last_error", "tts_version",
 )
 
@@ -67,11 +70,14 @@ def _declare(lib):
     lib.tts_gl_run.argtypes = [vp, ctypes.c_int, vp, I32P, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64,
                                ctypes.c_int, vp, vp]
     lib.tts_gl_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    FP = ctypes.POINTER(ctypes.c_float)
+    lib.tts_decoder_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
+    lib.tts_gl_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_last_error.restype = ctypes.c_char_p
     lib.tts_version.restype = ctypes.c_char_p
     for name in EXPORTS:
         fn = getattr(lib, name)
-        if fn.restype is ctypes.c_int or name.endswith(("_create", "_run", "_timing")):
+        if name.endswith(("_create", "_run", "_timing", "_profile")):
             fn.restype = ctypes.c_int
 
 

@@ -166,6 +166,14 @@ class AudioProcessor:
         lib.tts_gl_last_timing(h, ctypes.byref(ms), ctypes.byref(n))
         return dict(gl_loop_ms=ms.value, gl_iterations=n.value)
 
+    def profile_gl_kernels(self, reps=20):
+        """Mean duration (ms) of the GL iteration and overlap-add kernels for the last batch."""
+        lib, h = self._handle()
+        n = len(_native.GL_KERNELS)
+        ms = (ctypes.c_float * n)()
+        _native.check(lib.tts_gl_profile(h, int(reps), ms, n), "tts_gl_profile")
+        return dict(zip(_native.GL_KERNELS, [float(v) for v in ms]))
+
     def _single(self, spec_nT, mode):
         self._handle()  # raises without a GPU / library: no CPU fallback
         spec_nT = np.asarray(spec_nT, dtype=np.float32)

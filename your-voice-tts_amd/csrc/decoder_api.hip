@@ -50,6 +50,8 @@ struct tts_decoder {
     std::map<std::pair<int, int>, Graphs> graphs;
     float last_ms = 0.f;
     int last_steps = 0;
+    int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
+    InitArgs last_init{};
 };
 
 namespace {
@@ -88,7 +90,10 @@ tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, 
     return TTS_OK;
 }
 
-tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
+tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s, hipEvent_t* ev = nullptr) {
+    int mark = 0;
+#define MARK() \
+    if (ev) TTS_HIP(hipEventRecord(ev[mark++], s));
     const int nmel = d->nmel;
     const int64_t hps = (int64_t)d->Bcap * HATT;   // ping-pong stride of h buffers
     const int64_t xps = (int64_t)d->Bcap * XA;
@@ -105,7 +110,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.nseg = 1;
         a.W = d->W_pre1; a.K = nmel; a.N = PRE; a.act = ACT_RELU;
         a.out = d->pre1; a.ldo = PRE;
-        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     }
     // 2) prenet layer 2 -> xa[t&1][b][0:256]
     {
@@ -114,7 +120,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.nseg = 1;
         a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
         a.out = d->xa; a.out_pstride = xps; a.out_par = 0; a.ldo = XA;
-        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     }
     // 3) attention LSTM: x = [prenet | ctx_{t-1}] (xa[t&1]), h = h_att[(t+1)&1]  (tacotron2.py:195-197)
     {
@@ -125,7 +132,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.W = d->W_att; a.K = XA + HATT; a.N = 4 * HATT; a.bias = d->b_att;
         a.out = d->h_att; a.out_pstride = hps; a.out_par = 0; a.ldo = HATT;
         a.cell = d->c_att; a.ldc = HATT;
-        TTS_HIP(sgemm_launch(a, EPI_LSTM, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_ATT_LSTM, s));
     }
     // 4) processed query = query_layer(h_att)   (common_layers.py:170/179)
     {
@@ -134,7 +142,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.nseg = 1;
         a.W = d->W_q; a.K = HATT; a.N = ADIM;
         a.out = d->q; a.ldo = ADIM;
-        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_QUERY, s));
     }
     // 5) attention (energies, norm, forward attention, context)
     {
@@ -153,6 +162,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.align_hist = d->align_hist; a.align_ldb = (int64_t)d->hist_cap * Lmax; a.Lalign = Lmax;
         a.hist_cap = d->hist_cap;
         a.step = d->step; a.done = d->done; a.n_active = d->n_active;
+        MARK();
         TTS_HIP(launch_attention(a, s));
     }
     // 6) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec[(t+1)&1]   (tacotron2.py:206-208)
@@ -165,7 +175,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.W = d->W_dec; a.K = HATT + ENC + HDEC; a.N = 4 * HDEC; a.bias = d->b_dec;
         a.out = d->h_dec; a.out_pstride = hps; a.out_par = 0; a.ldo = HDEC;
         a.cell = d->c_dec; a.ldc = HDEC;
-        TTS_HIP(sgemm_launch(a, EPI_LSTM, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_DEC_LSTM, s));
     }
     // 7) mel = linear_projection([h_dec | ctx]) -> memory + history   (tacotron2.py:214-217)
     {
@@ -176,7 +187,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.W = d->W_mel; a.K = HDEC + ENC; a.N = nmel; a.bias = d->b_mel;
         a.out = d->mem; a.ldo = nmel;
         a.hist = d->mel_hist; a.ldh = (int64_t)d->hist_cap * nmel; a.hist_cap = d->hist_cap;
-        TTS_HIP(sgemm_launch(a, EPI_LINEAR, s));
+        MARK();
+        TTS_HIP(sgemm_launch(a, ROLE_MEL, s));
     }
     // 8) stopnet + stop rule + step advance
     {
@@ -189,8 +201,11 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s) {
         a.flag1 = d->flag1; a.count = d->count; a.done = d->done; a.n_steps = d->n_steps;
         a.step = d->step; a.n_active = d->n_active;
         a.max_steps = d->cfg.max_steps;  // replaced per run via graph key (see below)
+        MARK();
         TTS_HIP(launch_stop(a, s));
     }
+    MARK();
+#undef MARK
     return TTS_OK;
 }
 
@@ -459,6 +474,42 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
     TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
     d->last_steps = run;
+    d->last_B = B;
+    d->last_Lmax = Lmax;
+    d->last_max_steps = max_steps;
+    d->last_first = first;
+    d->last_init = ia;
+    return TTS_OK;
+}
+
+tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n_kernels) {
+    TTS_CHECK(d && kernel_ms && n_kernels >= TTS_DECODER_STEP_KERNELS, TTS_ERR_INVALID, "bad profile arguments");
+    TTS_CHECK(d->last_B > 0, TTS_ERR_INVALID, "tts_decoder_profile needs a previous tts_decoder_run");
+    // every sentence stays active for the first `last_first` steps: time only those
+    reps = std::max(1, std::min(reps, d->last_first - 1));
+    const int K = TTS_DECODER_STEP_KERNELS;
+    hipEvent_t ev[K + 1];
+    for (int i = 0; i <= K; ++i) TTS_HIP(hipEventCreate(&ev[i]));
+    hipStream_t s = d->stream;
+    const int saved_cap = d->cfg.max_steps;
+    d->cfg.max_steps = d->last_max_steps;
+    TTS_HIP(launch_decoder_init(d->last_init, s));
+    std::vector<double> acc(K, 0.0);
+    tts_status st = TTS_OK;
+    for (int r = 0; r < reps && st == TTS_OK; ++r) {
+        st = enqueue_step(d, d->last_B, d->last_Lmax, s, ev);
+        if (st) break;
+        TTS_HIP(hipEventSynchronize(ev[K]));
+        for (int i = 0; i < K; ++i) {
+            float ms = 0.f;
+            TTS_HIP(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            acc[i] += ms;
+        }
+    }
+    d->cfg.max_steps = saved_cap;
+    for (int i = 0; i <= K; ++i) (void)hipEventDestroy(ev[i]);
+    if (st) return st;
+    for (int i = 0; i < K; ++i) kernel_ms[i] = (float)(acc[i] / reps);
     return TTS_OK;
 }
 

@@ -353,6 +353,10 @@ struct tts_gl {
     std::map<GraphKey, hipGraphExec_t> graphs;
     float last_ms = 0.f;
     int last_launches = 0;
+    bool have_last = false;
+    IterArgs last_iter{};
+    FinArgs last_fin{};
+    size_t last_fstride = 0;
 };
 
 extern "C" {
@@ -542,6 +546,46 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipEventSynchronize(g->ev_t1));
     TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
     g->last_launches = iters;
+    g->have_last = true;
+    g->last_iter = ia;
+    g->last_fin = fa;
+    g->last_fstride = fstride;
+    return TTS_OK;
+}
+
+tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) {
+    TTS_CHECK(g && kernel_ms && n_kernels >= TTS_GL_KERNELS && reps >= 1, TTS_ERR_INVALID, "bad profile arguments");
+    TTS_CHECK(g->have_last, TTS_ERR_INVALID, "tts_gl_profile needs a previous tts_gl_run");
+    hipStream_t s = g->stream;
+    hipEvent_t ev[3];
+    for (auto& e : ev) TTS_HIP(hipEventCreate(&e));
+    const IterArgs& ia = g->last_iter;
+    const dim3 grid(ia.Fmax, ia.B), block(GL_THREADS);
+    double it_ms = 0.0, ola_ms = 0.0;
+    for (int r = 0; r < reps; ++r) {
+        IterArgs a = ia;
+        a.phase_u = nullptr;
+        a.prev = g->frames + (r & 1) * g->last_fstride;
+        a.next = g->frames + ((r + 1) & 1) * g->last_fstride;
+        TTS_HIP(hipEventRecord(ev[0], s));
+        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+        TTS_HIP(hipGetLastError());
+        TTS_HIP(hipEventRecord(ev[1], s));
+        FinArgs f = g->last_fin;
+        f.frames = a.next;
+        hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
+        TTS_HIP(hipGetLastError());
+        TTS_HIP(hipEventRecord(ev[2], s));
+        TTS_HIP(hipEventSynchronize(ev[2]));
+        float a_ms = 0.f, b_ms = 0.f;
+        TTS_HIP(hipEventElapsedTime(&a_ms, ev[0], ev[1]));
+        TTS_HIP(hipEventElapsedTime(&b_ms, ev[1], ev[2]));
+        it_ms += a_ms;
+        ola_ms += b_ms;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    kernel_ms[0] = (float)(it_ms / reps);
+    kernel_ms[1] = (float)(ola_ms / reps);
     return TTS_OK;
 }
 

@@ -23,6 +23,8 @@ struct Seg {
 };
 
 enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1 };
+// Decoder stage a launch serves; fixes the epilogue (LSTM roles use EPI_LSTM).
+enum Role { ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1 };
 
 struct SGemmArgs {
@@ -60,6 +62,6 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
                            hipStream_t s);
 inline size_t sgemm_packed_floats(int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; }
 
-hipError_t sgemm_launch(const SGemmArgs& a, int epi, hipStream_t s);
+hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s);
 
 }  // namespace tts

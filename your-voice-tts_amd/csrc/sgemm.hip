@@ -11,7 +11,8 @@ namespace tts {
 
 constexpr int MAX_WAVES = 8;
 
-template <int MT, int EPI>
+// ROLE only names the instantiation (distinct kernel names in rocprof traces per decoder stage).
+template <int MT, int EPI, int ROLE>
 __global__ __launch_bounds__(512) void sgemm_kernel(const SGemmArgs a) {
     if (a.n_active && *a.n_active == 0) return;
     const int ntile = blockIdx.x;
@@ -183,23 +184,30 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
     return hipGetLastError();
 }
 
-template <int EPI>
-static hipError_t launch_epi(const SGemmArgs& a, hipStream_t s) {
+template <int EPI, int ROLE>
+static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
     const int nchunks = a.K / 16;
     const int nw = nchunks < MAX_WAVES ? nchunks : MAX_WAVES;
     const dim3 grid((a.N + 15) / 16), block(nw * 64);
     const int mt = (a.B + 15) / 16;
     if (mt <= 1)
-        hipLaunchKernelGGL((sgemm_kernel<1, EPI>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((sgemm_kernel<1, EPI, ROLE>), grid, block, 0, s, a);
     else if (mt <= 2)
-        hipLaunchKernelGGL((sgemm_kernel<2, EPI>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((sgemm_kernel<2, EPI, ROLE>), grid, block, 0, s, a);
     else
-        hipLaunchKernelGGL((sgemm_kernel<4, EPI>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((sgemm_kernel<4, EPI, ROLE>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t sgemm_launch(const SGemmArgs& a, int epi, hipStream_t s) {
-    return epi == EPI_LSTM ? launch_epi<EPI_LSTM>(a, s) : launch_epi<EPI_LINEAR>(a, s);
+hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s) {
+    switch (role) {
+        case ROLE_PRENET: return launch_role<EPI_LINEAR, ROLE_PRENET>(a, s);
+        case ROLE_ATT_LSTM: return launch_role<EPI_LSTM, ROLE_ATT_LSTM>(a, s);
+        case ROLE_QUERY: return launch_role<EPI_LINEAR, ROLE_QUERY>(a, s);
+        case ROLE_DEC_LSTM: return launch_role<EPI_LSTM, ROLE_DEC_LSTM>(a, s);
+        case ROLE_MEL: return launch_role<EPI_LINEAR, ROLE_MEL>(a, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace tts

@@ -262,6 +262,15 @@ class Tacotron2:
         out = self.inference_batch([row for row in text.cpu().numpy()], speaker_ids=speaker_ids)
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
+    def profile_step_kernels(self, reps=50):
+        """Mean duration (ms) of each decoder-step kernel, HIP events on its own stream, for the
+        batch of the last inference call (measurement only)."""
+        lib, hdec, _ = self._handles(1, 1)
+        n = len(_native.DECODER_STEP_KERNELS)
+        ms = (ctypes.c_float * n)()
+        _native.check(lib.tts_decoder_profile(hdec, int(reps), ms, n), "tts_decoder_profile")
+        return dict(zip(_native.DECODER_STEP_KERNELS, [float(v) for v in ms]))
+
     def inference_truncated(self, text, speaker_ids=None):
         raise NotImplementedError("inference_truncated (continuous mode) is SURVEY 8(f) row 4, not yet built")
 
