@@ -47,14 +47,13 @@ def kernel_algorithmic(name, B, L, frames_total, r=1):
     """(kind, algorithmic bytes or flops per launch) for each timed kernel."""
     nm = 80 * r
     by = {
-        "prenet1": 4 * (256 * nm + B * (nm + 256)),
         "prenet2": 4 * (256 * 256 + B * (256 + 256)),
         "att_lstm": 4 * (4096 * 1792 + B * (1792 + 3 * 1024)),
         "query": 4 * (128 * 1024 + B * (1024 + 128)),
         "attention": 4 * B * (L * 640 + 2 * L + 128 + 512),
         "dec_lstm": 4 * (4096 * 2560 + B * (2560 + 3 * 1024)),
-        "mel_proj": 4 * (nm * 1536 + B * (1536 + 2 * nm)),
-        "stop": 4 * ((1024 + nm) + B * (1024 + nm + 1)),
+        # fused mel projection (nm rows) + folded prenet L1 (256 rows) + folded stopnet (1 row)
+        "mel_fused": 4 * ((nm + 257) * 1536 + B * (1536 + nm + 256 + 1)),
         "gl_iter": GL_BYTES_PER_FRAME_ITER * frames_total,
     }
     return ("hbm", by[name])

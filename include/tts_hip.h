@@ -87,9 +87,9 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
 /* Measurement only (no reference counterpart): re-runs up to `reps` steps of the last
  * tts_decoder_run's batch eagerly, with a HIP event before/after every kernel on the stream it
  * is launched on, and returns the mean duration (ms) of each step kernel, in launch order:
- * prenet1, prenet2, attention-LSTM, query, attention, decoder-LSTM, mel projection, stop.
+ * prenet2, attention-LSTM, query, attention, decoder-LSTM, fused mel/prenet1/stop.
  * Leaves the decoder state mid-sentence (the next tts_decoder_run re-initialises it). */
-#define TTS_DECODER_STEP_KERNELS 8
+#define TTS_DECODER_STEP_KERNELS 6
 tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n_kernels);
 
 /* Replaces Postnet (layers/tacotron2.py:30-45) + the residual add of models/tacotron2.py:69-70:
@@ -116,9 +116,10 @@ typedef struct tts_audio_config {
 #define TTS_GL_FROM_MEL 0     /* AudioProcessor.inv_mel_spectrogram (utils/audio.py:164-172) */
 #define TTS_GL_FROM_LINEAR 1  /* AudioProcessor.inv_spectrogram     (utils/audio.py:154-162) */
 
-/* inv_mel_basis: [host] fp32 [n_fft/2+1][num_mels] = pinv(mel basis) (utils/audio.py:64-66);
- * may be NULL when only the linear path is used. */
-tts_status tts_gl_create(const tts_audio_config* cfg, const float* inv_mel_basis, void* stream, tts_gl** out);
+/* inv_mel_basis: [host] fp64 [n_fft/2+1][num_mels] = pinv(mel basis) (utils/audio.py:64-66);
+ * may be NULL when only the linear path is used.  Magnitudes, FFTs and the phase are float64,
+ * the STFT is rounded to complex64 and the signal kept float32, as librosa 0.6.2 does. */
+tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basis, void* stream, tts_gl** out);
 void tts_gl_destroy(tts_gl* g);
 
 /* Batched Griffin-Lim vocoder: replaces inv_mel_spectrogram / inv_spectrogram, i.e.

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("TTS_HIP_LIB", os.path.join(_HERE, "libtts_hip.so"))
 
 TTS_GL_FROM_MEL = 0
 TTS_GL_FROM_LINEAR = 1
-DECODER_STEP_KERNELS = ("prenet1", "prenet2", "att_lstm", "query", "attention", "dec_lstm", "mel_proj", "stop")
+DECODER_STEP_KERNELS = ("prenet2", "att_lstm", "query", "attention", "dec_lstm", "mel_fused")
 GL_KERNELS = ("gl_iter", "gl_ola")
 
 # every symbol include/tts_hip.h declares

@@ -127,7 +127,7 @@ class AudioProcessor:
                 power=self.power, max_norm=self.max_norm, preemphasis=float(self.preemphasis),
                 signal_norm=int(bool(self.signal_norm)), symmetric_norm=int(bool(self.symmetric_norm)),
                 clip_norm=int(bool(self.clip_norm)))
-            pinv = np.ascontiguousarray(np.linalg.pinv(self._build_mel_basis()), dtype=np.float32)
+            pinv = np.ascontiguousarray(np.linalg.pinv(self._build_mel_basis()), dtype=np.float64)
             h = ctypes.c_void_p()
             _native.check(lib.tts_gl_create(ctypes.byref(cfg), pinv.ctypes.data_as(ctypes.c_void_p),
                                             _native.stream_handle(), ctypes.byref(h)), "tts_gl_create")

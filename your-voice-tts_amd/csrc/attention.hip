@@ -44,6 +44,18 @@ __global__ void decoder_init_kernel(const InitArgs a) {
     }
 }
 
+// Zero rows [n_steps[b], nmax) of a per-sentence history dst[b][step][width].
+__global__ void zero_tail_kernel(float* dst, int64_t ldb, const int* n_steps, int width, int nmax) {
+    const int b = blockIdx.x;
+    float* p = dst + (int64_t)b * ldb;
+    for (int64_t i = (int64_t)n_steps[b] * width + threadIdx.x; i < (int64_t)nmax * width; i += blockDim.x) p[i] = 0.f;
+}
+
+hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s) {
+    hipLaunchKernelGGL(zero_tail_kernel, dim3(B), dim3(256), 0, s, dst, ldb, n_steps, width, nmax);
+    return hipGetLastError();
+}
+
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B), dim3(256), 0, s, a);
     return hipGetLastError();
@@ -93,214 +105,240 @@ hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lm
 }
 
 // ------------------------------------------------------------------ attention step
+// One workgroup of 1024 threads per sentence; thread j owns encoder position j (L <= 1024).
 size_t attention_smem_bytes(int Lcap, int location) {
-    size_t f = ADIM + 4 * (size_t)Lcap + 8 * (size_t)Lcap + 64;
+    size_t f = 2 * ADIM + 4 * (size_t)Lcap + ATT_WAVES * (size_t)Lcap + 4 * ATT_WAVES;
     if (location) f += 2 * ((size_t)Lcap + 32) + (size_t)NLOC * Lcap + ADIM * NLOC;
     return f * sizeof(float);
 }
 
-// Per-thread strided partials then a block reduction (fixed order => deterministic).
-__device__ __forceinline__ float strided_sum(const float* x, int n, float* scr) {
-    float s = 0.f;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) s += x[j];
-    return block_sum(s, scr);
-}
-__device__ __forceinline__ float strided_max(const float* x, int n, float* scr) {
-    float m = -INFINITY;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) m = fmaxf(m, x[j]);
-    return block_max(m, scr);
-}
-// argmax with first-index ties; `prev_shift` reads x[j-1] (0 at j=0) instead of x[j].
-__device__ __forceinline__ int strided_argmax(const float* x, int n, bool prev_shift, float* scr, int* iscr) {
-    float m = -INFINITY;
-    int mi = 0x7fffffff;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        const float v = prev_shift ? (j ? x[j - 1] : 0.f) : x[j];
-        if (v > m || mi == 0x7fffffff) { m = v; mi = j; }
+// One barrier-pair block reduction of (sum of s, max of m, argmax of y with first-index ties).
+struct Red {
+    float s, m, y;
+    int i;
+};
+__device__ __forceinline__ Red block_reduce(float s, float m, float y, int i, float* scr) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        m = fmaxf(m, __shfl_xor(m, o, 64));
+        const float oy = __shfl_xor(y, o, 64);
+        const int oi = __shfl_xor(i, o, 64);
+        if (oy > y || (oy == y && oi < i)) { y = oy; i = oi; }
     }
-    return block_argmax(m, mi, scr, iscr);
+    if (lane == 0) {
+        scr[4 * w] = s;
+        scr[4 * w + 1] = m;
+        scr[4 * w + 2] = y;
+        reinterpret_cast<int*>(scr)[4 * w + 3] = i;
+    }
+    __syncthreads();
+    Red r{scr[0], scr[1], scr[2], reinterpret_cast<int*>(scr)[3]};
+    for (int k = 1; k < nw; ++k) {  // fixed order: deterministic
+        r.s += scr[4 * k];
+        r.m = fmaxf(r.m, scr[4 * k + 1]);
+        const float oy = scr[4 * k + 2];
+        const int oi = reinterpret_cast<int*>(scr)[4 * k + 3];
+        if (oy > r.y || (oy == r.y && oi < r.i)) { r.y = oy; r.i = oi; }
+    }
+    __syncthreads();  // scr reusable
+    return r;
 }
 
 __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a) {
-    if (*a.n_active == 0) return;
     const int b = blockIdx.x;
-    const int t = *a.step;
+    const int2 st = *reinterpret_cast<const int2*>(a.step);  // {step, n_active}
     const int L = a.lens[b];
+    if (st.y == 0) return;
+    const int t = st.x;
     const int Lc = a.Lcap;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     extern __shared__ __align__(16) float sm[];
     float* q = sm;
-    float* e = q + ADIM;
-    float* al = e + Lc;
-    float* an = al + Lc;
-    float* aold = an + Lc;
-    float* red = aold + Lc;
-    float* scr = red + 8 * Lc;
-    int* iscr = reinterpret_cast<int*>(scr + 32);
-    float* cat = scr + 64;
+    float* vv = q + ADIM;
+    float* aold = vv + ADIM;
+    float* an = aold + Lc;
+    float* wts = an + Lc;
+    float* spare = wts + Lc;
+    float* red = spare + Lc;
+    float* scr = red + ATT_WAVES * Lc;
+    float* cat = scr + 4 * ATT_WAVES;
     float* locf = cat + 2 * (Lc + 32);
     float* wd = locf + NLOC * Lc;
 
     const int64_t row = (int64_t)b * Lc;
+    const int j = tid;  // this thread's encoder position
+    const bool in = j < L;
     const float* h = a.h_att + (int64_t)(t & 1) * a.h_pstride + (int64_t)b * HATT;
-    for (int d = tid; d < ADIM; d += blockDim.x) q[d] = a.q[(int64_t)b * ADIM + d];
-    if (a.forward_attn)
-        for (int j = tid; j < L; j += blockDim.x) aold[j] = a.alpha[row + j];
+    // ---- phase 0: every independent load at once
+    if (tid < ADIM) q[tid] = a.q[(int64_t)b * ADIM + tid];
+    else if (tid < 2 * ADIM) vv[tid - ADIM] = a.v[tid - ADIM];
+    const float u = a.forward_attn ? a.u[b] : 0.f;
+    const float vb = a.v_b[0];
+    float aold_j = 0.f;
+    if (a.forward_attn && in) {
+        aold_j = a.alpha[row + j];
+        aold[j] = aold_j;
+    }
     if (a.location_attn) {
         // attention_cat = [attention_weights; attention_weights_cum] (common_layers.py:167-169),
         // zero padded by (31-1)/2 = 15 on both sides for location_conv (:90-96).
-        for (int j = tid; j < L + 2 * 15; j += blockDim.x) {
-            const int p = j - 15;
-            const bool in = p >= 0 && p < L;
-            cat[j] = in ? a.att_w[row + p] : 0.f;
-            cat[Lc + 32 + j] = in ? a.att_cum[row + p] : 0.f;
+        for (int c = tid; c < L + 2 * 15; c += blockDim.x) {
+            const int p = c - 15;
+            const bool ok = p >= 0 && p < L;
+            cat[c] = ok ? a.att_w[row + p] : 0.f;
+            cat[Lc + 32 + c] = ok ? a.att_cum[row + p] : 0.f;
         }
         for (int i = tid; i < ADIM * NLOC; i += blockDim.x) wd[i] = a.loc_dense[i];
     }
     __syncthreads();
     if (a.location_attn) {
         for (int idx = tid; idx < NLOC * L; idx += blockDim.x) {
-            const int f = idx / L, j = idx - f * L;
+            const int f = idx / L, jj = idx - f * L;
             const float* cw = a.loc_conv + f * 2 * KLOC;
             float s = 0.f;
-            for (int k = 0; k < KLOC; ++k) s += cw[k] * cat[j + k];
-            for (int k = 0; k < KLOC; ++k) s += cw[KLOC + k] * cat[Lc + 32 + j + k];
-            locf[f * Lc + j] = s;
+            for (int k = 0; k < KLOC; ++k) s += cw[k] * cat[jj + k];
+            for (int k = 0; k < KLOC; ++k) s += cw[KLOC + k] * cat[Lc + 32 + jj + k];
+            locf[f * Lc + jj] = s;
         }
         __syncthreads();
     }
-
-    // energies e_j = v . tanh(pq + [loc_j] + P_j) + b_v  (common_layers.py:166-182)
-    const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
-    for (int j0 = 0; j0 < L; j0 += 64) {
-        const int j = j0 + lane;
-        if (j < L) {
-            float s = 0.f;
-            for (int dd = 0; dd < ADIM / 8; ++dd) {
-                const int d = wave * (ADIM / 8) + dd;
-                float x = q[d];
-                if (a.location_attn) {
-                    float lc = 0.f;
-                    for (int f = 0; f < NLOC; ++f) lc += wd[d * NLOC + f] * locf[f * Lc + j];
-                    x += lc;
+    // ---- phase 1: energy partials, wave w owns d in [8w, 8w+8), lanes own positions
+    {
+        const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
+        constexpr int DPW = ADIM / ATT_WAVES;
+        const int d0 = wave * DPW;
+        for (int j0 = 0; j0 < L; j0 += 64) {
+            const int jj = j0 + lane;
+            if (jj < L) {
+                float pv[DPW];
+#pragma unroll
+                for (int dd = 0; dd < DPW; ++dd) pv[dd] = Pt[(int64_t)(d0 + dd) * Lc + jj];
+                float s = 0.f;
+#pragma unroll
+                for (int dd = 0; dd < DPW; ++dd) {
+                    const int d = d0 + dd;
+                    float x = q[d];  // processed_query (+ location) + processed_inputs (common_layers.py:172-174, 180)
+                    if (a.location_attn) {
+                        float lc = 0.f;
+                        for (int f = 0; f < NLOC; ++f) lc += wd[d * NLOC + f] * locf[f * Lc + jj];
+                        x += lc;
+                    }
+                    x += pv[dd];
+                    s += vv[d] * tanhf(x);
                 }
-                x += Pt[(int64_t)d * Lc + j];
-                s += a.v[d] * tanhf(x);
+                red[wave * Lc + jj] = s;
             }
-            red[wave * Lc + j] = s;
         }
     }
     __syncthreads();
-    const float vb = a.v_b[0];
-    for (int j = tid; j < L; j += blockDim.x) {
+    float e = -INFINITY;
+    if (in) {
         float s = 0.f;
-        for (int w = 0; w < 8; ++w) s += red[w * Lc + j];
-        e[j] = s + vb;
+        for (int w = 0; w < ATT_WAVES; ++w) s += red[w * Lc + j];
+        e = s + vb;
     }
-    __syncthreads();
-
-    // eval-mode windowing (common_layers.py:184-197)
+    // ---- eval-mode windowing (common_layers.py:184-197)
     if (a.windowing) {
         const int wi = a.win_idx[b];
         const int back = wi - 2, front = wi + 6;
-        for (int j = tid; j < L; j += blockDim.x)
-            if ((back > 0 && j < back) || (front < L && j >= front)) e[j] = -INFINITY;
-        __syncthreads();
+        if (in && ((back > 0 && j < back) || (front < L && j >= front))) e = -INFINITY;
         if (wi == -1) {
-            const float m = strided_max(e, L, scr);
-            __syncthreads();
-            if (tid == 0) e[0] = m;
-            __syncthreads();
+            const Red r = block_reduce(0.f, in ? e : -INFINITY, 0.f, 0, scr);
+            if (j == 0) e = r.m;
         }
-        const int idx = strided_argmax(e, L, false, scr, iscr);
-        if (tid == 0) a.win_idx[b] = idx;
-        __syncthreads();
+        const Red r = block_reduce(0.f, -INFINITY, in ? e : -INFINITY, in ? j : 0x7fffffff, scr);
+        if (tid == 0) a.win_idx[b] = r.i;
     }
-
-    // normalisation (common_layers.py:239-245)
+    // ---- normalisation (common_layers.py:239-245), fused with argmax(prev_alpha) for the mask
+    const float prev_j = (in && a.forward_attn) ? (j ? aold[j - 1] : 0.f) : -INFINITY;
+    float al = 0.f;
+    int n = 0;
     if (a.attn_norm == 0) {
-        const float m = strided_max(e, L, scr);
-        for (int j = tid; j < L; j += blockDim.x) al[j] = expf(e[j] - m);
-        __syncthreads();
-        const float s = strided_sum(al, L, scr);
-        for (int j = tid; j < L; j += blockDim.x) al[j] = al[j] / s;
+        const Red r1 = block_reduce(0.f, e, prev_j, in ? j : 0x7fffffff, scr);
+        n = r1.i;
+        const float ex = in ? expf(e - r1.m) : 0.f;
+        const Red r2 = block_reduce(ex, -INFINITY, 0.f, 0, scr);
+        al = ex / r2.s;
     } else {
-        for (int j = tid; j < L; j += blockDim.x) al[j] = sigmoidf_(e[j]);
-        __syncthreads();
-        const float s = strided_sum(al, L, scr);
-        for (int j = tid; j < L; j += blockDim.x) al[j] = al[j] / s;
+        const float sg = in ? sigmoidf_(e) : 0.f;
+        const Red r = block_reduce(sg, -INFINITY, prev_j, in ? j : 0x7fffffff, scr);
+        n = r.i;
+        al = sg / r.s;
     }
-    __syncthreads();
-    if (a.location_attn)  // update_location_attention (:163-164)
-        for (int j = tid; j < L; j += blockDim.x) a.att_cum[row + j] += al[j];
+    if (a.location_attn && in) a.att_cum[row + j] += al;  // update_location_attention (:163-164)
 
-    const float* w = al;
+    float w = al;
+    bool sparse = false;  // true when at most 5 positions can be nonzero (forward mask)
     if (a.forward_attn) {
         // apply_forward_attention (common_layers.py:199-223)
-        const float u = a.u[b];
-        const float omu = 1.f - u;
-        for (int j = tid; j < L; j += blockDim.x) {
-            const float prev = j ? aold[j - 1] : 0.f;
-            const float mix = __fadd_rn(__fadd_rn(__fmul_rn(omu, aold[j]), __fmul_rn(u, prev)), 1e-8f);
-            an[j] = __fmul_rn(mix, al[j]);
+        float anj = 0.f;
+        if (in) {
+            const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - u, aold_j), __fmul_rn(u, prev_j)), 1e-8f);
+            anj = __fmul_rn(mix, al);
         }
-        __syncthreads();
         if (a.forward_attn_mask) {
-            const int n = strided_argmax(aold, L, true, scr, iscr);  // argmax of prev_alpha
-            __syncthreads();
-            const float val = strided_max(an, L, scr);
-            __syncthreads();
+            const Red r = block_reduce(0.f, in ? anj : -INFINITY, 0.f, 0, scr);
             // Python slicing of :211-213 incl. the negative-index wrap for n < 2
-            for (int j = tid; j < L; j += blockDim.x) {
-                const bool z = (j >= n + 3) || (n >= 1 ? j < n - 1 : j < L - 1);
-                if (z) an[j] = 0.f;
-            }
-            __syncthreads();
-            if (tid == 0) an[(n - 2 + L) % L] = 0.01f * val;
-            __syncthreads();
+            if (in && ((j >= n + 3) || (n >= 1 ? j < n - 1 : j < L - 1))) anj = 0.f;
+            if (j == (n - 2 + L) % L) anj = 0.01f * r.m;
+            sparse = true;
         }
-        const float s = strided_sum(an, L, scr);
-        for (int j = tid; j < L; j += blockDim.x) an[j] = an[j] / s;
-        __syncthreads();
-        w = an;
-        for (int j = tid; j < L; j += blockDim.x) a.alpha[row + j] = an[j];
+        const Red r = block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr);
+        w = in ? anj / r.s : 0.f;
+        if (in) a.alpha[row + j] = w;
     }
+    if (in) wts[j] = w;
+    __syncthreads();
+    // ---- outputs: attention weights (alpha or alignment), history, stop-rule tail (tacotron2.py:268)
+    if (a.location_attn && in) a.att_w[row + j] = w;
+    if (!a.done[b] && t < a.hist_cap && a.align_hist)
+        for (int jj = tid; jj < a.Lalign; jj += blockDim.x)
+            a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + jj] = jj < L ? wts[jj] : 0.f;
+    if (tid == 0) a.tail[b] = L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0];
 
-    // context = w . inputs  (bmm, common_layers.py:217 / 253)
+    // ---- context = w . inputs  (bmm, common_layers.py:217 / 253)
     float* ctx_out = a.xa + (int64_t)((t + 1) & 1) * a.xa_pstride + (int64_t)b * XA + PRE;
     const float* encb = a.enc + row * ENC;
     float ctx = 0.f;
-    {
-        const int d = tid;  // blockDim == 512 == ENC
-        int j = 0;
-        for (; j + 4 <= L; j += 4) {
-            const float e0 = encb[(int64_t)(j + 0) * ENC + d];
-            const float e1 = encb[(int64_t)(j + 1) * ENC + d];
-            const float e2 = encb[(int64_t)(j + 2) * ENC + d];
-            const float e3 = encb[(int64_t)(j + 3) * ENC + d];
-            ctx += w[j] * e0;
-            ctx += w[j + 1] * e1;
-            ctx += w[j + 2] * e2;
-            ctx += w[j + 3] * e3;
+    if (sparse) {
+        // only (n-2)%L and [n-1, n+2] can be nonzero after the mask: sum those rows in index order
+        if (tid < ENC) {
+            const int x = (n - 2 + L) % L;
+            const int lo = n >= 1 ? n - 1 : L - 1;
+            const int hi = min(n + 2, L - 1);
+            if (x < lo) ctx += wts[x] * encb[(int64_t)x * ENC + tid];
+            for (int p = lo; p <= hi; ++p) ctx += wts[p] * encb[(int64_t)p * ENC + tid];
+            if (x > hi) ctx += wts[x] * encb[(int64_t)x * ENC + tid];
         }
-        for (; j < L; ++j) ctx += w[j] * encb[(int64_t)j * ENC + d];
-        ctx_out[d] = ctx;
+    } else {
+        const int d = tid & (ENC - 1), half = tid >> 9;
+        float acc = 0.f;
+        int jj = half;
+        for (; jj + 6 < L; jj += 8) {
+            const float e0 = encb[(int64_t)jj * ENC + d];
+            const float e1 = encb[(int64_t)(jj + 2) * ENC + d];
+            const float e2 = encb[(int64_t)(jj + 4) * ENC + d];
+            const float e3 = encb[(int64_t)(jj + 6) * ENC + d];
+            acc += wts[jj] * e0;
+            acc += wts[jj + 2] * e1;
+            acc += wts[jj + 4] * e2;
+            acc += wts[jj + 6] * e3;
+        }
+        for (; jj < L; jj += 2) acc += wts[jj] * encb[(int64_t)jj * ENC + d];
+        red[tid] = acc;
+        __syncthreads();
+        if (tid < ENC) ctx = red[tid] + red[tid + ENC];
     }
+    if (tid < ENC) ctx_out[tid] = ctx;
     if (a.forward_attn && a.trans_agent) {
         // u = sigmoid(ta([context, query]))  (:220-222)
-        float p = a.ta_w[tid] * ctx;
-        for (int k = tid; k < HATT; k += blockDim.x) p += a.ta_w[ENC + k] * h[k];
-        const float s = block_sum(p, scr);
-        if (tid == 0) a.u[b] = sigmoidf_(s + a.ta_b[0]);
+        float p = tid < ENC ? a.ta_w[tid] * ctx : 0.f;
+        p += a.ta_w[ENC + tid] * h[tid];  // blockDim == HATT
+        const Red r = block_reduce(p, -INFINITY, 0.f, 0, scr);
+        if (tid == 0) a.u[b] = sigmoidf_(r.s + a.ta_b[0]);
     }
-    // attention_weights: alpha (forward) or alignment; history; stop-rule tail (tacotron2.py:268)
-    const bool rec = !a.done[b] && t < a.hist_cap && a.align_hist;
-    for (int j = tid; j < a.Lalign; j += blockDim.x) {
-        const float v = j < L ? w[j] : 0.f;
-        if (j < L && a.location_attn) a.att_w[row + j] = v;
-        if (rec) a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + j] = v;
-    }
-    if (tid == 0) a.tail[b] = L >= 2 ? w[L - 2] + w[L - 1] : w[0];
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
@@ -309,16 +347,28 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t attention_prepare(int Lcap, int location) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_smem_bytes(Lcap, location));
+}
+
 // ------------------------------------------------------------------ stopnet + stop rule
 // stop = sigmoid(stopnet([h_dec; mel]))   (tacotron2.py:219-224, 262)
 // flags as tacotron2.py:257-277: stop_flags[0] is always true; [1] latches
 // (tail > 0.8 and t > L); [2] = t > 2L; 20 extra steps; cap checked only in the `elif`.
-__global__ __launch_bounds__(256) void stop_kernel(const StopArgs a) {
-    if (*a.n_active == 0) return;
-    const int t = *a.step;
+// One wave per sentence; every per-sentence load is issued before the dot product.
+__global__ __launch_bounds__(1024) void stop_kernel(const StopArgs a) {
+    const int2 st = *reinterpret_cast<const int2*>(a.step);
+    if (st.y == 0) return;
+    const int t = st.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __shared__ int sdone[64];
     for (int b = wave; b < a.B; b += nw) {
-        if (a.done[b]) continue;
+        const int dn = a.done[b];
+        const int L = a.lens[b];
+        const float tail = a.tail[b];
+        const int f1 = a.flag1[b];
+        const int cnt = a.count[b];
         const float* h = a.h_dec + (int64_t)(t & 1) * a.h_pstride + (int64_t)b * HDEC;
         const float* m = a.mem + (int64_t)b * a.nmel;
         float p = 0.f;
@@ -326,33 +376,38 @@ __global__ __launch_bounds__(256) void stop_kernel(const StopArgs a) {
         for (int k = lane; k < a.nmel; k += 64) p += a.w[HDEC + k] * m[k];
         p = wave_sum(p);
         if (lane == 0) {
-            const float st = sigmoidf_(p + a.b[0]);
-            if (t < a.hist_cap) a.stop_hist[(int64_t)b * a.stop_ldb + t] = st;
-            const int L = a.lens[b];
-            const int f1 = a.flag1[b] | ((a.tail[b] > 0.8f && t > L) ? 1 : 0);
-            a.flag1[b] = f1;
-            const bool f2 = t > 2 * L;
-            if (f1 && f2) {
-                const int c = a.count[b] + 1;
-                a.count[b] = c;
-                if (c > 20) { a.done[b] = 1; a.n_steps[b] = t + 1; }
-            } else if (t + 1 == a.max_steps) {
-                a.done[b] = 1;
-                a.n_steps[b] = t + 1;
+            int nd = dn;
+            if (!dn) {
+                const float stv = sigmoidf_(p + a.b[0]);
+                if (t < a.hist_cap) a.stop_hist[(int64_t)b * a.stop_ldb + t] = stv;
+                const int nf1 = f1 | ((tail > 0.8f && t > L) ? 1 : 0);
+                a.flag1[b] = nf1;
+                const bool f2 = t > 2 * L;
+                if (nf1 && f2) {
+                    a.count[b] = cnt + 1;
+                    if (cnt + 1 > 20) nd = 1;
+                } else if (t + 1 == a.max_steps) {
+                    nd = 1;
+                }
+                if (nd) {
+                    a.done[b] = 1;
+                    a.n_steps[b] = t + 1;
+                }
             }
+            sdone[b] = nd;
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         int n = 0;
-        for (int b = 0; b < a.B; ++b) n += a.done[b] ? 0 : 1;
-        *a.n_active = n;
-        *a.step = t + 1;
+        for (int b = 0; b < a.B; ++b) n += sdone[b] ? 0 : 1;
+        *reinterpret_cast<int2*>(a.step) = make_int2(t + 1, n);
     }
 }
 
 hipError_t launch_stop(const StopArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(stop_kernel, dim3(1), dim3(256), 0, s, a);
+    const int threads = 64 * (a.B < 16 ? a.B : 16);
+    hipLaunchKernelGGL(stop_kernel, dim3(1), dim3(threads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -12,7 +12,8 @@ constexpr int ADIM = 128;  // attention_dim
 constexpr int NLOC = 32;   // location filters
 constexpr int KLOC = 31;   // location kernel
 constexpr int XA = PRE + ENC;  // [prenet | ctx] row of the attention-LSTM input
-constexpr int ATT_THREADS = 512;
+constexpr int ATT_THREADS = 1024;  // one thread per encoder position (L <= 1024)
+constexpr int ATT_WAVES = ATT_THREADS / 64;
 
 // Flags (tts_decoder_config) + weights + device state pointers, passed by value.
 struct AttnArgs {
@@ -47,7 +48,7 @@ struct AttnArgs {
     int64_t align_ldb;     // stride per sentence
     int Lalign;
     int hist_cap;
-    const int* step;
+    const int* step;      // int2 {step, n_active}: n_active == step + 1
     const int* done;
     const int* n_active;
 };
@@ -91,9 +92,11 @@ struct InitArgs {
 };
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
+hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s);
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_stop(const StopArgs& a, hipStream_t s);
 size_t attention_smem_bytes(int Lcap, int location);
+hipError_t attention_prepare(int Lcap, int location);  // raise the dynamic-LDS limit once
 
 }  // namespace tts

@@ -1,15 +1,21 @@
-// Host runtime of the decoder: weight repacking, workspace, hipGraph-captured step loop.
+// Host runtime of the decoder: weight repacking/folding, workspace, hipGraph-captured step loop.
 //
-// One decoder step = 8 launches on the library's own stream (captured once per (B, Lmax)):
-//   prenet L1 (sgemm relu) -> prenet L2 (sgemm relu) -> attention LSTM (sgemm + LSTM epilogue)
-//   -> query (sgemm) -> attention (1 WG / sentence) -> decoder LSTM (sgemm + LSTM epilogue)
-//   -> mel projection (sgemm) -> stopnet + stop rule (1 WG).
-// The step index lives in device memory (advanced by the stop kernel), so the same graph is
-// replayed for every step; ping-pong activation buffers are selected by its parity.
+// One decoder step = 6 launches on the library's own stream:
+//   prenet L2 (sgemm relu) -> attention LSTM (sgemm + LSTM epilogue) -> query (sgemm)
+//   -> attention (1 WG / sentence) -> decoder LSTM (sgemm + LSTM epilogue)
+//   -> fused [mel projection | next step's prenet L1 | stopnet + stop rule] (sgemm).
+// Prenet L1 and the stopnet are folded into the mel projection at load time (W1 W_mel and
+// w_stop W_mel, fp64), so the reference's mel -> prenet -> ... chain loses two dependent launches.
+// Ping-pong activation buffers are bound statically per step parity: three graphs are captured
+// per (B, Lmax, max_steps) — one even step, one odd step, and a CHUNK-step run starting even.
+// The step index and active count live in device memory in two parity slots {step, n_active}:
+// a step reads its own slot and the stop rule writes the other, so no launch ever races on it.
 // The host synchronises only at chunk boundaries: the first chunk is the reference's lower
 // bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
+#include <algorithm>
 #include <map>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -20,7 +26,8 @@ using namespace tts;
 
 namespace {
 struct Graphs {
-    hipGraphExec_t one = nullptr, chunk = nullptr;
+    hipGraphExec_t step[2] = {nullptr, nullptr};
+    hipGraphExec_t chunk = nullptr;
 };
 constexpr int CHUNK = 8;
 }  // namespace
@@ -33,21 +40,20 @@ struct tts_decoder {
     std::vector<void*> allocs;
     // packed GEMM weights + logical biases
     float *W_pre1 = nullptr, *W_pre2 = nullptr, *W_att = nullptr, *b_att = nullptr, *W_q = nullptr;
-    float *W_dec = nullptr, *b_dec = nullptr, *W_mel = nullptr, *b_mel = nullptr;
+    float *W_dec = nullptr, *b_dec = nullptr, *W_melf = nullptr, *b_melf = nullptr;
     // reference-layout small weights
     float *v = nullptr, *v_b = nullptr, *ta_w = nullptr, *ta_b = nullptr, *loc_conv = nullptr, *loc_dense = nullptr;
-    float *W_in = nullptr, *stop_w = nullptr, *stop_b = nullptr, *att_init = nullptr, *dec_init = nullptr, *go = nullptr;
+    float *W_in = nullptr, *att_init = nullptr, *dec_init = nullptr, *go = nullptr;
     // workspace
     int Lcap = 0, Bcap = 0, hist_cap = 0;
     float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
     float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr;
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
-    int *n_steps = nullptr, *step = nullptr, *n_active = nullptr;
+    int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
     float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
-    int align_L = 0;  // Lmax the align history is currently laid out for
-    int* host_flags = nullptr;  // pinned: [n_active, step]
-    std::map<std::pair<int, int>, Graphs> graphs;
+    int* host_flags = nullptr;  // pinned
+    std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
     int last_steps = 0;
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
@@ -79,10 +85,6 @@ struct WeightMap {
     }
 };
 
-#define GETW(var, key, n)                                   \
-    const float* var = wm.get(key, n);                     \
-    if (!var) return TTS_ERR_INVALID;
-
 tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, hipStream_t s) {
     tts_status st = dmalloc(d, dst, n);
     if (st) return st;
@@ -90,62 +92,62 @@ tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, 
     return TTS_OK;
 }
 
-tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s, hipEvent_t* ev = nullptr) {
+// Launches of one decoder step of parity p (0: even step, 1: odd step).  `ev` (optional, 7
+// events) brackets every launch for tts_decoder_profile.
+tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, hipStream_t s,
+                        hipEvent_t* ev = nullptr) {
     int mark = 0;
 #define MARK() \
     if (ev) TTS_HIP(hipEventRecord(ev[mark++], s));
     const int nmel = d->nmel;
-    const int64_t hps = (int64_t)d->Bcap * HATT;   // ping-pong stride of h buffers
+    const int q = 1 - p;
+    const int64_t hps = (int64_t)d->Bcap * HATT;  // ping-pong slot strides
     const int64_t xps = (int64_t)d->Bcap * XA;
+    float* h_att_cur = d->h_att + p * hps;
+    float* h_att_prev = d->h_att + q * hps;
+    float* h_dec_cur = d->h_dec + p * hps;
+    float* h_dec_prev = d->h_dec + q * hps;
+    float* xa_cur = d->xa + p * xps;   // [prenet_t | ctx_{t-1}]
+    float* ctx_cur = d->xa + q * xps + PRE;  // ctx_t (row stride XA)
+    int* st_cur = d->state + 2 * p;
     SGemmArgs g{};
     g.B = B;
-    g.step = d->step;
+    g.step = st_cur;
     g.done = d->done;
-    g.n_active = d->n_active;
     g.out_par = -1;
-    // 1) prenet layer 1: relu(W1 . memory)   (common_layers.py:77-83; dropout off in eval)
-    {
-        SGemmArgs a = g;
-        a.seg[0] = Seg{d->mem, 0, -1, nmel, nmel};
-        a.nseg = 1;
-        a.W = d->W_pre1; a.K = nmel; a.N = PRE; a.act = ACT_RELU;
-        a.out = d->pre1; a.ldo = PRE;
-        MARK();
-        TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
-    }
-    // 2) prenet layer 2 -> xa[t&1][b][0:256]
+    // 1) prenet layer 2 -> xa_cur[b][0:256]   (common_layers.py:77-83; dropout off in eval)
     {
         SGemmArgs a = g;
         a.seg[0] = Seg{d->pre1, 0, -1, PRE, PRE};
         a.nseg = 1;
         a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
-        a.out = d->xa; a.out_pstride = xps; a.out_par = 0; a.ldo = XA;
+        a.out = xa_cur; a.ldo = XA;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     }
-    // 3) attention LSTM: x = [prenet | ctx_{t-1}] (xa[t&1]), h = h_att[(t+1)&1]  (tacotron2.py:195-197)
+    // 2) attention LSTM: x = [prenet_t | ctx_{t-1}], h = h_att_{t-1}   (tacotron2.py:195-197)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->xa, xps, 0, XA, XA};
-        a.seg[1] = Seg{d->h_att, hps, 1, HATT, HATT};
+        a.seg[0] = Seg{xa_cur, 0, -1, XA, XA};
+        a.seg[1] = Seg{h_att_prev, 0, -1, HATT, HATT};
         a.nseg = 2;
         a.W = d->W_att; a.K = XA + HATT; a.N = 4 * HATT; a.bias = d->b_att;
-        a.out = d->h_att; a.out_pstride = hps; a.out_par = 0; a.ldo = HATT;
+        a.out = h_att_cur; a.ldo = HATT;
         a.cell = d->c_att; a.ldc = HATT;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_ATT_LSTM, s));
     }
-    // 4) processed query = query_layer(h_att)   (common_layers.py:170/179)
+    // 3) processed query = query_layer(h_att_t)   (common_layers.py:170/179)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->h_att, hps, 0, HATT, HATT};
+        a.seg[0] = Seg{h_att_cur, 0, -1, HATT, HATT};
         a.nseg = 1;
         a.W = d->W_q; a.K = HATT; a.N = ADIM;
         a.out = d->q; a.ldo = ADIM;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_QUERY, s));
     }
-    // 5) attention (energies, norm, forward attention, context)
+    // 4) attention (energies, norm, forward attention, context -> ctx_t)
     {
         AttnArgs a{};
         const tts_decoder_config& c = d->cfg;
@@ -155,70 +157,79 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, hipStream_t s, hipEvent
         a.v = d->v; a.v_b = d->v_b; a.ta_w = d->ta_w; a.ta_b = d->ta_b;
         a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
-        a.h_att = d->h_att; a.h_pstride = hps;
+        a.h_att = h_att_cur; a.h_pstride = 0;
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
         a.tail = d->tail;
-        a.xa = d->xa; a.xa_pstride = xps;
+        a.xa = ctx_cur - PRE; a.xa_pstride = 0;  // kernel writes xa[b][PRE + d]
         a.align_hist = d->align_hist; a.align_ldb = (int64_t)d->hist_cap * Lmax; a.Lalign = Lmax;
         a.hist_cap = d->hist_cap;
-        a.step = d->step; a.done = d->done; a.n_active = d->n_active;
+        a.step = st_cur; a.done = d->done; a.n_active = st_cur + 1;
         MARK();
         TTS_HIP(launch_attention(a, s));
     }
-    // 6) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec[(t+1)&1]   (tacotron2.py:206-208)
+    // 5) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec_{t-1}   (tacotron2.py:206-208)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->h_att, hps, 0, HATT, HATT};
-        a.seg[1] = Seg{d->xa + PRE, xps, 1, XA, ENC};
-        a.seg[2] = Seg{d->h_dec, hps, 1, HDEC, HDEC};
+        a.seg[0] = Seg{h_att_cur, 0, -1, HATT, HATT};
+        a.seg[1] = Seg{ctx_cur, 0, -1, XA, ENC};
+        a.seg[2] = Seg{h_dec_prev, 0, -1, HDEC, HDEC};
         a.nseg = 3;
         a.W = d->W_dec; a.K = HATT + ENC + HDEC; a.N = 4 * HDEC; a.bias = d->b_dec;
-        a.out = d->h_dec; a.out_pstride = hps; a.out_par = 0; a.ldo = HDEC;
+        a.out = h_dec_cur; a.ldo = HDEC;
         a.cell = d->c_dec; a.ldc = HDEC;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_DEC_LSTM, s));
     }
-    // 7) mel = linear_projection([h_dec | ctx]) -> memory + history   (tacotron2.py:214-217)
+    // 6) fused: mel = linear_projection([h_dec | ctx]) (tacotron2.py:214-217) -> history;
+    //    prenet L1 of the next step; stop = sigmoid(stopnet([h_dec; mel])) + stop rule (:219-277)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->h_dec, hps, 0, HDEC, HDEC};
-        a.seg[1] = Seg{d->xa + PRE, xps, 1, XA, ENC};
+        a.seg[0] = Seg{h_dec_cur, 0, -1, HDEC, HDEC};
+        a.seg[1] = Seg{ctx_cur, 0, -1, XA, ENC};
         a.nseg = 2;
-        a.W = d->W_mel; a.K = HDEC + ENC; a.N = nmel; a.bias = d->b_mel;
-        a.out = d->mem; a.ldo = nmel;
+        a.W = d->W_melf; a.K = HDEC + ENC; a.N = nmel + PRE + 1; a.bias = d->b_melf;
         a.hist = d->mel_hist; a.ldh = (int64_t)d->hist_cap * nmel; a.hist_cap = d->hist_cap;
+        MelFused& m = a.mf;
+        m.nmel = nmel; m.pre1 = d->pre1; m.ldp = PRE;
+        m.stop_hist = d->stop_hist; m.stop_ldb = d->hist_cap;
+        m.lens = d->lens; m.tail = d->tail; m.flag1 = d->flag1; m.count = d->count;
+        m.done = d->done; m.n_steps = d->n_steps;
+        m.state_next = d->state + 2 * q;
+        m.max_steps = max_steps;
         MARK();
-        TTS_HIP(sgemm_launch(a, ROLE_MEL, s));
-    }
-    // 8) stopnet + stop rule + step advance
-    {
-        StopArgs a{};
-        a.w = d->stop_w; a.b = d->stop_b; a.nmel = nmel;
-        a.h_dec = d->h_dec; a.h_pstride = hps; a.mem = d->mem; a.lens = d->lens; a.tail = d->tail;
-        a.stop_hist = d->stop_hist; a.stop_ldb = d->hist_cap; a.hist_cap = d->hist_cap;
-        a.max_steps = 0;  // patched below through the device copy of the cap
-        a.B = B;
-        a.flag1 = d->flag1; a.count = d->count; a.done = d->done; a.n_steps = d->n_steps;
-        a.step = d->step; a.n_active = d->n_active;
-        a.max_steps = d->cfg.max_steps;  // replaced per run via graph key (see below)
-        MARK();
-        TTS_HIP(launch_stop(a, s));
+        TTS_HIP(sgemm_launch(a, ROLE_MEL_FUSED, s));
     }
     MARK();
 #undef MARK
     return TTS_OK;
 }
 
-tts_status build_graph(tts_decoder* d, int B, int Lmax, int steps, hipGraphExec_t* out) {
+tts_status build_graph(tts_decoder* d, int B, int Lmax, int max_steps, int first_parity, int steps,
+                       hipGraphExec_t* out) {
     hipGraph_t g = nullptr;
     TTS_HIP(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
     tts_status st = TTS_OK;
-    for (int i = 0; i < steps && st == TTS_OK; ++i) st = enqueue_step(d, B, Lmax, d->stream);
+    for (int i = 0; i < steps && st == TTS_OK; ++i)
+        st = enqueue_step(d, B, Lmax, max_steps, (first_parity + i) & 1, d->stream);
     hipError_t e = hipStreamEndCapture(d->stream, &g);
     if (st) return st;
     TTS_HIP(e);
     TTS_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     TTS_HIP(hipGraphDestroy(g));
+    return TTS_OK;
+}
+
+// Step-0 prenet layer 1 on the go frame (later steps get it from the fused mel launch).
+tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s) {
+    SGemmArgs a{};
+    a.B = B;
+    a.step = d->state;
+    a.out_par = -1;
+    a.seg[0] = Seg{d->mem, 0, -1, d->nmel, d->nmel};
+    a.nseg = 1;
+    a.W = d->W_pre1; a.K = d->nmel; a.N = PRE; a.act = ACT_RELU;
+    a.out = d->pre1; a.ldo = PRE;
+    TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     return TTS_OK;
 }
 
@@ -235,6 +246,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
               "max_len must be in [2, 1024] (512 with location attention)");
     TTS_CHECK(cfg->max_steps >= 1, TTS_ERR_INVALID, "max_steps must be >= 1");
     TTS_CHECK(cfg->attn_norm == 0 || cfg->attn_norm == 1, TTS_ERR_INVALID, "Unknown value for attention norm type");
+    TTS_CHECK(!cfg->trans_agent || cfg->forward_attn, TTS_ERR_INVALID, "trans_agent requires forward_attn");
     auto* d = new tts_decoder();
     d->cfg = *cfg;
     d->nmel = 80 * cfg->r;
@@ -278,7 +290,6 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     GW(dinit, "decoder.decoder_rnn_inits.weight", HDEC);
     const float *taw = nullptr, *tab = nullptr, *lcw = nullptr, *ldw = nullptr;
     if (cfg->trans_agent) {
-        TTS_CHECK(cfg->forward_attn, TTS_ERR_INVALID, "trans_agent requires forward_attn");
         taw = wm.get("decoder.attention_layer.ta.weight", HATT + ENC);
         tab = wm.get("decoder.attention_layer.ta.bias", 1);
         if (!taw || !tab) return fail(TTS_ERR_INVALID);
@@ -300,6 +311,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         if (_e != hipSuccess) return fail(hip_fail(_e, #x, __FILE__, __LINE__)); \
     } while (0)
     // packed GEMM weights
+    const int nfused = nmel + PRE + 1;
     CK(dmalloc(d, &d->W_pre1, sgemm_packed_floats(PRE, nmel)));
     HK(sgemm_pack(pre0, nmel, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre1, s));
     CK(dmalloc(d, &d->W_pre2, sgemm_packed_floats(PRE, PRE)));
@@ -314,16 +326,25 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     HK(sgemm_pack(d_wih, HATT + ENC, d_whh, HDEC, 4 * HDEC, ROWMAP_LSTM, HDEC, d->W_dec, s));
     CK(dmalloc(d, &d->b_dec, 4 * HDEC));
     HK(sgemm_pack_bias(d_bih, d_bhh, 4 * HDEC, ROWMAP_LSTM, HDEC, d->b_dec, s));
-    CK(dmalloc(d, &d->W_mel, sgemm_packed_floats(nmel, HDEC + ENC)));
-    HK(sgemm_pack(pw, HDEC + ENC, nullptr, 0, nmel, ROWMAP_IDENTITY, 0, d->W_mel, s));
-    CK(dmalloc(d, &d->b_mel, (nmel + 15) / 16 * 16));
-    HK(sgemm_pack_bias(pb, nullptr, nmel, ROWMAP_IDENTITY, 0, d->b_mel, s));
+    {
+        float *wf = nullptr, *bf = nullptr;  // folded logical matrix (temporary)
+        HK(hipMalloc(&wf, sizeof(float) * nfused * (HDEC + ENC)));
+        HK(hipMalloc(&bf, sizeof(float) * nfused));
+        hipError_t e = fold_mel_weights(pw, pb, pre0, sw, sb, nmel, HDEC + ENC, HDEC, wf, bf, s);
+        if (e == hipSuccess) e = dmalloc(d, &d->W_melf, sgemm_packed_floats(nfused, HDEC + ENC)) ? hipErrorOutOfMemory
+                                                                                                : hipSuccess;
+        if (e == hipSuccess) e = sgemm_pack(wf, HDEC + ENC, nullptr, 0, nfused, ROWMAP_IDENTITY, 0, d->W_melf, s);
+        if (e == hipSuccess) e = dmalloc(d, &d->b_melf, (nfused + 15) / 16 * 16) ? hipErrorOutOfMemory : hipSuccess;
+        if (e == hipSuccess) e = sgemm_pack_bias(bf, nullptr, nfused, ROWMAP_IDENTITY, 0, d->b_melf, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        (void)hipFree(wf);
+        (void)hipFree(bf);
+        HK(e);
+    }
     // small weights in reference layout
     CK(copy_weight(d, &d->v, vw, ADIM, s));
     CK(copy_weight(d, &d->v_b, vb, 1, s));
     CK(copy_weight(d, &d->W_in, win, (size_t)ADIM * ENC, s));
-    CK(copy_weight(d, &d->stop_w, sw, HDEC + nmel, s));
-    CK(copy_weight(d, &d->stop_b, sb, 1, s));
     CK(copy_weight(d, &d->att_init, ainit, HATT, s));
     CK(copy_weight(d, &d->dec_init, dinit, HDEC, s));
     CK(copy_weight(d, &d->go, goinit, nmel, s));
@@ -361,17 +382,18 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->count, Bc));
     CK(dmalloc(d, &d->done, Bc));
     CK(dmalloc(d, &d->n_steps, Bc));
-    CK(dmalloc(d, &d->step, 4));
-    CK(dmalloc(d, &d->n_active, 4));
+    CK(dmalloc(d, &d->state, 4));  // {step, n_active} x 2 parities; kernels load one slot as int2
     CK(dmalloc(d, &d->mel_hist, (size_t)Bc * d->hist_cap * nmel));
     CK(dmalloc(d, &d->stop_hist, (size_t)Bc * d->hist_cap));
     CK(dmalloc(d, &d->align_hist, (size_t)Bc * d->hist_cap * Lc));
+    HK(attention_prepare(Lc, cfg->location_attn));
     HK(hipMemsetAsync(d->xa, 0, sizeof(float) * 2 * Bc * XA, s));
     HK(hipMemsetAsync(d->h_att, 0, sizeof(float) * 2 * Bc * HATT, s));
     HK(hipMemsetAsync(d->h_dec, 0, sizeof(float) * 2 * Bc * HDEC, s));
     HK(hipMemsetAsync(d->mem, 0, sizeof(float) * Bc * nmel, s));
     HK(hipMemsetAsync(d->enc, 0, sizeof(float) * Bc * Lc * ENC, s));
     HK(hipMemsetAsync(d->Pt, 0, sizeof(float) * Bc * ADIM * Lc, s));
+    HK(hipMemsetAsync(d->state, 0, sizeof(int) * 4, s));
     HK(hipStreamSynchronize(s));
 #undef CK
 #undef HK
@@ -383,15 +405,13 @@ void tts_decoder_destroy(tts_decoder* d) {
     if (!d) return;
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     for (auto& kv : d->graphs) {
-        if (kv.second.one) (void)hipGraphExecDestroy(kv.second.one);
-        if (kv.second.chunk) (void)hipGraphExecDestroy(kv.second.chunk);
+        for (auto* x : {kv.second.step[0], kv.second.step[1], kv.second.chunk})
+            if (x) (void)hipGraphExecDestroy(x);
     }
     for (void* p : d->allocs) (void)hipFree(p);
     if (d->host_flags) (void)hipHostFree(d->host_flags);
-    if (d->ev_in) (void)hipEventDestroy(d->ev_in);
-    if (d->ev_out) (void)hipEventDestroy(d->ev_out);
-    if (d->ev_t0) (void)hipEventDestroy(d->ev_t0);
-    if (d->ev_t1) (void)hipEventDestroy(d->ev_t1);
+    for (hipEvent_t e : {d->ev_in, d->ev_out, d->ev_t0, d->ev_t1})
+        if (e) (void)hipEventDestroy(e);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -406,8 +426,7 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     int first = 0;
     for (int b = 0; b < B; ++b) {
         TTS_CHECK(lens[b] >= 2 && lens[b] <= Lmax, TTS_ERR_INVALID, "encoder length out of range [2, Lmax]");
-        const int lb = std::min(2 * lens[b] + 22, max_steps);
-        first = std::max(first, lb);
+        first = std::max(first, std::min(2 * lens[b] + 22, max_steps));
     }
     hipStream_t cs = static_cast<hipStream_t>(stream);
     hipStream_t s = d->stream;
@@ -424,35 +443,43 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
     ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
     ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
-    ia.step = d->step; ia.n_active = d->n_active;
+    ia.step = d->state; ia.n_active = d->state + 1;
     TTS_HIP(launch_decoder_init(ia, s));
-    // graphs for this (B, Lmax); max_steps is baked into the stop kernel args -> part of the key
-    const int saved_cap = d->cfg.max_steps;
-    d->cfg.max_steps = max_steps;
-    auto key = std::make_pair(B * 1000003 + max_steps, Lmax);
+    { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+    auto key = std::make_tuple(B, Lmax, max_steps);
     auto it = d->graphs.find(key);
     if (it == d->graphs.end()) {
         Graphs g;
-        tts_status st = build_graph(d, B, Lmax, 1, &g.one);
-        if (!st) st = build_graph(d, B, Lmax, CHUNK, &g.chunk);
-        if (st) { d->cfg.max_steps = saved_cap; return st; }
+        tts_status st = build_graph(d, B, Lmax, max_steps, 0, 1, &g.step[0]);
+        if (!st) st = build_graph(d, B, Lmax, max_steps, 1, 1, &g.step[1]);
+        if (!st) st = build_graph(d, B, Lmax, max_steps, 0, CHUNK, &g.chunk);
+        if (st) return st;
         it = d->graphs.emplace(key, g).first;
     }
-    d->cfg.max_steps = saved_cap;
     const Graphs& g = it->second;
     TTS_HIP(hipEventRecord(d->ev_t0, s));
-    int run = 0;
+    int run = 0;  // steps enqueued; the next step has parity run & 1
     auto launch_steps = [&](int n) -> tts_status {
-        for (; n >= CHUNK; n -= CHUNK, run += CHUNK) TTS_HIP(hipGraphLaunch(g.chunk, s));
-        for (; n > 0; --n, ++run) TTS_HIP(hipGraphLaunch(g.one, s));
+        while (n > 0) {
+            if ((run & 1) == 0 && n >= CHUNK) {
+                TTS_HIP(hipGraphLaunch(g.chunk, s));
+                run += CHUNK;
+                n -= CHUNK;
+            } else {
+                TTS_HIP(hipGraphLaunch(g.step[run & 1], s));
+                ++run;
+                --n;
+            }
+        }
         return TTS_OK;
     };
     tts_status st = launch_steps(first);
     if (st) return st;
     for (;;) {
-        TTS_HIP(hipMemcpyAsync(d->host_flags, d->n_active, sizeof(int), hipMemcpyDeviceToHost, s));
+        // n_active as seen by the next step (its parity slot)
+        TTS_HIP(hipMemcpyAsync(d->host_flags, d->state + 2 * (run & 1), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
         TTS_HIP(hipStreamSynchronize(s));
-        if (d->host_flags[0] == 0) break;
+        if (d->host_flags[1] == 0) break;
         TTS_CHECK(run < max_steps + 20, TTS_ERR_HIP, "decoder did not stop within max_steps + 20 (internal error)");
         st = launch_steps(CHUNK);
         if (st) return st;
@@ -470,6 +497,8 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     if (align)
         TTS_HIP(hipMemcpy2DAsync(align, (size_t)steps_cap * Lmax * 4, d->align_hist, (size_t)d->hist_cap * Lmax * 4,
                                  (size_t)nmax * Lmax * 4, B, hipMemcpyDeviceToDevice, s));
+    // the mel history is written unguarded by done[] (see EPI_MEL_FUSED): zero rows past n_steps
+    TTS_HIP(launch_zero_tail(mel, (int64_t)steps_cap * nm, d->n_steps, (int)nm, nmax, B, s));
     TTS_HIP(hipEventRecord(d->ev_out, s));
     TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
     TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
@@ -482,6 +511,13 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     return TTS_OK;
 }
 
+tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run) {
+    TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
+    *loop_ms = d->last_ms;
+    *steps_run = d->last_steps;
+    return TTS_OK;
+}
+
 tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n_kernels) {
     TTS_CHECK(d && kernel_ms && n_kernels >= TTS_DECODER_STEP_KERNELS, TTS_ERR_INVALID, "bad profile arguments");
     TTS_CHECK(d->last_B > 0, TTS_ERR_INVALID, "tts_decoder_profile needs a previous tts_decoder_run");
@@ -491,13 +527,11 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
     hipEvent_t ev[K + 1];
     for (int i = 0; i <= K; ++i) TTS_HIP(hipEventCreate(&ev[i]));
     hipStream_t s = d->stream;
-    const int saved_cap = d->cfg.max_steps;
-    d->cfg.max_steps = d->last_max_steps;
     TTS_HIP(launch_decoder_init(d->last_init, s));
+    tts_status st = enqueue_prenet_go(d, d->last_B, s);
     std::vector<double> acc(K, 0.0);
-    tts_status st = TTS_OK;
     for (int r = 0; r < reps && st == TTS_OK; ++r) {
-        st = enqueue_step(d, d->last_B, d->last_Lmax, s, ev);
+        st = enqueue_step(d, d->last_B, d->last_Lmax, d->last_max_steps, r & 1, s, ev);
         if (st) break;
         TTS_HIP(hipEventSynchronize(ev[K]));
         for (int i = 0; i < K; ++i) {
@@ -506,17 +540,9 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
             acc[i] += ms;
         }
     }
-    d->cfg.max_steps = saved_cap;
     for (int i = 0; i <= K; ++i) (void)hipEventDestroy(ev[i]);
     if (st) return st;
     for (int i = 0; i < K; ++i) kernel_ms[i] = (float)(acc[i] / reps);
-    return TTS_OK;
-}
-
-tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run) {
-    TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
-    *loop_ms = d->last_ms;
-    *steps_run = d->last_steps;
     return TTS_OK;
 }
 

@@ -1,17 +1,22 @@
 // Batched Griffin-Lim vocoder (AudioProcessor.inv_mel_spectrogram / inv_spectrogram,
 // utils/audio.py:154-201, librosa 0.6.2 stft/istft semantics) for gfx950.
 //
+// Precision follows the reference exactly where it is observable: the magnitude |S|^power and
+// every FFT are float64 (scipy.fftpack on float64 frames), the STFT matrix is rounded to
+// complex64 before the phase is taken (librosa stft's dtype), and the overlap-added signal y is
+// float32 (librosa istft's dtype), accumulated frame by frame in float32 as librosa does.  GL
+// amplifies rounding ~100x over 60 iterations, so this is what keeps the waveform within 1e-4.
+//
 // HBM layout (per call):
-//   S      [B][Fmax][1025]       |S|^power, frame-major (one 4.1 KB row per frame)
-//   frames [2][B][Fmax][WINP]    windowed inverse-FFT output of every frame, window support only
-//                                (WIN = 1102 samples; the padded Hann is zero elsewhere)
+//   S      [B][Fmax][1025] f64    |S|^power, frame-major (one 8.2 KB row per frame)
+//   frames [2][B][Fmax][WINP] f64 windowed inverse-FFT output of every frame, window support only
+//                                 (WIN = 1102 samples; the padded Hann is zero elsewhere)
 // One workgroup per (sentence, frame) per iteration does the whole GL iteration for its frame:
 //   overlap-add gather of the previous iteration's frames (<= 5 contributors per sample) with the
 //   window-sum-square normalisation and the STFT's reflect padding -> window -> 2048-point real
-//   FFT (1024-point complex Stockham radix-4 in LDS) -> X/|X| * S -> inverse real FFT -> window
+//   FFT (1024-point complex Stockham radix-4 in LDS) -> S * X/|X| -> inverse real FFT -> window
 //   -> store the frame.  Iterations ping-pong the frames buffer (a frame's neighbours still read
 //   the previous iteration), one launch per iteration, replayed from a hipGraph.
-// Roofline: HBM-bound by the algorithm's 6300 B per frame-iteration.
 #include <cmath>
 #include <map>
 #include <tuple>
@@ -27,51 +32,56 @@ constexpr int NFFT = 2048;
 constexpr int NB = 1025;  // bins
 constexpr int NH = 1024;  // complex FFT size
 constexpr int GL_THREADS = 256;
+constexpr int MAG_FRAMES = 4;  // frames per workgroup in the magnitude kernel
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_PER = 8;  // samples per thread per scan tile
 
 struct Geo {
     int hop, win, woff, winp;  // woff = (NFFT - win) / 2, winp = win rounded up to 4
 };
 
 struct GLConst {
-    const float* win;   // [2048] padded periodic Hann
-    const float* win2;  // [2048] win^2
-    const float2* tw;   // [2048] e^{-2 pi i m / 2048}
+    const double* win;    // [2048] padded periodic Hann
+    const double* win2;   // [2048] win^2
+    const double2* tw;    // [2048] e^{-2 pi i m / 2048}
 };
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return float2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
-__device__ __forceinline__ float2 cconj(float2 a) { return float2{a.x, -a.y}; }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return double2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ double2 cconj(double2 a) { return double2{a.x, -a.y}; }
 
-// Stockham radix-4, 5 passes, 256 threads x 1 butterfly.  src -> result in dst (returned).
+// Stockham radix-4, 5 passes, 256 threads x 1 butterfly.  Returns the buffer holding the result.
 template <bool INV>
-__device__ float2* fft1024(float2* src, float2* dst, const float2* __restrict__ tw) {
+__device__ double2* fft1024(double2* src, double2* dst, const double2* __restrict__ tw) {
     const int j = threadIdx.x;
 #pragma unroll
     for (int Ns = 1; Ns < NH; Ns *= 4) {
         const int k = j & (Ns - 1);
-        float2 v[4];
+        double2 v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = src[j + r * 256];
         if (Ns > 1) {
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
-                float2 w = tw[k * r * (512 / Ns)];
+                double2 w = tw[k * r * (512 / Ns)];
                 if (INV) w = cconj(w);
                 v[r] = cmul(v[r], w);
             }
         }
-        const float2 a0 = float2{v[0].x + v[2].x, v[0].y + v[2].y};
-        const float2 a1 = float2{v[0].x - v[2].x, v[0].y - v[2].y};
-        const float2 a2 = float2{v[1].x + v[3].x, v[1].y + v[3].y};
-        const float2 a3 = float2{v[1].x - v[3].x, v[1].y - v[3].y};
+        const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
+        const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
+        const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
+        const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
         // -i*a3 = (a3.y, -a3.x); +i*a3 = (-a3.y, a3.x)
-        const float2 m3 = INV ? float2{-a3.y, a3.x} : float2{a3.y, -a3.x};
+        const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
         const int idxD = (j / Ns) * Ns * 4 + k;
-        dst[idxD] = float2{a0.x + a2.x, a0.y + a2.y};
-        dst[idxD + Ns] = float2{a1.x + m3.x, a1.y + m3.y};
-        dst[idxD + 2 * Ns] = float2{a0.x - a2.x, a0.y - a2.y};
-        dst[idxD + 3 * Ns] = float2{a1.x - m3.x, a1.y - m3.y};
+        dst[idxD] = double2{a0.x + a2.x, a0.y + a2.y};
+        dst[idxD + Ns] = double2{a1.x + m3.x, a1.y + m3.y};
+        dst[idxD + 2 * Ns] = double2{a0.x - a2.x, a0.y - a2.y};
+        dst[idxD + 3 * Ns] = double2{a1.x - m3.x, a1.y - m3.y};
         __syncthreads();
-        float2* t = src;
+        double2* t = src;
         src = dst;
         dst = t;
     }
@@ -94,20 +104,21 @@ __device__ __forceinline__ int reflect_idx(int p, int N) {
     return pp < N ? pp : period - pp;
 }
 
-// y[p] of the previous iteration's iSTFT: overlap-add of the frames covering OLA position
-// q = p + n_fft/2, divided by the window sum-square where it exceeds float32 tiny.
-__device__ __forceinline__ float ola_sample(const float* __restrict__ fr, int q, int F, const Geo& g,
-                                            const float* __restrict__ win2) {
+// float32 y[p] of the previous iteration's iSTFT (librosa istft): float64 frame contributions
+// added frame by frame into a float32 accumulator, divided (float32) by the float32 window
+// sum-square where it exceeds float32 tiny.  q = p + n_fft/2 is the untrimmed position.
+__device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q, int F, const Geo& g,
+                                            const double* __restrict__ win2) {
+    if (q < g.woff) return 0.f;
     int ilo = q - g.woff - g.win + 1;
     ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
-    if (q < g.woff) return 0.f;
     int ihi = (q - g.woff) / g.hop;
     if (ihi > F - 1) ihi = F - 1;
     float y = 0.f, wss = 0.f;
     for (int i = ilo; i <= ihi; ++i) {
         const int o = q - i * g.hop;  // offset inside frame i (0..2047)
-        y += fr[(int64_t)i * g.winp + (o - g.woff)];
-        wss += win2[o];
+        y = (float)((double)y + fr[(int64_t)i * g.winp + (o - g.woff)]);
+        wss = (float)((double)wss + win2[o]);
     }
     return wss > 1.17549435e-38f ? y / wss : y;
 }
@@ -118,14 +129,15 @@ struct MagArgs {
     const float* spec;
     int n_in, Fmax;
     const int* F;
-    const float* pinv;  // [1025][n_mels]
-    float* S;
+    const double* pinv;  // [1025][n_mels]
+    double* S;
     float min_db, ref_db, power, max_norm;
     int signal_norm, symmetric, clip;
 };
 
+// _denormalize (utils/audio.py:96-112) then _db_to_amp(x + ref_level_db) (:125-126), in float32
+// as numpy computes them on the float32 network output.
 __device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) {
-    // _denormalize (utils/audio.py:96-112) then _db_to_amp(x + ref_level_db) (:125-126)
     float d = x;
     if (a.signal_norm) {
         if (a.symmetric) {
@@ -141,39 +153,43 @@ __device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) {
 
 __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     const int b = blockIdx.y;
-    const int f0 = blockIdx.x * 16;
+    const int f0 = blockIdx.x * MAG_FRAMES;
     const int Fb = a.F[b];
     if (f0 >= Fb) return;
-    const int nf = min(16, Fb - f0);
+    const int nf = min(MAG_FRAMES, Fb - f0);
     const float* sp = a.spec + ((int64_t)b * a.Fmax + f0) * a.n_in;
-    float* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
+    double* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
     if (a.mode == TTS_GL_FROM_LINEAR) {
-        for (int i = threadIdx.x; i < nf * NB; i += blockDim.x) S[i] = powf(denorm_to_amp(sp[i], a), a.power);
+        // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160)
+        for (int i = threadIdx.x; i < nf * NB; i += blockDim.x) S[i] = (double)powf(denorm_to_amp(sp[i], a), a.power);
         return;
     }
-    __shared__ float amp[16][80];
-    for (int i = threadIdx.x; i < nf * a.n_in; i += blockDim.x) amp[i / a.n_in][i % a.n_in] = denorm_to_amp(sp[i], a);
+    __shared__ double amp[MAG_FRAMES][80];
+    for (int i = threadIdx.x; i < MAG_FRAMES * a.n_in; i += blockDim.x) {
+        const int f = i / a.n_in, m = i % a.n_in;
+        amp[f][m] = f < nf ? (double)denorm_to_amp(sp[f * a.n_in + m], a) : 0.0;
+    }
     __syncthreads();
-    // _mel_to_linear: max(1e-10, pinv(M) . S)  (utils/audio.py:64-66), then ** power
+    // _mel_to_linear: max(1e-10, pinv(M) . S) in float64 (utils/audio.py:64-66), then ** power
     for (int k = threadIdx.x; k < NB; k += blockDim.x) {
-        const float* pr = a.pinv + (int64_t)k * a.n_in;
-        float acc[16];
+        const double* pr = a.pinv + (int64_t)k * a.n_in;
+        double acc[MAG_FRAMES];
 #pragma unroll
-        for (int f = 0; f < 16; ++f) acc[f] = 0.f;
+        for (int f = 0; f < MAG_FRAMES; ++f) acc[f] = 0.0;
         for (int m = 0; m < a.n_in; ++m) {
-            const float w = pr[m];
+            const double w = pr[m];
 #pragma unroll
-            for (int f = 0; f < 16; ++f) acc[f] += w * amp[f][m];
+            for (int f = 0; f < MAG_FRAMES; ++f) acc[f] += w * amp[f][m];
         }
-        for (int f = 0; f < nf; ++f) S[(int64_t)f * NB + k] = powf(fmaxf(acc[f], 1e-10f), a.power);
+        for (int f = 0; f < nf; ++f) S[(int64_t)f * NB + k] = pow(fmax(acc[f], 1e-10), (double)a.power);
     }
 }
 
 // ---------------------------------------------------------------- GL iteration
 struct IterArgs {
-    const float* S;       // [B][Fmax][1025]
-    const float* prev;    // frames of the previous iteration (null for the initial iSTFT)
-    float* next;          // frames written by this iteration
+    const double* S;      // [B][Fmax][1025]
+    const double* prev;   // frames of the previous iteration (null for the initial iSTFT)
+    double* next;         // frames written by this iteration
     const int* F;
     int Fmax;
     int B;
@@ -199,38 +215,40 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     if (f >= Fb) return;
     const Geo g = a.g;
     const int tid = threadIdx.x;
-    __shared__ __align__(16) float2 buf0[NH];
-    __shared__ __align__(16) float2 buf1[NH];
-    __shared__ __align__(16) float2 X[NB + 3];
-    const float* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    __shared__ __align__(16) double2 buf0[NH];
+    __shared__ __align__(16) double2 buf1[NH];
+    __shared__ __align__(16) double2 X[NB + 1];
+    const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
 
     if (!INIT) {
-        // ---- STFT frame f of the previous iteration's signal (librosa stft, centre reflect pad)
+        // ---- STFT frame f of the previous iteration's float32 signal (librosa stft, centre reflect pad)
         const int N = g.hop * (Fb - 1);
-        const float* fr = a.prev + (int64_t)b * a.Fmax * g.winp;
-        float* xr = reinterpret_cast<float*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
+        const double* fr = a.prev + (int64_t)b * a.Fmax * g.winp;
+        double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
         for (int n = tid; n < NFFT; n += GL_THREADS) {
-            const float w = a.c.win[n];
-            float v = 0.f;
-            if (w != 0.f) {
+            const double w = a.c.win[n];
+            double v = 0.0;
+            if (w != 0.0) {
                 const int p = reflect_idx(f * g.hop + n - NFFT / 2, N);
-                v = w * ola_sample(fr, p + NFFT / 2, Fb, g, a.c.win2);
+                v = w * (double)ola_sample(fr, p + NFFT / 2, Fb, g, a.c.win2);
             }
             xr[n] = v;
         }
         __syncthreads();
-        float2* Z = fft1024<false>(buf0, buf1, a.c.tw);
-        // real-FFT split + phase projection: X_k <- S_k * X_k / |X_k|   (angle(0) = 0 -> 1)
+        const double2* Z = fft1024<false>(buf0, buf1, a.c.tw);
+        // real-FFT split; the STFT value is stored complex64 (librosa stft dtype) and its phase
+        // exp(i angle(X)) (angle(0) = 0) is applied to |S| in float64 (utils/audio.py:187-188)
         for (int k = tid; k < NB; k += GL_THREADS) {
-            const float2 zk = Z[k & (NH - 1)];
-            const float2 zc = cconj(Z[(NH - k) & (NH - 1)]);
-            const float2 E = float2{0.5f * (zk.x + zc.x), 0.5f * (zk.y + zc.y)};
-            const float2 O = float2{0.5f * (zk.y - zc.y), -0.5f * (zk.x - zc.x)};  // -i (zk - zc) / 2
-            const float2 Xk = float2{E.x + (a.c.tw[k].x * O.x - a.c.tw[k].y * O.y),
-                                     E.y + (a.c.tw[k].x * O.y + a.c.tw[k].y * O.x)};
-            const float r = sqrtf(Xk.x * Xk.x + Xk.y * Xk.y);
-            const float s = Sf[k];
-            X[k] = r > 0.f ? float2{s * (Xk.x / r), s * (Xk.y / r)} : float2{s, 0.f};
+            const double2 zk = Z[k & (NH - 1)];
+            const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
+            const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
+            const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};  // -i (zk - zc) / 2
+            const double2 t = a.c.tw[k];
+            const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
+            const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
+            const double r = sqrt(xre * xre + xim * xim);
+            const double s = Sf[k];
+            X[k] = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
         }
     } else {
         // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183)
@@ -239,40 +257,39 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
             sincos(2.0 * M_PI * u, &sn, &cs);
-            const float s = Sf[k];
-            X[k] = float2{(float)(s * cs), (float)(s * sn)};
+            const double s = Sf[k];
+            X[k] = double2{s * cs, s * sn};
         }
     }
     __syncthreads();
     // ---- inverse real FFT (istft: ifft of the Hermitian-extended spectrum, .real => Im X_0 = Im X_N/2 = 0)
     if (tid == 0) {
-        X[0].y = 0.f;
-        X[NB - 1].y = 0.f;
+        X[0].y = 0.0;
+        X[NB - 1].y = 0.0;
     }
     __syncthreads();
     for (int k = tid; k < NH; k += GL_THREADS) {
-        const float2 xk = X[k];
-        const float2 xc = cconj(X[NH - k]);
-        const float2 E = float2{0.5f * (xk.x + xc.x), 0.5f * (xk.y + xc.y)};
-        const float2 D = float2{0.5f * (xk.x - xc.x), 0.5f * (xk.y - xc.y)};
-        const float2 w = cconj(a.c.tw[k]);
-        const float2 O = cmul(D, w);
-        buf0[k] = float2{E.x - O.y, E.y + O.x};  // E + i O
+        const double2 xk = X[k];
+        const double2 xc = cconj(X[NH - k]);
+        const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
+        const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
+        const double2 O = cmul(D, cconj(a.c.tw[k]));
+        buf0[k] = double2{E.x - O.y, E.y + O.x};  // E + i O
     }
     __syncthreads();
-    const float2* z = fft1024<true>(buf0, buf1, a.c.tw);
-    // ---- window and store the support [woff, woff+win)
-    float* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
-    const float* zr = reinterpret_cast<const float*>(z);
+    const double2* z = fft1024<true>(buf0, buf1, a.c.tw);
+    // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft)
+    double* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
+    const double* zr = reinterpret_cast<const double*>(z);
     for (int n = tid; n < g.win; n += GL_THREADS) {
         const int m = g.woff + n;
-        out[n] = a.c.win[m] * (zr[m] * (1.f / NH));
+        out[n] = a.c.win[m] * (zr[m] * (1.0 / NH));
     }
 }
 
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
 struct FinArgs {
-    const float* frames;
+    const double* frames;
     const int* F;
     int Fmax, B;
     Geo g;
@@ -290,44 +307,64 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     a.y[(int64_t)b * a.Nmax + p] = ola_sample(a.frames + (int64_t)b * a.Fmax * a.g.winp, p + NFFT / 2, Fb, a.g, a.c.win2);
 }
 
-// y[n] = x[n] + c*y[n-1] (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136), fp64.
-// One workgroup per sentence: chunked scan, carries combined serially in fixed order.
-__global__ __launch_bounds__(1024) void preemph_scan_kernel(const float* y, int64_t Nmax, const int* F, int hop,
-                                                            double coef, int apply, double* wav) {
+// y[n] = x[n] + c*y[n-1] in float64 (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136).
+// One workgroup per sentence, tiles of SCAN_THREADS*SCAN_PER samples: coalesced tile load into
+// LDS, per-thread serial scan, Hillis-Steele scan of the (c^len, value) carries, coalesced store.
+__global__ __launch_bounds__(SCAN_THREADS) void preemph_scan_kernel(const float* y, int64_t Nmax, const int* F, int hop,
+                                                                    double coef, int apply, double* wav) {
     const int b = blockIdx.x;
     const int64_t N = (int64_t)hop * (F[b] - 1);
     const float* x = y + (int64_t)b * Nmax;
     double* o = wav + (int64_t)b * Nmax;
-    const int T = blockDim.x, tid = threadIdx.x;
-    const int64_t chunk = (N + T - 1) / T;
-    const int64_t s0 = tid * chunk, s1 = s0 + chunk < N ? s0 + chunk : N;
-    __shared__ double endv[1024];
-    __shared__ double powc[1024];
-    __shared__ double carry[1025];
+    const int tid = threadIdx.x;
     if (!apply) {
-        for (int64_t i = tid; i < N; i += T) o[i] = (double)x[i];
+        for (int64_t i = tid; i < N; i += blockDim.x) o[i] = (double)x[i];
         return;
     }
-    double acc = 0.0, pc = 1.0;
-    for (int64_t i = s0; i < s1; ++i) {
-        acc = (double)x[i] + coef * acc;
-        pc *= coef;
-    }
-    endv[tid] = acc;
-    powc[tid] = pc;
-    __syncthreads();
-    if (tid == 0) {
-        double c = 0.0;
-        for (int i = 0; i < T; ++i) {
-            carry[i] = c;
-            c = endv[i] + powc[i] * c;
+    constexpr int TILE = SCAN_THREADS * SCAN_PER;
+    __shared__ double tile[TILE];
+    __shared__ double sa[SCAN_THREADS], sb[SCAN_THREADS];
+    double cpow[SCAN_PER + 1];
+    cpow[0] = 1.0;
+    for (int k = 1; k <= SCAN_PER; ++k) cpow[k] = cpow[k - 1] * coef;
+    double carry = 0.0;  // y at the end of the previous tile
+    for (int64_t t0 = 0; t0 < N; t0 += TILE) {
+        for (int i = tid; i < TILE; i += SCAN_THREADS) tile[i] = t0 + i < N ? (double)x[t0 + i] : 0.0;
+        __syncthreads();
+        // local serial scan of this thread's SCAN_PER samples with zero carry-in
+        double v = 0.0;
+        double loc[SCAN_PER];
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; ++k) {
+            v = tile[tid * SCAN_PER + k] + coef * v;
+            loc[k] = v;
         }
-    }
-    __syncthreads();
-    acc = carry[tid];
-    for (int64_t i = s0; i < s1; ++i) {
-        acc = (double)x[i] + coef * acc;
-        o[i] = acc;
+        // inclusive scan of (A, B) pairs, y_end = A * y_in + B; combine (A1,B1) then (A2,B2) = (A1 A2, B1 A2 + B2)
+        double A = cpow[SCAN_PER], Bv = v;
+        for (int off = 1; off < SCAN_THREADS; off <<= 1) {
+            sa[tid] = A;
+            sb[tid] = Bv;
+            __syncthreads();
+            if (tid >= off) {
+                const double pa = sa[tid - off], pb = sb[tid - off];
+                Bv = pb * A + Bv;
+                A = pa * A;
+            }
+            __syncthreads();
+        }
+        // exclusive carry into this thread = inclusive of the previous thread, applied to the tile carry-in
+        sa[tid] = A;
+        sb[tid] = Bv;
+        __syncthreads();
+        const double cin = tid == 0 ? carry : sa[tid - 1] * carry + sb[tid - 1];
+        const double tile_end = sa[SCAN_THREADS - 1] * carry + sb[SCAN_THREADS - 1];
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; ++k) tile[tid * SCAN_PER + k] = loc[k] + cpow[k + 1] * cin;
+        __syncthreads();
+        for (int i = tid; i < TILE; i += SCAN_THREADS)
+            if (t0 + i < N) o[t0 + i] = tile[i];
+        carry = tile_end;
+        __syncthreads();
     }
 }
 
@@ -343,11 +380,12 @@ struct tts_gl {
     Geo g{};
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
-    float *win = nullptr, *win2 = nullptr, *pinv = nullptr;
-    float2* tw = nullptr;
+    double *win = nullptr, *win2 = nullptr, *pinv = nullptr;
+    double2* tw = nullptr;
     // workspace
-    size_t S_floats = 0, fr_floats = 0, y_floats = 0;
-    float *S = nullptr, *frames = nullptr, *y = nullptr;
+    size_t S_n = 0, fr_n = 0, y_n = 0;
+    double *S = nullptr, *frames = nullptr;
+    float* y = nullptr;
     int* F = nullptr;
     int Fcap_B = 0;
     std::map<GraphKey, hipGraphExec_t> graphs;
@@ -374,7 +412,7 @@ void tts_gl_destroy(tts_gl* g) {
     delete g;
 }
 
-tts_status tts_gl_create(const tts_audio_config* cfg, const float* inv_mel_basis, void* stream, tts_gl** out) {
+tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basis, void* stream, tts_gl** out) {
     TTS_CHECK(cfg && out, TTS_ERR_INVALID, "null argument");
     TTS_CHECK(cfg->n_fft == NFFT, TTS_ERR_UNSUPPORTED, "n_fft must be 2048 (num_freq 1025)");
     TTS_CHECK(cfg->win_length >= 2 && cfg->win_length <= NFFT, TTS_ERR_INVALID, "win_length must be in [2, n_fft]");
@@ -387,17 +425,15 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const float* inv_mel_basis
     g->g.win = cfg->win_length;
     g->g.woff = (NFFT - cfg->win_length) / 2;  // librosa util.pad_center
     g->g.winp = (cfg->win_length + 3) / 4 * 4;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    // host tables in double, rounded once
-    std::vector<float> win(NFFT, 0.f), win2(NFFT, 0.f);
+    (void)stream;
+    std::vector<double> win(NFFT, 0.0), win2(NFFT, 0.0);
     for (int n = 0; n < cfg->win_length; ++n) {
         const double w = 0.5 - 0.5 * std::cos(2.0 * M_PI * n / cfg->win_length);  // periodic Hann
-        win[g->g.woff + n] = (float)w;
-        win2[g->g.woff + n] = (float)(w * w);
+        win[g->g.woff + n] = w;
+        win2[g->g.woff + n] = w * w;
     }
-    std::vector<float2> tw(NFFT);
-    for (int m = 0; m < NFFT; ++m)
-        tw[m] = float2{(float)std::cos(2.0 * M_PI * m / NFFT), (float)-std::sin(2.0 * M_PI * m / NFFT)};
+    std::vector<double2> tw(NFFT);
+    for (int m = 0; m < NFFT; ++m) tw[m] = double2{std::cos(2.0 * M_PI * m / NFFT), -std::sin(2.0 * M_PI * m / NFFT)};
     auto fail = [&](hipError_t e, const char* what) {
         tts_status st = hip_fail(e, what, __FILE__, __LINE__);
         tts_gl_destroy(g);
@@ -409,19 +445,18 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const float* inv_mel_basis
     if ((e = hipEventCreateWithFlags(&g->ev_out, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreate(&g->ev_t0)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreate(&g->ev_t1)) != hipSuccess) return fail(e, "event");
-    if ((e = hipMalloc(&g->win, NFFT * 4)) != hipSuccess) return fail(e, "hipMalloc");
-    if ((e = hipMalloc(&g->win2, NFFT * 4)) != hipSuccess) return fail(e, "hipMalloc");
-    if ((e = hipMalloc(&g->tw, NFFT * sizeof(float2))) != hipSuccess) return fail(e, "hipMalloc");
-    if ((e = hipMemcpy(g->win, win.data(), NFFT * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
-    if ((e = hipMemcpy(g->win2, win2.data(), NFFT * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
-    if ((e = hipMemcpy(g->tw, tw.data(), NFFT * sizeof(float2), hipMemcpyHostToDevice)) != hipSuccess)
+    if ((e = hipMalloc(&g->win, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&g->win2, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&g->tw, NFFT * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMemcpy(g->win, win.data(), NFFT * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
+    if ((e = hipMemcpy(g->win2, win2.data(), NFFT * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
+    if ((e = hipMemcpy(g->tw, tw.data(), NFFT * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "copy");
     if (inv_mel_basis) {
         const size_t n = (size_t)NB * cfg->num_mels;
-        if ((e = hipMalloc(&g->pinv, n * 4)) != hipSuccess) return fail(e, "hipMalloc");
-        if ((e = hipMemcpy(g->pinv, inv_mel_basis, n * 4, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
+        if ((e = hipMalloc(&g->pinv, n * 8)) != hipSuccess) return fail(e, "hipMalloc");
+        if ((e = hipMemcpy(g->pinv, inv_mel_basis, n * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
     }
-    (void)s;
     *out = g;
     return TTS_OK;
 }
@@ -431,30 +466,28 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_CHECK(g && spec && F && wav && B >= 1 && Fmax >= 2 && iters >= 0, TTS_ERR_INVALID, "bad gl_run arguments");
     TTS_CHECK(mode == TTS_GL_FROM_MEL || mode == TTS_GL_FROM_LINEAR, TTS_ERR_INVALID, "bad mode");
     TTS_CHECK(mode == TTS_GL_FROM_LINEAR || g->pinv, TTS_ERR_INVALID, "mel mode needs inv_mel_basis at create");
-    if (mode == TTS_GL_FROM_LINEAR)
-        TTS_CHECK(g->cfg.power > 0, TTS_ERR_INVALID, "power must be > 0");
     for (int b = 0; b < B; ++b) TTS_CHECK(F[b] >= 2 && F[b] <= Fmax, TTS_ERR_INVALID, "F[b] out of range [2, Fmax]");
     hipStream_t cs = static_cast<hipStream_t>(stream);
     hipStream_t s = g->stream;
     const Geo geo = g->g;
     const int64_t Nmax = (int64_t)geo.hop * (Fmax - 1);
-    // workspace (grow only; graphs keyed on shapes are invalidated when buffers move)
+    // workspace (grow only; graphs bake the buffer addresses and are dropped when they move)
     const size_t needS = (size_t)B * Fmax * NB, needF = (size_t)2 * B * Fmax * geo.winp, needY = (size_t)B * Nmax;
     bool moved = false;
-    auto grow = [&](float** p, size_t& have, size_t need) -> tts_status {
+    auto grow = [&](void** p, size_t& have, size_t need, size_t elem) -> tts_status {
         if (need <= have) return TTS_OK;
         if (*p) TTS_HIP(hipFree(*p));
         *p = nullptr;
-        TTS_HIP(hipMalloc(p, need * 4));
+        TTS_HIP(hipMalloc(p, need * elem));
         have = need;
         moved = true;
         return TTS_OK;
     };
     TTS_HIP(hipStreamSynchronize(s));
     tts_status st;
-    if ((st = grow(&g->S, g->S_floats, needS))) return st;
-    if ((st = grow(&g->frames, g->fr_floats, needF))) return st;
-    if ((st = grow(&g->y, g->y_floats, needY))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, 8))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, 8))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->y), g->y_n, needY, 4))) return st;
     if (B > g->Fcap_B) {
         if (g->F) TTS_HIP(hipFree(g->F));
         g->F = nullptr;
@@ -484,7 +517,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ma.signal_norm = g->cfg.signal_norm;
     ma.symmetric = g->cfg.symmetric_norm;
     ma.clip = g->cfg.clip_norm;
-    hipLaunchKernelGGL(gl_magnitude_kernel, dim3((Fmax + 15) / 16, B), dim3(256), 0, s, ma);
+    hipLaunchKernelGGL(gl_magnitude_kernel, dim3((Fmax + MAG_FRAMES - 1) / MAG_FRAMES, B), dim3(256), 0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
     IterArgs ia{};
@@ -538,7 +571,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.Nmax = Nmax;
     hipLaunchKernelGGL(gl_ola_kernel, dim3((Nmax + 255) / 256, B), dim3(256), 0, s, fa);
     TTS_HIP(hipGetLastError());
-    hipLaunchKernelGGL(preemph_scan_kernel, dim3(B), dim3(1024), 0, s, g->y, Nmax, g->F, geo.hop,
+    hipLaunchKernelGGL(preemph_scan_kernel, dim3(B), dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop,
                        g->cfg.preemphasis, g->cfg.preemphasis != 0.0 ? 1 : 0, wav);
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_out, s));

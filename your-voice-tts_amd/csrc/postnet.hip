@@ -62,11 +62,15 @@ __global__ __launch_bounds__(256) void conv_k5_kernel(const ConvArgs a) {
     const int wc = (wave & 1) * 32;   // wave's channel offset in tile
     __shared__ float xs[BM + 2 * PAD][BK + 1];
     __shared__ float ws[BK][KW][BN];
-    floatx4 acc[2][2];
+    // one accumulator set per kernel tap: five 512-long fma chains instead of one 2560-long
+    // chain keeps the fp32 accumulation error near the reference's blocked CPU convolution
+    floatx4 acc[KW][2][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int k = 0; k < KW; ++k)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[k][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const float* inb = a.in + (int64_t)b * a.Tmax * a.Cin;
     for (int ci0 = 0; ci0 < a.Cin; ci0 += BK) {
         // stage input rows t0-2 .. t0+BM+1, channels ci0 .. ci0+15 (zero outside [0, T_b))
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(256) void conv_k5_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) acc[i][j] = mfma16x16x4(av[i], bv[j], acc[i][j]);
+                    for (int j = 0; j < 2; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
             }
         }
         __syncthreads();
@@ -118,7 +122,10 @@ __global__ __launch_bounds__(256) void conv_k5_kernel(const ConvArgs a) {
                 const int t = t0 + wt + i * 16 + (lane >> 4) * 4 + r;
                 const int co = c0 + wc + j * 16 + (lane & 15);
                 if (t < Tb && co < a.Cout) {
-                    float y = acc[i][j][r] * a.scale[co] + a.shift[co];
+                    float sum = acc[0][i][j][r];
+#pragma unroll
+                    for (int k = 1; k < KW; ++k) sum += acc[k][i][j][r];
+                    float y = sum * a.scale[co] + a.shift[co];
                     if (a.act_tanh) y = tanhf(y);
                     if (resb) y = resb[(int64_t)t * a.Cout + co] + y;
                     outb[(int64_t)t * a.Cout + co] = y;

@@ -22,10 +22,32 @@ struct Seg {
     int len;  // multiple of 16
 };
 
-enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1 };
-// Decoder stage a launch serves; fixes the epilogue (LSTM roles use EPI_LSTM).
-enum Role { ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4 };
+enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2 };
+// Decoder stage a launch serves; fixes the epilogue (LSTM roles use EPI_LSTM, ROLE_MEL_FUSED
+// uses EPI_MEL_FUSED).
+enum Role { ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4, ROLE_MEL_FUSED = 5 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1 };
+
+// EPI_MEL_FUSED: one GEMM over x = [h_dec | ctx] whose output rows are
+//   [0, nmel)            mel frame(s)                  -> history
+//   [nmel, nmel+256)     prenet layer-1 pre-activation -> relu -> pre1 (next step's prenet)
+//   nmel+256             stop-token logit              -> sigmoid -> history + stop rule
+// using weights folded at load time: W1' = W1 W_mel, w_stop' = [w_s_h | 0] + w_s_mel W_mel.
+struct MelFused {
+    int nmel;
+    float* pre1;
+    int ldp;
+    float* stop_hist;
+    int64_t stop_ldb;
+    const int* lens;
+    const float* tail;
+    int* flag1;
+    int* count;
+    int* done;
+    int* n_steps;
+    int* state_next;  // int2 {t+1, n_active} read by the next step (other parity slot)
+    int max_steps;
+};
 
 struct SGemmArgs {
     Seg seg[3];
@@ -45,9 +67,11 @@ struct SGemmArgs {
     int hist_cap;
     float* cell;  // LSTM cell state [b*ldc + unit], updated in place
     int ldc;
-    const int* step;      // device step counter or null (=0)
+    const int* step;      // int2 {step, n_active} of this step's parity slot, or null (= {0, 1});
+                          // the kernel exits early when n_active == 0
     const int* done;      // per-row done flags or null
-    const int* n_active;  // early exit when *n_active == 0, or null
+    const int* n_active;  // unused (kept adjacent to step)
+    MelFused mf;          // EPI_MEL_FUSED only
 };
 
 // Row maps used when repacking reference matrices.
@@ -63,5 +87,8 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
 inline size_t sgemm_packed_floats(int N, int K) { return (size_t)((N + 15) / 16) * 16 * K; }
 
 hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s);
+// Wf [nmel+257][K] logical rows + bf [nmel+257] for ROLE_MEL_FUSED (see MelFused).
+hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
+                            int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s);
 
 }  // namespace tts

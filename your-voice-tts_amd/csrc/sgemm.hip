@@ -9,17 +9,33 @@
 
 namespace tts {
 
-constexpr int MAX_WAVES = 8;
+constexpr int MAX_WAVES = 16;
+constexpr int PRE_DIM = 256;  // prenet width (layers/tacotron2.py:108)
 
 // ROLE only names the instantiation (distinct kernel names in rocprof traces per decoder stage).
 template <int MT, int EPI, int ROLE>
-__global__ __launch_bounds__(512) void sgemm_kernel(const SGemmArgs a) {
-    if (a.n_active && *a.n_active == 0) return;
+__global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
+    // {step, n_active} in one load (adjacent words), issued with the epilogue prefetches
+    const int2 st = a.step ? *reinterpret_cast<const int2*>(a.step) : make_int2(0, 1);
     const int ntile = blockIdx.x;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int nw = blockDim.x >> 6;
-    const int step = a.step ? *a.step : 0;
+    float pre_bias[4] = {0.f, 0.f, 0.f, 0.f}, pre_cell = 0.f;
+    if (EPI == EPI_LSTM && (int)threadIdx.x < a.B * 4) {
+        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
+        pre_cell = a.cell[(int64_t)b * a.ldc + ntile * 4 + u];
+    }
+    if (st.y == 0) {
+        // every sentence is done: steps past the end are no-ops, but the fused stop launch
+        // still forwards {step+1, 0} so the next parity slot reads "done" as well
+        if (EPI == EPI_MEL_FUSED && ntile == 0 && threadIdx.x == 0)
+            *reinterpret_cast<int2*>(a.mf.state_next) = make_int2(st.x + 1, 0);
+        return;
+    }
+    const int step = st.x;
     const int nchunks = a.K >> 4;
     const int cbeg = wave * nchunks / nw;
     const int cend = (wave + 1) * nchunks / nw;
@@ -44,12 +60,14 @@ __global__ __launch_bounds__(512) void sgemm_kernel(const SGemmArgs a) {
         cb[s] = kstart >> 4;  // first chunk past segment s
     }
 
-    floatx4 acc[MT];
+    // two independent accumulator chains per m-tile (even / odd chunk) hide the MFMA latency
+    floatx4 acc[MT], acc2[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = acc2[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const float4* __restrict__ Wp = reinterpret_cast<const float4*>(a.W) + (size_t)ntile * nchunks * 64 + lane;
-    constexpr int U = 4;
+    // U chunks of loads (U KiB of weights per wave) in flight before the first MFMA
+    constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
     for (int c0 = cbeg; c0 < cend; c0 += U) {
         float4 wv[U];
         float4 xv[U][MT];
@@ -71,16 +89,22 @@ __global__ __launch_bounds__(512) void sgemm_kernel(const SGemmArgs a) {
             }
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < U; u += 2) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 acc[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, acc[mt]);
+                acc2[mt] = mfma16x16x4(xv[u + 1][mt].x, wv[u + 1].x, acc2[mt]);
                 acc[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, acc[mt]);
+                acc2[mt] = mfma16x16x4(xv[u + 1][mt].y, wv[u + 1].y, acc2[mt]);
                 acc[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, acc[mt]);
+                acc2[mt] = mfma16x16x4(xv[u + 1][mt].z, wv[u + 1].z, acc2[mt]);
                 acc[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, acc[mt]);
+                acc2[mt] = mfma16x16x4(xv[u + 1][mt].w, wv[u + 1].w, acc2[mt]);
             }
         }
     }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] += acc2[mt];
 
     // Cross-wave K reduction in a fixed order.
     __shared__ float red[MAX_WAVES][MT][64][4];
@@ -115,20 +139,72 @@ __global__ __launch_bounds__(512) void sgemm_kernel(const SGemmArgs a) {
             if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
             if (track && !(a.done && a.done[b])) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
         }
+    } else if (EPI == EPI_MEL_FUSED) {
+        const MelFused& m = a.mf;
+        const int nrow = m.nmel + PRE_DIM + 1;
+        for (int e = threadIdx.x; e < a.B * 16; e += blockDim.x) {
+            const int b = e >> 4, col = e & 15;
+            const int n = ntile * 16 + col;
+            if (n >= nrow - 1) continue;  // stop row handled below
+            const float v = fin[b][col] + a.bias[n];
+            if (n < m.nmel) {
+                // unguarded by done[]: the stop WG of this same launch may set it; rows past
+                // n_steps are garbage the host masks out (tts_decoder_run zero-fills them)
+                if (track) a.hist[(int64_t)b * a.ldh + (int64_t)step * m.nmel + n] = v;
+            } else {
+                m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
+            }
+        }
+        const int stop_tile = (nrow - 1) >> 4;
+        if (ntile == stop_tile) {
+            // stopnet + stop rule (tacotron2.py:219-224, 257-277): stop_flags[0] is always true;
+            // [1] latches (tail > 0.8 and t > L); [2] = t > 2L; then 20 extra steps; the cap is
+            // checked only in the `elif`, so a sentence whose flags are all set may pass it.
+            __shared__ int sdone[64];
+            const int col = (nrow - 1) & 15;
+            const int b = threadIdx.x;
+            if (b < a.B) {
+                int nd = a.done[b];
+                if (!nd) {
+                    const float stv = sigmoidf_(fin[b][col] + a.bias[nrow - 1]);
+                    if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
+                    const int L = m.lens[b];
+                    const int f1 = m.flag1[b] | ((m.tail[b] > 0.8f && step > L) ? 1 : 0);
+                    m.flag1[b] = f1;
+                    if (f1 && step > 2 * L) {
+                        const int c = m.count[b] + 1;
+                        m.count[b] = c;
+                        if (c > 20) nd = 1;
+                    } else if (step + 1 == m.max_steps) {
+                        nd = 1;
+                    }
+                    if (nd) {
+                        m.done[b] = 1;
+                        m.n_steps[b] = step + 1;
+                    }
+                }
+                sdone[b] = nd;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                int na = 0;
+                for (int k = 0; k < a.B; ++k) na += sdone[k] ? 0 : 1;
+                *reinterpret_cast<int2*>(m.state_next) = make_int2(step + 1, na);
+            }
+        }
     } else {
         // LSTM cell (torch LSTMCell, gate order i, f, g, o): c' = s(f)c + s(i)tanh(g); h' = s(o)tanh(c')
         float* out = a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0);
-        for (int e = threadIdx.x; e < a.B * 4; e += blockDim.x) {
+        const int e = threadIdx.x;  // blockDim >= 256 >= B*4 for the LSTM shapes (K >= 1792)
+        if (e < a.B * 4) {
             const int b = e >> 2, u = e & 3;
             const int unit = ntile * 4 + u;
-            const float* bl = a.bias + ntile * 16;
-            const float gi = fin[b][u] + bl[u];
-            const float gf = fin[b][4 + u] + bl[4 + u];
-            const float gg = fin[b][8 + u] + bl[8 + u];
-            const float go = fin[b][12 + u] + bl[12 + u];
-            float* cp = a.cell + (int64_t)b * a.ldc + unit;
-            const float c2 = sigmoidf_(gf) * (*cp) + sigmoidf_(gi) * tanhf(gg);
-            *cp = c2;
+            const float gi = fin[b][u] + pre_bias[0];
+            const float gf = fin[b][4 + u] + pre_bias[1];
+            const float gg = fin[b][8 + u] + pre_bias[2];
+            const float go = fin[b][12 + u] + pre_bias[3];
+            const float c2 = sigmoidf_(gf) * pre_cell + sigmoidf_(gi) * tanhf(gg);
+            a.cell[(int64_t)b * a.ldc + unit] = c2;
             out[(int64_t)b * a.ldo + unit] = sigmoidf_(go) * tanhf(c2);
         }
     }
@@ -206,8 +282,42 @@ hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s) {
         case ROLE_QUERY: return launch_role<EPI_LINEAR, ROLE_QUERY>(a, s);
         case ROLE_DEC_LSTM: return launch_role<EPI_LSTM, ROLE_DEC_LSTM>(a, s);
         case ROLE_MEL: return launch_role<EPI_LINEAR, ROLE_MEL>(a, s);
+        case ROLE_MEL_FUSED: return launch_role<EPI_MEL_FUSED, ROLE_MEL_FUSED>(a, s);
         default: return hipErrorInvalidValue;
     }
+}
+
+// Folded weights of the fused mel/prenet-1/stop GEMM (logical row-major [nmel+257][K], fp64
+// accumulation, rounded once):  rows [0,nmel) = W_mel;  [nmel, nmel+256) = W1 W_mel;
+// nmel+256 = [w_s_h | 0] + w_s_mel W_mel.  Biases b_mel, W1 b_mel, b_s + w_s_mel b_mel.
+__global__ void fold_mel_kernel(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
+                                int nmel, int K, int hdec, float* Wf, float* bf) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nrow = nmel + PRE_DIM + 1;
+    if (i >= (int64_t)nrow * (K + 1)) return;
+    const int n = i / (K + 1), k = i % (K + 1);  // k == K: bias
+    double v = 0.0;
+    if (n < nmel) {
+        v = k < K ? Wm[(int64_t)n * K + k] : bm[n];
+    } else if (n < nmel + PRE_DIM) {
+        const float* w1 = W1 + (int64_t)(n - nmel) * nmel;
+        for (int m = 0; m < nmel; ++m) v += (double)w1[m] * (k < K ? Wm[(int64_t)m * K + k] : bm[m]);
+    } else {
+        v = k < K ? (k < hdec ? ws[k] : 0.0) : bs[0];
+        for (int m = 0; m < nmel; ++m) v += (double)ws[hdec + m] * (k < K ? Wm[(int64_t)m * K + k] : bm[m]);
+    }
+    if (k < K)
+        Wf[(int64_t)n * K + k] = (float)v;
+    else
+        bf[n] = (float)v;
+}
+
+hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
+                            int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s) {
+    const int64_t total = (int64_t)(nmel + PRE_DIM + 1) * (K + 1);
+    hipLaunchKernelGGL(fold_mel_kernel, dim3((total + 255) / 256), dim3(256), 0, s, Wm, bm, W1, ws, bs, nmel, K, hdec,
+                       Wf, bf);
+    return hipGetLastError();
 }
 
 }  // namespace tts

@@ -169,6 +169,7 @@ class Tacotron2:
             self._lstm = lstm
         return self._lstm
 
+    @torch.no_grad()
     def encode(self, ids: torch.Tensor, lens, speaker_ids=None):
         """Embedding + Encoder.inference (models/tacotron2.py:63-66, layers/tacotron2.py:78-83)
         on a padded batch; every sentence sees zero padding past its own length, as alone."""
