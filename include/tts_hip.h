@@ -32,6 +32,7 @@ typedef int tts_status;
 #define TTS_ERR_UNSUPPORTED 3 /* configuration the path does not implement        */
 #define TTS_ERR_NOMEM 4
 
+typedef struct tts_encoder tts_encoder;
 typedef struct tts_decoder tts_decoder;
 typedef struct tts_postnet tts_postnet;
 typedef struct tts_gl tts_gl;
@@ -42,6 +43,19 @@ typedef struct tts_tensor {
     const float* data; /* [dev] fp32                                                        */
     int64_t numel;
 } tts_tensor;
+
+/* Replaces the embedding lookup + Encoder.inference of Tacotron2.inference (models/tacotron2.py:
+ * 63-64, layers/tacotron2.py:48-83): 3 x (Conv1d k=5 + BatchNorm + ReLU) and the bidirectional
+ * LSTM.  `tensors` must hold embedding.weight and every encoder.* key. */
+tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_batch, int max_len,
+                              void* stream, tts_encoder** out);
+void tts_encoder_destroy(tts_encoder* e);
+/*   ids  [dev]  int32 [B][Lmax] character ids (entries past lens[b] ignored)
+ *   lens [host] int32 [B], 1 <= lens[b] <= Lmax
+ *   out  [dev]  fp32 [B][Lmax][512]; each sentence is encoded at its own length, rows past
+ *                lens[b] are zero. */
+tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
+                           float* out, void* stream);
 
 /* Decoder flags: the arguments of layers/tacotron2.py:98-100 (Decoder.__init__) that change
  * inference numerics, as mapped from the JSON config by utils/generic_utils.py:275-288. */

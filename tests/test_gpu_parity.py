@@ -68,6 +68,32 @@ def test_full_inference_vs_reference(case):
     np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"].argmax(1))
 
 
+@pytest.mark.parametrize("case", ["t2_fwdmask_L12", "t2_fwdmask_L40", "t2_fwdmask_L100"])
+def test_encoder_vs_reference(case):
+    """HIP encoder (embedding + 3 conv/BN/ReLU + BiLSTM) vs the reference's encoder outputs."""
+    z = golden(case)
+    m = _model(golden_flags(z))
+    L = len(z["ids"])
+    enc = m.encode(torch.from_numpy(z["ids"])[None].cuda(), [L])
+    assert rel_rms(enc[0].cpu().numpy(), z["enc"]) < MEL_RTOL
+
+
+def test_encoder_ragged_batch():
+    """Padded batch: each sentence encoded at its own length (reverse LSTM starts at L_b-1),
+    rows past L_b are zero."""
+    cases = ["t2_fwdmask_L40", "t2_fwdmask_L100", "t2_fwdmask_L12"]
+    zs = [golden(c) for c in cases]
+    m = _model(golden_flags(zs[0]))
+    lens = [len(z["ids"]) for z in zs]
+    ids = torch.zeros(len(zs), max(lens), dtype=torch.long)
+    for b, z in enumerate(zs):
+        ids[b, :lens[b]] = torch.from_numpy(z["ids"])
+    enc = m.encode(ids.cuda(), lens).cpu().numpy()
+    for b, z in enumerate(zs):
+        assert rel_rms(enc[b, :lens[b]], z["enc"]) < MEL_RTOL
+        assert np.all(enc[b, lens[b]:] == 0)
+
+
 def test_batched_ragged_decoder_matches_batch1():
     """A padded batch: every sentence gets exactly its batch-1 reference result."""
     cases = ["t2_fwdmask_L40", "t2_fwdmask_L12", "t2_fwdmask_L100", "t2_fwdmask_L12", "t2_fwdmask_L40"]

@@ -19,6 +19,7 @@ GL_KERNELS = ("gl_iter", "gl_ola")
 
 # every symbol include/tts_hip.h declares
 EXPORTS = (
+    "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_last_timing",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
@@ -53,6 +54,11 @@ I32P = ctypes.POINTER(ctypes.c_int32)
 
 def _declare(lib):
     vp = ctypes.c_void_p
+    lib.tts_encoder_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, ctypes.c_int, vp,
+                                       ctypes.POINTER(vp)]
+    lib.tts_encoder_destroy.argtypes = [vp]
+    lib.tts_encoder_destroy.restype = None
+    lib.tts_encoder_run.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
     lib.tts_decoder_create.argtypes = [ctypes.POINTER(DecoderConfig), ctypes.POINTER(TensorView), ctypes.c_int, vp,
                                        ctypes.POINTER(vp)]
     lib.tts_decoder_destroy.argtypes = [vp]

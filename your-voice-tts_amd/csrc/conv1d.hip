@@ -1,0 +1,175 @@
+// fp32 MFMA implicit-GEMM Conv1d (see conv1d.h).
+//
+//   out[b][t][co] = act( scale[co] * sum_{k<KW} sum_ci in[b][t+k-PAD][ci] * W[co][ci][k] + shift[co] ) (+ resid)
+//
+// GEMM view: M = frames, N = output channels, K = (tap, input channel).  A workgroup owns a
+// BM x 64 output tile; per 16-channel K step it stages the BM+KW-1 input rows and the
+// 16 x KW x 64 weight slab in LDS, then each wave issues v_mfma_f32_16x16x4_f32 on its
+// (BM/WM) x (64/WN) sub-tile.  One accumulator set per tap keeps the fp32 fma chains short
+// (Cin long instead of KW*Cin).  Two tile shapes: BM=64 (2x2 waves of 32x32) for large batches,
+// BM=16 (1x4 waves of 16x16) so that a single sentence still spreads over >= 100 workgroups.
+#include "conv1d.h"
+
+namespace tts {
+
+namespace {
+
+template <int KW, int BM, int WM, int WN>
+__global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
+    constexpr int PAD = (KW - 1) / 2;
+    constexpr int BK = 16;
+    constexpr int BN = CONV_BN;
+    constexpr int TM = BM / WM / 16;
+    constexpr int TN = BN / WN / 16;
+    const int b = blockIdx.z;
+    const int t0 = blockIdx.x * BM;
+    const int c0 = blockIdx.y * BN;
+    const int Tb = a.T[b];
+    if (t0 >= Tb) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wt = (wave / WN) * (BM / WM);
+    const int wc = (wave % WN) * (BN / WN);
+    __shared__ float xs[BM + KW - 1][BK + 1];
+    __shared__ __align__(16) float ws[BK][KW][BN];
+    floatx4 acc[KW][TM][TN];
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[k][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int ci0 = 0; ci0 < a.Cin; ci0 += BK) {
+        for (int i = tid; i < (BM + KW - 1) * (BK / 4); i += blockDim.x) {
+            const int r = i / (BK / 4), c4 = i % (BK / 4);
+            const int t = t0 - PAD + r;
+            float4 v = float4{0.f, 0.f, 0.f, 0.f};
+            if (t >= 0 && t < Tb) {
+                const float* row = a.ids ? a.table + (int64_t)a.ids[(int64_t)b * a.Tmax + t] * a.Cin
+                                         : a.in + ((int64_t)b * a.Tmax + t) * a.Cin;
+                v = *reinterpret_cast<const float4*>(row + ci0 + c4 * 4);
+            }
+            xs[r][c4 * 4 + 0] = v.x;
+            xs[r][c4 * 4 + 1] = v.y;
+            xs[r][c4 * 4 + 2] = v.z;
+            xs[r][c4 * 4 + 3] = v.w;
+        }
+        for (int i = tid; i < BK * KW * (BN / 4); i += blockDim.x) {
+            const int c4 = i % (BN / 4);
+            const int rk = i / (BN / 4);  // ci_local * KW + k
+            const float4 v = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0 * KW + rk)) * a.co_pad + c0 + c4 * 4);
+            *reinterpret_cast<float4*>(&ws[rk / KW][rk % KW][c4 * 4]) = v;
+        }
+        __syncthreads();
+        const int row = lane & 15, kq = lane >> 4;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 4) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = xs[wt + i * 16 + row + k][kk + kq];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = ws[kk + kq][k][wc + j * 16 + row];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
+            }
+        }
+        __syncthreads();
+    }
+    // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)
+    float* outb = a.out + (int64_t)b * a.Tmax * a.Cout;
+    const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * a.Cout : nullptr;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int t = t0 + wt + i * 16 + (lane >> 4) * 4 + r;
+                const int co = c0 + wc + j * 16 + (lane & 15);
+                if (t < Tb && co < a.Cout) {
+                    float sum = acc[0][i][j][r];
+#pragma unroll
+                    for (int k = 1; k < KW; ++k) sum += acc[k][i][j][r];
+                    float y = a.scale ? sum * a.scale[co] : sum;
+                    if (a.shift) y += a.shift[co];
+                    if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+                    else if (a.act == CONV_TANH) y = tanhf(y);
+                    if (resb) y = resb[(int64_t)t * a.Cout + co] + y;
+                    outb[(int64_t)t * a.Cout + co] = y;
+                }
+            }
+}
+
+__global__ void conv_pack_kernel(const float* W, int Cout, int Cin, int KW, int co_pad, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)Cin * KW * co_pad;
+    if (i >= total) return;
+    const int co = i % co_pad;
+    const int k = (i / co_pad) % KW;
+    const int ci = i / ((int64_t)co_pad * KW);
+    out[i] = co < Cout ? W[((int64_t)co * Cin + ci) * KW + k] : 0.f;
+}
+
+__global__ void linear_pack_kernel(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Cin * Cout) return;
+    const int n = i % Cout, ci = i / Cout;
+    out[(int64_t)ci * co_pad + co_offset + n] = W[(int64_t)n * Cin + ci];
+}
+
+__global__ void fold_bn_kernel(const float* bias, const float* gamma, const float* beta, const float* mean,
+                               const float* var, int C, float* scale, float* shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float sc = gamma[c] / sqrtf(var[c] + 1e-5f);
+    scale[c] = sc;
+    shift[c] = beta[c] + (bias[c] - mean[c]) * sc;
+}
+
+template <int KW>
+hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
+    const dim3 block(256);
+    if (frames_hint <= 4096) {
+        const dim3 grid((a.Tmax + 15) / 16, a.co_pad / CONV_BN, B);
+        hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4>), grid, block, 0, s, a);
+    } else {
+        const dim3 grid((a.Tmax + 63) / 64, a.co_pad / CONV_BN, B);
+        hipLaunchKernelGGL((conv_kernel<KW, 64, 2, 2>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t conv_pack(const float* W, int Cout, int Cin, int KW, float* out, hipStream_t s) {
+    const int co_pad = conv_co_pad(Cout);
+    const int64_t total = (int64_t)Cin * KW * co_pad;
+    hipLaunchKernelGGL(conv_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, KW, co_pad, out);
+    return hipGetLastError();
+}
+
+hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,
+                               hipStream_t s) {
+    const int64_t total = (int64_t)Cin * Cout;
+    hipLaunchKernelGGL(linear_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, co_offset, co_pad,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t fold_bn(const float* bias, const float* gamma, const float* beta, const float* mean, const float* var,
+                   int C, float* scale, float* shift, hipStream_t s) {
+    hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias, gamma, beta, mean, var, C, scale,
+                       shift);
+    return hipGetLastError();
+}
+
+hipError_t conv_launch(const ConvArgs& a, int KW, int B, int frames_hint, hipStream_t s) {
+    if (KW == 5) return launch_kw<5>(a, B, frames_hint, s);
+    if (KW == 1) return launch_kw<1>(a, B, frames_hint, s);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace tts

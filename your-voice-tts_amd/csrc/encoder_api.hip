@@ -1,0 +1,251 @@
+// Tacotron2 encoder (embedding + Encoder.inference, models/tacotron2.py:63-66,
+// layers/tacotron2.py:48-83) as HIP launches replayed from a hipGraph per (B, Lmax):
+//   conv 1 with the embedding gather fused into its input staging -> conv 2 -> conv 3
+//   (Conv1d k=5 + BatchNorm folded + ReLU, dropout off in eval) -> LSTM input projection for both
+//   directions as one KW=1 conv (biases b_ih + b_hh folded) -> Lmax recurrence launches, each a
+//   skinny MFMA GEMM over both directions' W_hh with the LSTM cell fused in its epilogue.
+// Every sentence is processed at its own length: the convolutions read zeros past L_b and the
+// reverse direction starts at L_b - 1, which is what the reference computes running alone.
+#include <algorithm>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "conv1d.h"
+#include "sgemm.h"
+
+using namespace tts;
+
+namespace {
+constexpr int EDIM = 512;  // encoder width
+constexpr int EH = 256;    // LSTM hidden per direction
+constexpr int EG = 4 * EH; // gate rows per direction
+}  // namespace
+
+struct tts_encoder {
+    int num_chars = 0, Bcap = 0, Lcap = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    std::vector<void*> allocs;
+    float* emb = nullptr;
+    float *Wc[3] = {}, *sc[3] = {}, *sh[3] = {};
+    float *Wp = nullptr, *bp = nullptr;  // projection [512][1][2048], bias [2048]
+    float* Whh = nullptr;                // packed [2 directions][64 tiles][16 chunks][64][4]
+    int *ids = nullptr, *T = nullptr;
+    float *act0 = nullptr, *act1 = nullptr, *xi = nullptr, *h = nullptr, *c = nullptr, *out = nullptr;
+    std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+};
+
+namespace {
+
+template <typename T>
+tts_status emalloc(tts_encoder* e, T** p, size_t n) {
+    void* q = nullptr;
+    TTS_HIP(hipMalloc(&q, n * sizeof(T) + 16));
+    e->allocs.push_back(q);
+    *p = static_cast<T*>(q);
+    return TTS_OK;
+}
+
+tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s) {
+    // outputs past L_b and the initial LSTM state are zero
+    TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
+    TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * (size_t)e->Bcap * EH, s));
+    TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * (size_t)e->Bcap * EH, s));
+    float* bufs[2] = {e->act0, e->act1};
+    for (int l = 0; l < 3; ++l) {
+        ConvArgs a{};
+        a.in = l == 0 ? nullptr : bufs[(l - 1) & 1];
+        a.ids = l == 0 ? e->ids : nullptr;
+        a.table = e->emb;
+        a.out = bufs[l & 1];
+        a.W = e->Wc[l];
+        a.scale = e->sc[l];
+        a.shift = e->sh[l];
+        a.T = e->T;
+        a.Tmax = Lmax;
+        a.Cin = EDIM;
+        a.Cout = EDIM;
+        a.co_pad = EDIM;
+        a.act = CONV_RELU;
+        TTS_HIP(conv_launch(a, 5, B, frames, s));
+    }
+    {
+        ConvArgs a{};
+        a.in = bufs[0];  // conv 3 output
+        a.out = e->xi;
+        a.W = e->Wp;
+        a.shift = e->bp;
+        a.T = e->T;
+        a.Tmax = Lmax;
+        a.Cin = EDIM;
+        a.Cout = 2 * EG;
+        a.co_pad = 2 * EG;
+        a.act = CONV_NONE;
+        TTS_HIP(conv_launch(a, 1, B, frames, s));
+    }
+    const int64_t hs = (int64_t)e->Bcap * EH;  // per-direction stride; h slots [2][2][Bcap][H]
+    for (int st = 0; st < Lmax; ++st) {
+        float* h_prev = e->h + (int64_t)((st + 1) & 1) * 2 * hs;
+        float* h_next = e->h + (int64_t)(st & 1) * 2 * hs;
+        SGemmArgs a{};
+        a.B = B;
+        a.out_par = -1;
+        a.seg[0] = Seg{h_prev, 0, -1, EH, EH};
+        a.seg[1] = Seg{h_prev + hs, 0, -1, EH, EH};
+        a.nseg = 1;
+        a.W = e->Whh;
+        a.K = EH;
+        a.N = 2 * EG;
+        EncLstm& E = a.enc;
+        E.tiles_per_dir = EG / 16;
+        E.H = EH;
+        E.s = st;
+        E.lens = e->T;
+        E.xi = e->xi;
+        E.Tmax = Lmax;
+        E.c = e->c;
+        E.cstride = hs;
+        E.h_next = h_next;
+        E.enc_out = e->out;
+        TTS_HIP(sgemm_launch(a, ROLE_ENC_LSTM, s));
+    }
+    return TTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void tts_encoder_destroy(tts_encoder* e) {
+    if (!e) return;
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (void* p : e->allocs) (void)hipFree(p);
+    for (hipEvent_t ev : {e->ev_in, e->ev_out})
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_batch, int max_len, void* stream,
+                              tts_encoder** out) {
+    TTS_CHECK(tensors && out, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(max_batch >= 1 && max_batch <= 64, TTS_ERR_UNSUPPORTED, "max_batch must be in [1, 64]");
+    TTS_CHECK(max_len >= 1 && max_len <= 4096, TTS_ERR_UNSUPPORTED, "max_len must be in [1, 4096]");
+    std::unordered_map<std::string, std::pair<const float*, int64_t>> wm;
+    for (int i = 0; i < n_tensors; ++i) wm[tensors[i].key] = {tensors[i].data, tensors[i].numel};
+    auto get = [&](const std::string& k, int64_t numel) -> const float* {
+        auto it = wm.find(k);
+        if (it == wm.end()) { set_error("missing weight " + k); return nullptr; }
+        if (numel >= 0 && it->second.second != numel) { set_error("weight " + k + " has wrong size"); return nullptr; }
+        return it->second.first;
+    };
+    auto* e = new tts_encoder();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    auto fail = [&](tts_status code) { tts_encoder_destroy(e); return code; };
+    tts_status st = TTS_OK;
+#define CK(x)                    \
+    do {                         \
+        st = (x);                \
+        if (st) return fail(st); \
+    } while (0)
+#define HK(x)                                                                    \
+    do {                                                                         \
+        hipError_t _e = (x);                                                     \
+        if (_e != hipSuccess) return fail(hip_fail(_e, #x, __FILE__, __LINE__)); \
+    } while (0)
+    HK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HK(hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming));
+    HK(hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming));
+    auto it = wm.find("embedding.weight");
+    if (it == wm.end() || it->second.second % EDIM) { set_error("missing/bad embedding.weight"); return fail(TTS_ERR_INVALID); }
+    e->num_chars = (int)(it->second.second / EDIM);
+    CK(emalloc(e, &e->emb, (size_t)e->num_chars * EDIM));
+    HK(hipMemcpyAsync(e->emb, it->second.first, sizeof(float) * e->num_chars * EDIM, hipMemcpyDeviceToDevice, s));
+    for (int l = 0; l < 3; ++l) {
+        const std::string pre = "encoder.convolutions." + std::to_string(l) + ".net.";
+        const float* w = get(pre + "0.weight", (int64_t)EDIM * EDIM * 5);
+        const float* bias = get(pre + "0.bias", EDIM);
+        const float* g = get(pre + "1.weight", EDIM);
+        const float* be = get(pre + "1.bias", EDIM);
+        const float* mu = get(pre + "1.running_mean", EDIM);
+        const float* var = get(pre + "1.running_var", EDIM);
+        if (!w || !bias || !g || !be || !mu || !var) return fail(TTS_ERR_INVALID);
+        CK(emalloc(e, &e->Wc[l], (size_t)EDIM * 5 * EDIM));
+        CK(emalloc(e, &e->sc[l], EDIM));
+        CK(emalloc(e, &e->sh[l], EDIM));
+        HK(conv_pack(w, EDIM, EDIM, 5, e->Wc[l], s));
+        HK(fold_bn(bias, g, be, mu, var, EDIM, e->sc[l], e->sh[l], s));
+    }
+    CK(emalloc(e, &e->Wp, (size_t)EDIM * 2 * EG));
+    CK(emalloc(e, &e->bp, 2 * EG));
+    CK(emalloc(e, &e->Whh, sgemm_packed_floats(EG, EH) * 2));
+    const char* sfx[2] = {"", "_reverse"};
+    for (int d = 0; d < 2; ++d) {
+        const std::string pre = "encoder.lstm.";
+        const float* wih = get(pre + "weight_ih_l0" + sfx[d], (int64_t)EG * EDIM);
+        const float* whh = get(pre + "weight_hh_l0" + sfx[d], (int64_t)EG * EH);
+        const float* bih = get(pre + "bias_ih_l0" + sfx[d], EG);
+        const float* bhh = get(pre + "bias_hh_l0" + sfx[d], EG);
+        if (!wih || !whh || !bih || !bhh) return fail(TTS_ERR_INVALID);
+        HK(linear_pack_as_conv(wih, EG, EDIM, d * EG, 2 * EG, e->Wp, s));
+        // bias: b_ih + b_hh in reference gate order (i, f, g, o) x unit
+        HK(sgemm_pack_bias(bih, bhh, EG, ROWMAP_IDENTITY, 0, e->bp + d * EG, s));
+        HK(sgemm_pack(whh, EH, nullptr, 0, EG, ROWMAP_LSTM, EH, e->Whh + d * sgemm_packed_floats(EG, EH), s));
+    }
+    e->Bcap = max_batch;
+    e->Lcap = max_len;
+    const size_t BL = (size_t)max_batch * max_len;
+    CK(emalloc(e, &e->ids, BL));
+    CK(emalloc(e, &e->T, max_batch));
+    CK(emalloc(e, &e->act0, BL * EDIM));
+    CK(emalloc(e, &e->act1, BL * EDIM));
+    CK(emalloc(e, &e->xi, BL * 2 * EG));
+    CK(emalloc(e, &e->h, (size_t)4 * max_batch * EH));
+    CK(emalloc(e, &e->c, (size_t)2 * max_batch * EH));
+    CK(emalloc(e, &e->out, BL * EDIM));
+    HK(hipStreamSynchronize(s));
+#undef CK
+#undef HK
+    *out = e;
+    return TTS_OK;
+}
+
+tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax, float* out,
+                           void* stream) {
+    TTS_CHECK(e && ids && lens && out, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(B >= 1 && B <= e->Bcap && Lmax >= 1 && Lmax <= e->Lcap, TTS_ERR_INVALID,
+              "batch / length exceeds encoder capacity");
+    for (int b = 0; b < B; ++b)
+        TTS_CHECK(lens[b] >= 1 && lens[b] <= Lmax, TTS_ERR_INVALID, "length out of range [1, Lmax]");
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t s = e->stream;
+    TTS_HIP(hipEventRecord(e->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
+    TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    auto key = std::make_pair(B, Lmax);
+    auto git = e->graphs.find(key);
+    if (git == e->graphs.end()) {
+        hipGraph_t g = nullptr;
+        TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        // tile shape depends on the batch's total frames: key on the worst case (Lmax per sentence)
+        tts_status st = enqueue_encoder(e, B, Lmax, B * Lmax, s);
+        hipError_t ee = hipStreamEndCapture(s, &g);
+        if (st) return st;
+        TTS_HIP(ee);
+        hipGraphExec_t exec = nullptr;
+        TTS_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+        TTS_HIP(hipGraphDestroy(g));
+        git = e->graphs.emplace(key, exec).first;
+    }
+    TTS_HIP(hipGraphLaunch(git->second, s));
+    TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipEventRecord(e->ev_out, s));
+    TTS_HIP(hipStreamWaitEvent(cs, e->ev_out, 0));
+    return TTS_OK;
+}
+
+}  // extern "C"

@@ -22,10 +22,30 @@ struct Seg {
     int len;  // multiple of 16
 };
 
-enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2 };
+enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2, EPI_ENC_LSTM = 3 };
+
+// EPI_ENC_LSTM: one step s of the bidirectional encoder LSTM (layers/tacotron2.py:56-61, 82):
+// workgroups [0, tiles_per_dir) run the forward direction on seg[0] = h_fwd(s-1) at position s,
+// the rest the reverse direction on seg[1] = h_bwd(s-1) at position L_b-1-s.  Gates add the
+// precomputed input projection xi (both biases folded in); sentences with s >= L_b are idle.
+struct EncLstm {
+    int tiles_per_dir;
+    int H;
+    int s;
+    const int* lens;
+    const float* xi;  // [B][Tmax][2*4H]
+    int Tmax;
+    float* c;         // [2][cstride]
+    int64_t cstride;  // per-direction stride of c and h_next (>= B*H)
+    float* h_next;    // [2][cstride]
+    float* enc_out;   // [B][Tmax][2H]
+};
 // Decoder stage a launch serves; fixes the epilogue (LSTM roles use EPI_LSTM, ROLE_MEL_FUSED
 // uses EPI_MEL_FUSED).
-enum Role { ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4, ROLE_MEL_FUSED = 5 };
+enum Role {
+    ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4, ROLE_MEL_FUSED = 5,
+    ROLE_ENC_LSTM = 6
+};
 enum Act { ACT_NONE = 0, ACT_RELU = 1 };
 
 // EPI_MEL_FUSED: one GEMM over x = [h_dec | ctx] whose output rows are
@@ -72,6 +92,7 @@ struct SGemmArgs {
     const int* done;      // per-row done flags or null
     const int* n_active;  // unused (kept adjacent to step)
     MelFused mf;          // EPI_MEL_FUSED only
+    EncLstm enc;          // EPI_ENC_LSTM only
 };
 
 // Row maps used when repacking reference matrices.

@@ -28,6 +28,21 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
         pre_cell = a.cell[(int64_t)b * a.ldc + ntile * 4 + u];
     }
+    const int dir = EPI == EPI_ENC_LSTM ? ntile / a.enc.tiles_per_dir : 0;
+    int enc_pos = -1;  // encoder position this thread's (b, unit) updates, -1 when idle
+    if (EPI == EPI_ENC_LSTM && (int)threadIdx.x < a.B * 4) {
+        const EncLstm& E = a.enc;
+        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+        const int unit = (ntile - dir * E.tiles_per_dir) * 4 + u;
+        const int L = E.lens[b];
+        if (E.s < L) {
+            enc_pos = dir ? L - 1 - E.s : E.s;
+            const float* xi = E.xi + ((int64_t)b * E.Tmax + enc_pos) * (8 * E.H) + dir * 4 * E.H + unit;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) pre_bias[g] = xi[g * E.H];
+            pre_cell = E.c[dir * E.cstride + (int64_t)b * E.H + unit];
+        }
+    }
     if (st.y == 0) {
         // every sentence is done: steps past the end are no-ops, but the fused stop launch
         // still forwards {step+1, 0} so the next parity slot reads "done" as well
@@ -48,8 +63,9 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     int kstart = 0;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-        const Seg& g = a.seg[s];
-        const bool live = s < a.nseg;
+        // the encoder LSTM reads one segment: its direction's previous hidden state
+        const Seg& g = a.seg[EPI == EPI_ENC_LSTM ? (s == 0 ? dir : 2) : s];
+        const bool live = EPI == EPI_ENC_LSTM ? s == 0 : s < a.nseg;
         const float* p = live ? g.p + (g.par >= 0 ? (int64_t)((step + g.par) & 1) * g.pstride : 0) : nullptr;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -138,6 +154,22 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             if (out) out[(int64_t)b * a.ldo + n] = v;
             if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
             if (track && !(a.done && a.done[b])) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
+        }
+    } else if (EPI == EPI_ENC_LSTM) {
+        const EncLstm& E = a.enc;
+        const int e = threadIdx.x;
+        if (e < a.B * 4 && enc_pos >= 0) {
+            const int b = e >> 2, u = e & 3;
+            const int unit = (ntile - dir * E.tiles_per_dir) * 4 + u;
+            const float gi = fin[b][u] + pre_bias[0];
+            const float gf = fin[b][4 + u] + pre_bias[1];
+            const float gg = fin[b][8 + u] + pre_bias[2];
+            const float go = fin[b][12 + u] + pre_bias[3];
+            const float c2 = sigmoidf_(gf) * pre_cell + sigmoidf_(gi) * tanhf(gg);
+            const float h = sigmoidf_(go) * tanhf(c2);
+            E.c[dir * E.cstride + (int64_t)b * E.H + unit] = c2;
+            E.h_next[dir * E.cstride + (int64_t)b * E.H + unit] = h;
+            E.enc_out[((int64_t)b * E.Tmax + enc_pos) * (2 * E.H) + dir * E.H + unit] = h;
         }
     } else if (EPI == EPI_MEL_FUSED) {
         const MelFused& m = a.mf;
@@ -283,6 +315,7 @@ hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s) {
         case ROLE_DEC_LSTM: return launch_role<EPI_LSTM, ROLE_DEC_LSTM>(a, s);
         case ROLE_MEL: return launch_role<EPI_LINEAR, ROLE_MEL>(a, s);
         case ROLE_MEL_FUSED: return launch_role<EPI_MEL_FUSED, ROLE_MEL_FUSED>(a, s);
+        case ROLE_ENC_LSTM: return launch_role<EPI_ENC_LSTM, ROLE_ENC_LSTM>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

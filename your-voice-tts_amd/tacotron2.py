@@ -119,6 +119,7 @@ class Tacotron2:
             lib = _native.load_library()
             lib.tts_decoder_destroy(self._native[0])
             lib.tts_postnet_destroy(self._native[1])
+            lib.tts_encoder_destroy(self._native[3])
             self._native = None
 
     def __del__(self):
@@ -155,45 +156,29 @@ class Tacotron2:
             arr2, keep2 = _native.tensor_views(post_w)
             p = ctypes.c_void_p()
             _native.check(lib.tts_postnet_create(arr2, len(post_w), 80, stream, ctypes.byref(p)), "tts_postnet_create")
-            self._native = (h, p, key)
+            enc_w = {k: v.float().contiguous() for k, v in self._params.items()
+                     if (k.startswith("encoder.") or k == "embedding.weight") and v.is_floating_point()}
+            arr3, keep3 = _native.tensor_views(enc_w)
+            e = ctypes.c_void_p()
+            _native.check(lib.tts_encoder_create(arr3, len(enc_w), key[2], key[1], stream, ctypes.byref(e)),
+                          "tts_encoder_create")
+            self._native = (h, p, key, e)
         return lib, self._native[0], self._native[1]
 
-    # ------------------------------------------------------------------ encoder (PyTorch-ROCm)
-    def _encoder_lstm(self):
-        if getattr(self, "_lstm", None) is None:
-            lstm = torch.nn.LSTM(512, 256, num_layers=1, batch_first=True, bidirectional=True).to(self.device)
-            with torch.no_grad():
-                for name, prm in lstm.named_parameters():
-                    prm.copy_(self._params["encoder.lstm." + name])
-            lstm.eval()
-            self._lstm = lstm
-        return self._lstm
-
+    # ------------------------------------------------------------------ encoder
     @torch.no_grad()
     def encode(self, ids: torch.Tensor, lens, speaker_ids=None):
         """Embedding + Encoder.inference (models/tacotron2.py:63-66, layers/tacotron2.py:78-83)
-        on a padded batch; every sentence sees zero padding past its own length, as alone."""
+        on a padded batch through libtts_hip ``tts_encoder_run``; every sentence is encoded at its
+        own length (zero padding past it), as the reference does running it alone."""
         p = self._params
         B, Lmax = ids.shape
-        lens_t = torch.as_tensor(lens, device=ids.device)
-        valid = (torch.arange(Lmax, device=ids.device)[None, :] < lens_t[:, None]).float()  # [B, L]
-        x = F.embedding(ids, p["embedding.weight"]).transpose(1, 2)  # [B, 512, L]
-        for i in range(3):
-            pre = f"encoder.convolutions.{i}.net."
-            x = x * valid[:, None, :]
-            x = F.conv1d(x, p[pre + "0.weight"], p[pre + "0.bias"], padding=2)
-            x = F.batch_norm(x, p[pre + "1.running_mean"], p[pre + "1.running_var"], p[pre + "1.weight"],
-                             p[pre + "1.bias"], training=False, eps=1e-5)
-            x = F.relu(x)
-        x = x.transpose(1, 2).contiguous()  # [B, L, 512]
-        lstm = self._encoder_lstm()
-        if B == 1 or min(lens) == Lmax:
-            out, _ = lstm(x)
-        else:  # each sentence's reverse direction starts at its own last position
-            packed = torch.nn.utils.rnn.pack_padded_sequence(x, torch.as_tensor(lens), batch_first=True,
-                                                             enforce_sorted=False)
-            out, _ = lstm(packed)
-            out, _ = torch.nn.utils.rnn.pad_packed_sequence(out, batch_first=True, total_length=Lmax)
+        lib, _, _ = self._handles(Lmax, B)
+        ids32 = ids.to(self.device, dtype=torch.int32).contiguous()
+        out = torch.empty(B, Lmax, 512, device=self.device)
+        _native.check(lib.tts_encoder_run(self._native[3], ctypes.c_void_p(ids32.data_ptr()), _native.i32_array(lens),
+                                          B, Lmax, ctypes.c_void_p(out.data_ptr()), _native.stream_handle()),
+                      "tts_encoder_run")
         if speaker_ids is not None and "speaker_embedding.weight" in p:
             out = out + F.embedding(torch.as_tensor(speaker_ids, device=ids.device).view(-1),
                                     p["speaker_embedding.weight"])[:, None, :]
