@@ -1,8 +1,8 @@
-// Decoder-step kernels other than the GEMMs: state init, processed-inputs projection,
-// the attention step (one workgroup per sentence) and the stop rule.
+// Decoder-step kernels other than the GEMMs: state init, processed-inputs projection and the
+// attention step (one workgroup per sentence).
 //
 // Reference: Attention.forward and helpers (layers/common_layers.py:139-256),
-// Decoder._init_states / inference stop rule (layers/tacotron2.py:157-177, 256-277).
+// Decoder._init_states (layers/tacotron2.py:157-177).
 #include "decoder.h"
 
 namespace tts {
@@ -32,6 +32,7 @@ __global__ void decoder_init_kernel(const InitArgs a) {
     if (threadIdx.x == 0) {
         a.u[b] = 0.5f;
         a.win_idx[b] = -1;
+        a.nidx[b] = 1;  // argmax of prev_alpha = [0, 1, 1e-7, ...]
         a.tail[b] = 0.f;
         a.flag1[b] = 0;
         a.count[b] = 0;
@@ -44,6 +45,11 @@ __global__ void decoder_init_kernel(const InitArgs a) {
     }
 }
 
+hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 // Zero rows [n_steps[b], nmax) of a per-sentence history dst[b][step][width].
 __global__ void zero_tail_kernel(float* dst, int64_t ldb, const int* n_steps, int width, int nmax) {
     const int b = blockIdx.x;
@@ -53,11 +59,6 @@ __global__ void zero_tail_kernel(float* dst, int64_t ldb, const int* n_steps, in
 
 hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s) {
     hipLaunchKernelGGL(zero_tail_kernel, dim3(B), dim3(256), 0, s, dst, ldb, n_steps, width, nmax);
-    return hipGetLastError();
-}
-
-hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -107,7 +108,7 @@ hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lm
 // ------------------------------------------------------------------ attention step
 // One workgroup of 1024 threads per sentence; thread j owns encoder position j (L <= 1024).
 size_t attention_smem_bytes(int Lcap, int location) {
-    size_t f = 2 * ADIM + 4 * (size_t)Lcap + ATT_WAVES * (size_t)Lcap + 4 * ATT_WAVES;
+    size_t f = 2 * ADIM + 3 * (size_t)Lcap + ATT_WAVES * (size_t)Lcap + 4 * ATT_WAVES;
     if (location) f += 2 * ((size_t)Lcap + 32) + (size_t)NLOC * Lcap + ADIM * NLOC;
     return f * sizeof(float);
 }
@@ -148,39 +149,62 @@ __device__ __forceinline__ Red block_reduce(float s, float m, float y, int i, fl
 
 __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a) {
     const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Lc = a.Lcap;
+    const int64_t row = (int64_t)b * Lc;
+    constexpr int DPW = ADIM / ATT_WAVES;  // attention dims per wave in the energy loop
+    // ---- phase 0: every load that depends only on kernel arguments is issued up front, so the
+    // kernel pays one memory round trip before computing (latency-bound at batch 1)
     const int2 st = *reinterpret_cast<const int2*>(a.step);  // {step, n_active}
     const int L = a.lens[b];
+    const int j = tid;  // this thread's encoder position
+    const bool in = j < L;
+    // forward attention + mask: after the mask at most (n-2)%L and [n-1, n+2] are nonzero, where
+    // n = argmax(prev_alpha) was carried from the previous step; the context needs only those rows
+    const bool sparse = a.forward_attn && a.forward_attn_mask;
+    const int n = sparse ? a.nidx[b] : 0;
+    const float u = a.forward_attn ? a.u[b] : 0.f;
+    const float vb = a.v_b[0];
+    float qv = 0.f;
+    if (tid < ADIM) qv = a.q[(int64_t)b * ADIM + tid];
+    else if (tid < 2 * ADIM) qv = a.v[tid - ADIM];
+    const float aold_j = (a.forward_attn && in) ? a.alpha[row + j] : 0.f;
+    const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
+    const int d0 = wave * DPW;
+    float pv0[DPW], pv1[DPW];
+#pragma unroll
+    for (int dd = 0; dd < DPW; ++dd) {
+        pv0[dd] = lane < L ? Pt[(int64_t)(d0 + dd) * Lc + lane] : 0.f;
+        pv1[dd] = lane + 64 < L ? Pt[(int64_t)(d0 + dd) * Lc + lane + 64] : 0.f;
+    }
+    const float* encb = a.enc + row * ENC;
+    const int cx = sparse ? (n - 2 + L) % L : 0;
+    const int clo = sparse ? (n >= 1 ? n - 1 : L - 1) : 0;
+    const int chi = sparse ? min(n + 2, L - 1) : -1;
+    float ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f};
+    if (sparse && tid < ENC) {
+        ex = encb[(int64_t)cx * ENC + tid];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (clo + k <= chi) erow[k] = encb[(int64_t)(clo + k) * ENC + tid];
+    }
     if (st.y == 0) return;
     const int t = st.x;
-    const int Lc = a.Lcap;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     extern __shared__ __align__(16) float sm[];
     float* q = sm;
     float* vv = q + ADIM;
     float* aold = vv + ADIM;
     float* an = aold + Lc;
     float* wts = an + Lc;
-    float* spare = wts + Lc;
-    float* red = spare + Lc;
+    float* red = wts + Lc;
     float* scr = red + ATT_WAVES * Lc;
     float* cat = scr + 4 * ATT_WAVES;
     float* locf = cat + 2 * (Lc + 32);
     float* wd = locf + NLOC * Lc;
 
-    const int64_t row = (int64_t)b * Lc;
-    const int j = tid;  // this thread's encoder position
-    const bool in = j < L;
-    const float* h = a.h_att + (int64_t)(t & 1) * a.h_pstride + (int64_t)b * HATT;
-    // ---- phase 0: every independent load at once
-    if (tid < ADIM) q[tid] = a.q[(int64_t)b * ADIM + tid];
-    else if (tid < 2 * ADIM) vv[tid - ADIM] = a.v[tid - ADIM];
-    const float u = a.forward_attn ? a.u[b] : 0.f;
-    const float vb = a.v_b[0];
-    float aold_j = 0.f;
-    if (a.forward_attn && in) {
-        aold_j = a.alpha[row + j];
-        aold[j] = aold_j;
-    }
+    if (tid < ADIM) q[tid] = qv;
+    else if (tid < 2 * ADIM) vv[tid - ADIM] = qv;
+    if (a.forward_attn && in) aold[j] = aold_j;
     if (a.location_attn) {
         // attention_cat = [attention_weights; attention_weights_cum] (common_layers.py:167-169),
         // zero padded by (31-1)/2 = 15 on both sides for location_conv (:90-96).
@@ -204,32 +228,25 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         }
         __syncthreads();
     }
-    // ---- phase 1: energy partials, wave w owns d in [8w, 8w+8), lanes own positions
-    {
-        const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
-        constexpr int DPW = ADIM / ATT_WAVES;
-        const int d0 = wave * DPW;
-        for (int j0 = 0; j0 < L; j0 += 64) {
-            const int jj = j0 + lane;
-            if (jj < L) {
-                float pv[DPW];
+    // ---- energy partials e_j = v . tanh(pq [+ loc_j] + P_j) + b_v (common_layers.py:166-182):
+    // wave w owns d in [8w, 8w+8), lanes own positions
+    for (int j0 = 0; j0 < L; j0 += 64) {
+        const int jj = j0 + lane;
+        if (jj < L) {
+            float s = 0.f;
 #pragma unroll
-                for (int dd = 0; dd < DPW; ++dd) pv[dd] = Pt[(int64_t)(d0 + dd) * Lc + jj];
-                float s = 0.f;
-#pragma unroll
-                for (int dd = 0; dd < DPW; ++dd) {
-                    const int d = d0 + dd;
-                    float x = q[d];  // processed_query (+ location) + processed_inputs (common_layers.py:172-174, 180)
-                    if (a.location_attn) {
-                        float lc = 0.f;
-                        for (int f = 0; f < NLOC; ++f) lc += wd[d * NLOC + f] * locf[f * Lc + jj];
-                        x += lc;
-                    }
-                    x += pv[dd];
-                    s += vv[d] * tanhf(x);
+            for (int dd = 0; dd < DPW; ++dd) {
+                const int d = d0 + dd;
+                float x = q[d];
+                if (a.location_attn) {
+                    float lc = 0.f;
+                    for (int f = 0; f < NLOC; ++f) lc += wd[d * NLOC + f] * locf[f * Lc + jj];
+                    x += lc;
                 }
-                red[wave * Lc + jj] = s;
+                x += j0 == 0 ? pv0[dd] : (j0 == 64 ? pv1[dd] : Pt[(int64_t)d * Lc + jj]);
+                s += vv[d] * tanhf(x);
             }
+            red[wave * Lc + jj] = s;
         }
     }
     __syncthreads();
@@ -251,42 +268,46 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         const Red r = block_reduce(0.f, -INFINITY, in ? e : -INFINITY, in ? j : 0x7fffffff, scr);
         if (tid == 0) a.win_idx[b] = r.i;
     }
-    // ---- normalisation (common_layers.py:239-245), fused with argmax(prev_alpha) for the mask
-    const float prev_j = (in && a.forward_attn) ? (j ? aold[j - 1] : 0.f) : -INFINITY;
+    // ---- normalisation (common_layers.py:239-245)
     float al = 0.f;
-    int n = 0;
     if (a.attn_norm == 0) {
-        const Red r1 = block_reduce(0.f, e, prev_j, in ? j : 0x7fffffff, scr);
-        n = r1.i;
-        const float ex = in ? expf(e - r1.m) : 0.f;
-        const Red r2 = block_reduce(ex, -INFINITY, 0.f, 0, scr);
-        al = ex / r2.s;
+        const Red r1 = block_reduce(0.f, e, 0.f, 0, scr);
+        const float exj = in ? expf(e - r1.m) : 0.f;
+        const Red r2 = block_reduce(exj, -INFINITY, 0.f, 0, scr);
+        al = exj / r2.s;
     } else {
         const float sg = in ? sigmoidf_(e) : 0.f;
-        const Red r = block_reduce(sg, -INFINITY, prev_j, in ? j : 0x7fffffff, scr);
-        n = r.i;
+        const Red r = block_reduce(sg, -INFINITY, 0.f, 0, scr);
         al = sg / r.s;
     }
     if (a.location_attn && in) a.att_cum[row + j] += al;  // update_location_attention (:163-164)
 
     float w = al;
-    bool sparse = false;  // true when at most 5 positions can be nonzero (forward mask)
     if (a.forward_attn) {
         // apply_forward_attention (common_layers.py:199-223)
         float anj = 0.f;
         if (in) {
-            const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - u, aold_j), __fmul_rn(u, prev_j)), 1e-8f);
+            const float prev = j ? aold[j - 1] : 0.f;
+            const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - u, aold_j), __fmul_rn(u, prev)), 1e-8f);
             anj = __fmul_rn(mix, al);
         }
-        if (a.forward_attn_mask) {
+        float denom;
+        if (sparse) {
             const Red r = block_reduce(0.f, in ? anj : -INFINITY, 0.f, 0, scr);
             // Python slicing of :211-213 incl. the negative-index wrap for n < 2
             if (in && ((j >= n + 3) || (n >= 1 ? j < n - 1 : j < L - 1))) anj = 0.f;
-            if (j == (n - 2 + L) % L) anj = 0.01f * r.m;
-            sparse = true;
+            if (j == cx) anj = 0.01f * r.m;
+            if (in) an[j] = anj;
+            __syncthreads();
+            // the <= 5 surviving entries, summed in index order by every thread (identical result)
+            denom = 0.f;
+            if (cx < clo) denom += an[cx];
+            for (int p = clo; p <= chi; ++p) denom += an[p];
+            if (cx > chi) denom += an[cx];
+        } else {
+            denom = block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr).s;
         }
-        const Red r = block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr);
-        w = in ? anj / r.s : 0.f;
+        w = in ? anj / denom : 0.f;
         if (in) a.alpha[row + j] = w;
     }
     if (in) wts[j] = w;
@@ -296,21 +317,31 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     if (!a.done[b] && t < a.hist_cap && a.align_hist)
         for (int jj = tid; jj < a.Lalign; jj += blockDim.x)
             a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + jj] = jj < L ? wts[jj] : 0.f;
-    if (tid == 0) a.tail[b] = L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0];
-
+    if (tid == 0) {
+        a.tail[b] = L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0];
+        if (sparse) {
+            // next step's n = argmax(prev_alpha) = 1 + first argmax of alpha[0..L-2], or 0 when
+            // those are all zero; only the surviving positions can be nonzero (index order, strict >)
+            float bv = 0.f;
+            int bi = -1;
+            auto consider = [&](int p) {
+                if (p <= L - 2 && wts[p] > bv) { bv = wts[p]; bi = p; }
+            };
+            if (cx < clo) consider(cx);
+            for (int p = clo; p <= chi; ++p) consider(p);
+            if (cx > chi) consider(cx);
+            a.nidx[b] = bi >= 0 ? bi + 1 : 0;
+        }
+    }
     // ---- context = w . inputs  (bmm, common_layers.py:217 / 253)
-    float* ctx_out = a.xa + (int64_t)((t + 1) & 1) * a.xa_pstride + (int64_t)b * XA + PRE;
-    const float* encb = a.enc + row * ENC;
     float ctx = 0.f;
     if (sparse) {
-        // only (n-2)%L and [n-1, n+2] can be nonzero after the mask: sum those rows in index order
         if (tid < ENC) {
-            const int x = (n - 2 + L) % L;
-            const int lo = n >= 1 ? n - 1 : L - 1;
-            const int hi = min(n + 2, L - 1);
-            if (x < lo) ctx += wts[x] * encb[(int64_t)x * ENC + tid];
-            for (int p = lo; p <= hi; ++p) ctx += wts[p] * encb[(int64_t)p * ENC + tid];
-            if (x > hi) ctx += wts[x] * encb[(int64_t)x * ENC + tid];
+            if (cx < clo) ctx += wts[cx] * ex;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (clo + k <= chi) ctx += wts[clo + k] * erow[k];
+            if (cx > chi) ctx += wts[cx] * ex;
         }
     } else {
         const int d = tid & (ENC - 1), half = tid >> 9;
@@ -331,9 +362,10 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         __syncthreads();
         if (tid < ENC) ctx = red[tid] + red[tid + ENC];
     }
-    if (tid < ENC) ctx_out[tid] = ctx;
+    if (tid < ENC) a.ctx[(int64_t)b * XA + tid] = ctx;
     if (a.forward_attn && a.trans_agent) {
         // u = sigmoid(ta([context, query]))  (:220-222)
+        const float* h = a.h_att + (int64_t)b * HATT;
         float p = tid < ENC ? a.ta_w[tid] * ctx : 0.f;
         p += a.ta_w[ENC + tid] * h[tid];  // blockDim == HATT
         const Red r = block_reduce(p, -INFINITY, 0.f, 0, scr);
@@ -350,65 +382,6 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
 hipError_t attention_prepare(int Lcap, int location) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_smem_bytes(Lcap, location));
-}
-
-// ------------------------------------------------------------------ stopnet + stop rule
-// stop = sigmoid(stopnet([h_dec; mel]))   (tacotron2.py:219-224, 262)
-// flags as tacotron2.py:257-277: stop_flags[0] is always true; [1] latches
-// (tail > 0.8 and t > L); [2] = t > 2L; 20 extra steps; cap checked only in the `elif`.
-// One wave per sentence; every per-sentence load is issued before the dot product.
-__global__ __launch_bounds__(1024) void stop_kernel(const StopArgs a) {
-    const int2 st = *reinterpret_cast<const int2*>(a.step);
-    if (st.y == 0) return;
-    const int t = st.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __shared__ int sdone[64];
-    for (int b = wave; b < a.B; b += nw) {
-        const int dn = a.done[b];
-        const int L = a.lens[b];
-        const float tail = a.tail[b];
-        const int f1 = a.flag1[b];
-        const int cnt = a.count[b];
-        const float* h = a.h_dec + (int64_t)(t & 1) * a.h_pstride + (int64_t)b * HDEC;
-        const float* m = a.mem + (int64_t)b * a.nmel;
-        float p = 0.f;
-        for (int k = lane; k < HDEC; k += 64) p += a.w[k] * h[k];
-        for (int k = lane; k < a.nmel; k += 64) p += a.w[HDEC + k] * m[k];
-        p = wave_sum(p);
-        if (lane == 0) {
-            int nd = dn;
-            if (!dn) {
-                const float stv = sigmoidf_(p + a.b[0]);
-                if (t < a.hist_cap) a.stop_hist[(int64_t)b * a.stop_ldb + t] = stv;
-                const int nf1 = f1 | ((tail > 0.8f && t > L) ? 1 : 0);
-                a.flag1[b] = nf1;
-                const bool f2 = t > 2 * L;
-                if (nf1 && f2) {
-                    a.count[b] = cnt + 1;
-                    if (cnt + 1 > 20) nd = 1;
-                } else if (t + 1 == a.max_steps) {
-                    nd = 1;
-                }
-                if (nd) {
-                    a.done[b] = 1;
-                    a.n_steps[b] = t + 1;
-                }
-            }
-            sdone[b] = nd;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int n = 0;
-        for (int b = 0; b < a.B; ++b) n += sdone[b] ? 0 : 1;
-        *reinterpret_cast<int2*>(a.step) = make_int2(t + 1, n);
-    }
-}
-
-hipError_t launch_stop(const StopArgs& a, hipStream_t s) {
-    const int threads = 64 * (a.B < 16 ? a.B : 16);
-    hipLaunchKernelGGL(stop_kernel, dim3(1), dim3(threads), 0, s, a);
-    return hipGetLastError();
 }
 
 }  // namespace tts

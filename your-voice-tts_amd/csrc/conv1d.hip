@@ -29,8 +29,14 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = (wave / WN) * (BM / WM);
     const int wc = (wave % WN) * (BN / WN);
-    __shared__ float xs[BM + KW - 1][BK + 1];
-    __shared__ __align__(16) float ws[BK][KW][BN];
+    // double-buffered LDS stages; the next K step's global loads are in registers while the
+    // current step's MFMAs run (one barrier per K step)
+    constexpr int XROWS = BM + KW - 1;
+    constexpr int XN = XROWS * (BK / 4);     // float4 of input per stage
+    constexpr int WN4 = BK * KW * (BN / 4);  // float4 of weights per stage
+    constexpr int XR = (XN + 255) / 256, WR = (WN4 + 255) / 256;
+    __shared__ float xs[2][XROWS][BK + 1];
+    __shared__ __align__(16) float ws[2][BK][KW][BN];
     floatx4 acc[KW][TM][TN];
 #pragma unroll
     for (int k = 0; k < KW; ++k)
@@ -38,44 +44,78 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[k][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int ci0 = 0; ci0 < a.Cin; ci0 += BK) {
-        for (int i = tid; i < (BM + KW - 1) * (BK / 4); i += blockDim.x) {
-            const int r = i / (BK / 4), c4 = i % (BK / 4);
-            const int t = t0 - PAD + r;
+    const int* idsb = a.ids ? a.ids + (int64_t)b * a.Tmax : nullptr;
+    float4 xr[XR], wr[WR];
+    auto gload = [&](int ci0) {
+#pragma unroll
+        for (int q = 0; q < XR; ++q) {
+            const int i = tid + q * 256;
             float4 v = float4{0.f, 0.f, 0.f, 0.f};
-            if (t >= 0 && t < Tb) {
-                const float* row = a.ids ? a.table + (int64_t)a.ids[(int64_t)b * a.Tmax + t] * a.Cin
-                                         : a.in + ((int64_t)b * a.Tmax + t) * a.Cin;
-                v = *reinterpret_cast<const float4*>(row + ci0 + c4 * 4);
+            if (i < XN) {
+                const int r = i / (BK / 4), c4 = i % (BK / 4);
+                const int t = t0 - PAD + r;
+                if (t >= 0 && t < Tb) {
+                    const float* src = idsb ? a.table + (int64_t)idsb[t] * a.Cin
+                                            : a.in + ((int64_t)b * a.Tmax + t) * a.Cin;
+                    v = *reinterpret_cast<const float4*>(src + ci0 + c4 * 4);
+                }
             }
-            xs[r][c4 * 4 + 0] = v.x;
-            xs[r][c4 * 4 + 1] = v.y;
-            xs[r][c4 * 4 + 2] = v.z;
-            xs[r][c4 * 4 + 3] = v.w;
+            xr[q] = v;
         }
-        for (int i = tid; i < BK * KW * (BN / 4); i += blockDim.x) {
-            const int c4 = i % (BN / 4);
-            const int rk = i / (BN / 4);  // ci_local * KW + k
-            const float4 v = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0 * KW + rk)) * a.co_pad + c0 + c4 * 4);
-            *reinterpret_cast<float4*>(&ws[rk / KW][rk % KW][c4 * 4]) = v;
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+            const int i = tid + q * 256;
+            if (i < WN4) {
+                const int c4 = i % (BN / 4), rk = i / (BN / 4);  // rk = ci_local * KW + k
+                wr[q] = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0 * KW + rk)) * a.co_pad + c0 + c4 * 4);
+            }
         }
-        __syncthreads();
-        const int row = lane & 15, kq = lane >> 4;
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < XR; ++q) {
+            const int i = tid + q * 256;
+            if (i < XN) {
+                const int r = i / (BK / 4), c4 = i % (BK / 4);
+                xs[buf][r][c4 * 4 + 0] = xr[q].x;
+                xs[buf][r][c4 * 4 + 1] = xr[q].y;
+                xs[buf][r][c4 * 4 + 2] = xr[q].z;
+                xs[buf][r][c4 * 4 + 3] = xr[q].w;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+            const int i = tid + q * 256;
+            if (i < WN4) {
+                const int c4 = i % (BN / 4), rk = i / (BN / 4);
+                *reinterpret_cast<float4*>(&ws[buf][rk / KW][rk % KW][c4 * 4]) = wr[q];
+            }
+        }
+    };
+    const int nsteps = a.Cin / BK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    const int row = lane & 15, kq = lane >> 4;
+    for (int st = 0; st < nsteps; ++st) {
+        const int cur = st & 1;
+        if (st + 1 < nsteps) gload((st + 1) * BK);
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
 #pragma unroll
             for (int kk = 0; kk < BK; kk += 4) {
                 float av[TM], bv[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) av[i] = xs[wt + i * 16 + row + k][kk + kq];
+                for (int i = 0; i < TM; ++i) av[i] = xs[cur][wt + i * 16 + row + k][kk + kq];
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bv[j] = ws[kk + kq][k][wc + j * 16 + row];
+                for (int j = 0; j < TN; ++j) bv[j] = ws[cur][kk + kq][k][wc + j * 16 + row];
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
             }
         }
+        if (st + 1 < nsteps) lstore(cur ^ 1);
         __syncthreads();
     }
     // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)

@@ -1,4 +1,4 @@
-// Decoder-step state and the non-GEMM kernels of the step (attention, stop rule).
+// Decoder-step state and the non-GEMM kernels of the step (init, processed inputs, attention).
 #pragma once
 #include "common.h"
 
@@ -32,47 +32,23 @@ struct AttnArgs {
     const float* Pt;       // [B][128][Lcap] processed inputs, transposed
     const float* enc;      // [B][Lcap][512]
     const int* lens;       // [B]
-    const float* h_att;    // ping-pong base [2][B][1024] (row of step parity)
-    int64_t h_pstride;
+    const float* h_att;    // [B][1024] this step's attention-LSTM output
     // state
     float* alpha;          // [B][Lcap]
     float* att_w;          // [B][Lcap]
     float* att_cum;        // [B][Lcap]
     float* u;              // [B]
     int* win_idx;          // [B]
+    int* nidx;             // [B] argmax of prev_alpha for the next step (forward mask)
     float* tail;           // [B] att_w[L-2] + att_w[L-1]
     // outputs
-    float* xa;             // ping-pong base [2][B][768]; ctx goes to xa[(t+1)&1][b][256:]
-    int64_t xa_pstride;
+    float* ctx;            // [B] rows of stride XA: context written to ctx[b*XA + d]
     float* align_hist;     // [B][hist_cap][Lalign] or null
     int64_t align_ldb;     // stride per sentence
     int Lalign;
     int hist_cap;
-    const int* step;      // int2 {step, n_active}: n_active == step + 1
+    const int* step;       // int2 {step, n_active} of this step's parity slot
     const int* done;
-    const int* n_active;
-};
-
-struct StopArgs {
-    const float* w;      // stopnet weight [1024 + 80r]
-    const float* b;      // [1]
-    int nmel;            // 80*r
-    const float* h_dec;  // ping-pong base [2][B][1024]
-    int64_t h_pstride;
-    const float* mem;    // [B][nmel] this step's mel frame(s)
-    const int* lens;
-    const float* tail;
-    float* stop_hist;    // [B][hist_cap]
-    int64_t stop_ldb;
-    int hist_cap;
-    int max_steps;
-    int B;
-    int* flag1;
-    int* count;
-    int* done;
-    int* n_steps;
-    int* step;
-    int* n_active;
 };
 
 struct InitArgs {
@@ -87,7 +63,7 @@ struct InitArgs {
     float* c_dec;
     float* xa; int64_t xa_pstride;
     float* mem;
-    float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; float* tail;
+    float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; int* nidx; float* tail;
     int* flag1; int* count; int* done; int* n_steps; int* step; int* n_active;
 };
 
@@ -95,7 +71,6 @@ hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s);
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
-hipError_t launch_stop(const StopArgs& a, hipStream_t s);
 size_t attention_smem_bytes(int Lcap, int location);
 hipError_t attention_prepare(int Lcap, int location);  // raise the dynamic-LDS limit once
 

@@ -49,7 +49,7 @@ struct tts_decoder {
     float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
     float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr;
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
-    int *lens = nullptr, *win_idx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
+    int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
     float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
     int* host_flags = nullptr;  // pinned
@@ -157,13 +157,13 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         a.v = d->v; a.v_b = d->v_b; a.ta_w = d->ta_w; a.ta_b = d->ta_b;
         a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
-        a.h_att = h_att_cur; a.h_pstride = 0;
+        a.h_att = h_att_cur;
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
-        a.tail = d->tail;
-        a.xa = ctx_cur - PRE; a.xa_pstride = 0;  // kernel writes xa[b][PRE + d]
+        a.nidx = d->nidx; a.tail = d->tail;
+        a.ctx = ctx_cur;  // kernel writes ctx[b*XA + d]
         a.align_hist = d->align_hist; a.align_ldb = (int64_t)d->hist_cap * Lmax; a.Lalign = Lmax;
         a.hist_cap = d->hist_cap;
-        a.step = st_cur; a.done = d->done; a.n_active = st_cur + 1;
+        a.step = st_cur; a.done = d->done;
         MARK();
         TTS_HIP(launch_attention(a, s));
     }
@@ -378,6 +378,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->tail, Bc));
     CK(dmalloc(d, &d->lens, Bc));
     CK(dmalloc(d, &d->win_idx, Bc));
+    CK(dmalloc(d, &d->nidx, Bc));
     CK(dmalloc(d, &d->flag1, Bc));
     CK(dmalloc(d, &d->count, Bc));
     CK(dmalloc(d, &d->done, Bc));
@@ -442,7 +443,7 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
     ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
     ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
-    ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
+    ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
     ia.step = d->state; ia.n_active = d->state + 1;
     TTS_HIP(launch_decoder_init(ia, s));
     { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
