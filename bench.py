@@ -36,6 +36,7 @@ t2mod = importlib.import_module("your-voice-tts_amd.tacotron2")
 audiomod = importlib.import_module("your-voice-tts_amd.audio")
 weights = importlib.import_module("your-voice-tts_amd.weights")
 gu = importlib.import_module("your-voice-tts_amd.generic_utils")
+sharding = importlib.import_module("your-voice-tts_amd.sharding")
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA peak (same table)
@@ -71,22 +72,28 @@ def build(args, device):
     return cfg, model, ap
 
 
-def make_ids(args, rank):
+def make_job(args, world, rank, max_steps):
+    """The whole job's sentences (world x batch) and this rank's LPT share (sharding.py)."""
+    n = world * args.batch
     if args.lengths == "fixed":
-        return [weights.synthetic_ids(args.L, 1) for _ in range(args.batch)]  # configs[1]: L=100, seed 1
-    lens = weights.synthetic_lengths(args.batch, 2 + rank)  # configs[2]/[3]: L ~ U{60..160}
-    return [weights.synthetic_ids(int(L), 1000 * rank + b) for b, L in enumerate(lens)]
+        ids = [weights.synthetic_ids(args.L, 1) for _ in range(n)]  # configs[1]: L=100, seed 1
+    else:
+        # configs[2] (B=64, seed 2) on one GPU; configs[3] (B=512 over 8 GPUs, seed 3) otherwise
+        lens = weights.synthetic_lengths(n, 2 if world == 1 else 3)
+        ids = [weights.synthetic_ids(int(L), 100 + b) for b, L in enumerate(lens)]
+    costs = [sharding.sentence_cost(len(x), max_steps) for x in ids]
+    mine = sharding.lpt_partition(costs, world, capacity=args.batch)[rank]
+    return ids, mine
 
 
 @torch.no_grad()
-def run_step(model, ap, ids, world, seed, gather_buf=None):
-    out = model.inference_batch(ids)
+def run_step(model, ap, ids, mine, world, seed):
+    out = model.inference_batch([ids[i] for i in mine])
     wav = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=seed)
     if world > 1:
-        n = gather_buf[0].shape[-1]
-        local = torch.zeros(wav.shape[0], n, dtype=wav.dtype, device=wav.device)
-        local[:, :wav.shape[1]] = wav
-        dist.all_gather_into_tensor(gather_buf[1], local)  # RCCL over xGMI: finished waveforms only
+        # finished waveforms only, gather-v to rank 0 over RCCL (point-to-point, one link per peer)
+        rows = [wav[k, :ap.hop_length * (T - 1)] for k, T in enumerate(out["frames"])]
+        sharding.gather_waveforms(rows, mine, len(ids))
     return out["frames"], wav
 
 
@@ -157,16 +164,11 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     cfg, model, ap = build(args, device)
-    ids = make_ids(args, rank)
-    gather_buf = None
-    if world > 1:
-        # waveform capacity per sentence: 275 * (max frames - 1) with frames <= 2*Lmax+22 under the mask
-        cap = ap.hop_length * (model.decoder.max_decoder_steps + 20)
-        gather_buf = (torch.zeros(args.batch, cap, dtype=torch.float64, device=device),
-                      torch.zeros(world * args.batch, cap, dtype=torch.float64, device=device))
+    all_ids, mine = make_job(args, world, rank, model.decoder.max_decoder_steps)
+    ids = [all_ids[i] for i in mine]
 
     for w in range(args.warmup):
-        run_step(model, ap, ids, world, seed=w, gather_buf=gather_buf)
+        run_step(model, ap, all_ids, mine, world, seed=w)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -174,7 +176,7 @@ def main():
     t0 = time.perf_counter()
     frames = None
     for k in range(args.steps):
-        frames, _ = run_step(model, ap, ids, world, seed=1000 + k, gather_buf=gather_buf)
+        frames, _ = run_step(model, ap, all_ids, mine, world, seed=1000 + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -259,7 +261,8 @@ def main():
                    "sentences_per_gpu": args.batch, "L": args.L if args.lengths == "fixed" else "U{60..160}",
                    "frames_per_step": frames_per_step, "gl_iters": args.iters,
                    "model_config": "config_tacotron2.json + forward_attn_mask (synthesize.py:86)",
-                   "parallelism": f"sentence-sharded x{world}, RCCL waveform gather" if world > 1 else "single GPU"},
+                   "parallelism": (f"sentence-sharded x{world} (LPT), RCCL gather-v of waveforms to rank 0"
+                                   if world > 1 else "single GPU")},
         "rtf": rtf,
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -14,7 +14,8 @@
  *     on the calling thread.  No exceptions cross the ABI.
  *   - A handle is not reentrant: one thread/stream per handle at a time (the reference decoder
  *     keeps per-call state on the module and is not reentrant either, layers/tacotron2.py:161-177).
- *   - All arithmetic is fp32 (fp64 for the inverse pre-emphasis, as scipy.signal.lfilter).
+ *   - Model arithmetic is fp32 (as the reference's torch modules); Griffin-Lim magnitudes, FFTs
+ *     and the inverse pre-emphasis are fp64 (scipy.fftpack / scipy.signal.lfilter precision).
  */
 #ifndef TTS_HIP_H
 #define TTS_HIP_H

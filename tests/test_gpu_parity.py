@@ -127,6 +127,45 @@ def test_batch64_lengths_property():
         assert rel_rms(out["mel_post"][b, :T].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
 
 
+@pytest.mark.parametrize("L", [2, 3, 4, 5])
+def test_shortest_sentences_vs_oracle(L):
+    """L=2..5: the forward mask's negative-index wrap ((n-2) % L) and the clipped window [n-1, n+2]
+    overlap at these lengths; the context must still only sum the surviving positions."""
+    w = weights_mod()
+    fl = golden_flags(golden("t2_fwdmask_L12"))
+    m = _model(fl)
+    ids = w.synthetic_ids(L, 50 + L)
+    out = m.inference_batch([ids])
+    ref = Tacotron2Oracle(w.tacotron2_weights(0), dtype=np.float32, **fl).inference(ids)
+    T = out["frames"][0]
+    assert T == ref["mel"].shape[0]
+    np.testing.assert_array_equal(out["align"][0, :T, :L].cpu().numpy().argmax(1), ref["align"].argmax(1))
+    assert rel_rms(out["mel"][0, :T].cpu().numpy(), ref["mel"]) < MEL_RTOL
+    assert rel_rms(out["mel_post"][0, :T].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
+
+
+def test_sharded_synthesis_single_rank(audio_cfg):
+    """sharding.synthesize_sharded over a 1-rank RCCL group equals the single-process batch."""
+    import torch.distributed as dist
+    sh = load_pkg("sharding")
+    synth = load_pkg("synthesis")
+    audio = load_pkg("audio")
+    w = weights_mod()
+    fl = golden_flags(golden("t2_fwdmask_L12"))
+    m = _model(fl)
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 5})
+    ids = [w.synthetic_ids(L, 7 + L) for L in (9, 17, 4)]
+    store = dist.TCPStore("127.0.0.1", 0, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    try:
+        pcm, info = sh.synthesize_sharded(m, ap, ids, seed=11)
+    finally:
+        dist.destroy_process_group()
+    wavs, _ = synth.synthesize_batch(m, ap, ids, seed=11, phase="device")
+    np.testing.assert_array_equal(pcm, sh.join_int16(wavs))
+    assert info["partition"] == [[0, 1, 2]]
+
+
 @pytest.mark.parametrize("case", sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gl_*mel*.npz"))))
 def test_griffin_lim_vs_reference_glue(case, audio_cfg):
     """inv_mel_spectrogram with the reference's np.random phases (seeded) vs the reference's
