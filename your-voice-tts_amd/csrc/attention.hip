@@ -244,7 +244,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
                     x += lc;
                 }
                 x += j0 == 0 ? pv0[dd] : (j0 == 64 ? pv1[dd] : Pt[(int64_t)d * Lc + jj]);
-                s += vv[d] * tanhf(x);
+                s += vv[d] * tanh_fast(x);
             }
             red[wave * Lc + jj] = s;
         }

@@ -91,4 +91,12 @@ __device__ __forceinline__ int block_argmax(float v, int i, float* scratch, int*
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// tanh from the hardware exp2 / reciprocal (2 transcendental issues instead of the libm
+// range-reduction sequence): absolute error <= ~3e-7 over the whole range, saturating exactly
+// to +-1.  Used where tanh feeds a weighted sum (attention energies), not a recurrence.
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // exp(2x)
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
 }  // namespace tts

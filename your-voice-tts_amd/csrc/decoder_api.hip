@@ -118,7 +118,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     // 1) prenet layer 2 -> xa_cur[b][0:256]   (common_layers.py:77-83; dropout off in eval)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->pre1, 0, -1, PRE, PRE};
+        a.seg[0] = Seg{d->pre1, PRE, PRE};
         a.nseg = 1;
         a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
         a.out = xa_cur; a.ldo = XA;
@@ -128,8 +128,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     // 2) attention LSTM: x = [prenet_t | ctx_{t-1}], h = h_att_{t-1}   (tacotron2.py:195-197)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{xa_cur, 0, -1, XA, XA};
-        a.seg[1] = Seg{h_att_prev, 0, -1, HATT, HATT};
+        a.seg[0] = Seg{xa_cur, XA, XA};
+        a.seg[1] = Seg{h_att_prev, HATT, HATT};
         a.nseg = 2;
         a.W = d->W_att; a.K = XA + HATT; a.N = 4 * HATT; a.bias = d->b_att;
         a.out = h_att_cur; a.ldo = HATT;
@@ -140,7 +140,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     // 3) processed query = query_layer(h_att_t)   (common_layers.py:170/179)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{h_att_cur, 0, -1, HATT, HATT};
+        a.seg[0] = Seg{h_att_cur, HATT, HATT};
         a.nseg = 1;
         a.W = d->W_q; a.K = HATT; a.N = ADIM;
         a.out = d->q; a.ldo = ADIM;
@@ -170,9 +170,9 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     // 5) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec_{t-1}   (tacotron2.py:206-208)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{h_att_cur, 0, -1, HATT, HATT};
-        a.seg[1] = Seg{ctx_cur, 0, -1, XA, ENC};
-        a.seg[2] = Seg{h_dec_prev, 0, -1, HDEC, HDEC};
+        a.seg[0] = Seg{h_att_cur, HATT, HATT};
+        a.seg[1] = Seg{ctx_cur, XA, ENC};
+        a.seg[2] = Seg{h_dec_prev, HDEC, HDEC};
         a.nseg = 3;
         a.W = d->W_dec; a.K = HATT + ENC + HDEC; a.N = 4 * HDEC; a.bias = d->b_dec;
         a.out = h_dec_cur; a.ldo = HDEC;
@@ -184,8 +184,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     //    prenet L1 of the next step; stop = sigmoid(stopnet([h_dec; mel])) + stop rule (:219-277)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{h_dec_cur, 0, -1, HDEC, HDEC};
-        a.seg[1] = Seg{ctx_cur, 0, -1, XA, ENC};
+        a.seg[0] = Seg{h_dec_cur, HDEC, HDEC};
+        a.seg[1] = Seg{ctx_cur, XA, ENC};
         a.nseg = 2;
         a.W = d->W_melf; a.K = HDEC + ENC; a.N = nmel + PRE + 1; a.bias = d->b_melf;
         a.hist = d->mel_hist; a.ldh = (int64_t)d->hist_cap * nmel; a.hist_cap = d->hist_cap;
@@ -225,7 +225,7 @@ tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s) {
     a.B = B;
     a.step = d->state;
     a.out_par = -1;
-    a.seg[0] = Seg{d->mem, 0, -1, d->nmel, d->nmel};
+    a.seg[0] = Seg{d->mem, d->nmel, d->nmel};
     a.nseg = 1;
     a.W = d->W_pre1; a.K = d->nmel; a.N = PRE; a.act = ACT_RELU;
     a.out = d->pre1; a.ldo = PRE;

@@ -92,8 +92,8 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         SGemmArgs a{};
         a.B = B;
         a.out_par = -1;
-        a.seg[0] = Seg{h_prev, 0, -1, EH, EH};
-        a.seg[1] = Seg{h_prev + hs, 0, -1, EH, EH};
+        a.seg[0] = Seg{h_prev, EH, EH};
+        a.seg[1] = Seg{h_prev + hs, EH, EH};
         a.nseg = 1;
         a.W = e->Whh;
         a.K = EH;

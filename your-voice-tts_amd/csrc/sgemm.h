@@ -13,11 +13,10 @@
 namespace tts {
 
 // One input segment of the logically concatenated activation row X[b] = [seg0 | seg1 | seg2].
-// Ping-pong buffers: row pointer = p + ((step + par) & 1) * pstride when par >= 0.
+// Pointers are bound per launch (the decoder captures one graph per step parity), so a launch
+// can issue its activation loads before it reads the device step state.
 struct Seg {
     const float* p;
-    int64_t pstride;
-    int par;  // -1: no ping-pong
     int ld;   // row stride (floats)
     int len;  // multiple of 16
 };

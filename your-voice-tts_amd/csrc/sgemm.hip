@@ -11,18 +11,50 @@ namespace tts {
 
 constexpr int MAX_WAVES = 16;
 constexpr int PRE_DIM = 256;  // prenet width (layers/tacotron2.py:108)
+__device__ const int kOneActive[2] = {0, 1};  // {step 0, 1 active} for launches without step state
 
 // ROLE only names the instantiation (distinct kernel names in rocprof traces per decoder stage).
+// MT = m-tiles of 16 batch rows on the MFMA path; MT = 0 is the batch-1 VALU path.
 template <int MT, int EPI, int ROLE>
 __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
-    // {step, n_active} in one load (adjacent words), issued with the epilogue prefetches
-    const int2 st = a.step ? *reinterpret_cast<const int2*>(a.step) : make_int2(0, 1);
+    constexpr bool VALU = MT == 0;
+    constexpr int NT = VALU ? 1 : MT;
+    // Latency structure (batch-1 decode: every launch is one dependent link of the step chain):
+    // the step state, the epilogue operands, and the wave's whole weight + activation slice are
+    // all issued as vector loads before anything waits, so a launch pays one memory round trip.
+    // (A scalar load of the step state would be waited on at once, before the weight loads
+    // issue.)  The "all sentences done" exit is taken after the MFMAs: it only costs steps past
+    // the end.
+    const int* sp = a.step ? a.step : kOneActive;
+    int st_x = sp[0];
+    int st_y = sp[1];
     const int ntile = blockIdx.x;
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
     const int nw = blockDim.x >> 6;
+    const int tid = threadIdx.x;
     float pre_bias[4] = {0.f, 0.f, 0.f, 0.f}, pre_cell = 0.f;
-    if (EPI == EPI_LSTM && (int)threadIdx.x < a.B * 4) {
+    int pre_done = 0;
+    if ((EPI == EPI_LINEAR || EPI == EPI_MEL_FUSED) && tid < a.B * 16) {
+        const int n = ntile * 16 + (tid & 15);
+        if (a.bias && n < a.N) pre_bias[0] = a.bias[n];
+        if (a.done) pre_done = a.done[tid >> 4];
+    }
+    // stop-rule operands of the fused mel launch (one workgroup, one thread per sentence)
+    const int stop_tile = EPI == EPI_MEL_FUSED ? (a.mf.nmel + PRE_DIM) >> 4 : -1;
+    int sr_done = 1, sr_len = 0, sr_flag = 0, sr_count = 0;
+    float sr_tail = 0.f, sr_bias = 0.f;
+    if (EPI == EPI_MEL_FUSED && ntile == stop_tile && tid < a.B) {
+        sr_done = a.done[tid];
+        sr_len = a.mf.lens[tid];
+        sr_flag = a.mf.flag1[tid];
+        sr_count = a.mf.count[tid];
+        sr_tail = a.mf.tail[tid];
+        // lane-dependent index (B <= 64, so tid & (B >> 8) == 0): a vector load, waited late,
+        // not a scalar one waited at the next kernel-argument load
+        sr_bias = a.bias[a.mf.nmel + PRE_DIM + (tid & (a.B >> 8))];
+    }
+    if (EPI == EPI_LSTM && tid < a.B * 4) {
         const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
 #pragma unroll
         for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
@@ -43,22 +75,15 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             pre_cell = E.c[dir * E.cstride + (int64_t)b * E.H + unit];
         }
     }
-    if (st.y == 0) {
-        // every sentence is done: steps past the end are no-ops, but the fused stop launch
-        // still forwards {step+1, 0} so the next parity slot reads "done" as well
-        if (EPI == EPI_MEL_FUSED && ntile == 0 && threadIdx.x == 0)
-            *reinterpret_cast<int2*>(a.mf.state_next) = make_int2(st.x + 1, 0);
-        return;
-    }
-    const int step = st.x;
     const int nchunks = a.K >> 4;
     const int cbeg = wave * nchunks / nw;
     const int cend = (wave + 1) * nchunks / nw;
 
-    // Per-lane activation base pointers: row b = mt*16 + (lane&15), k offset (lane>>4)*4.
-    const int xrow = lane & 15;
+    // Per-lane activation base pointers: row b = mt*16 + (lane&15) (VALU path: row 0 for every
+    // lane), k offset (lane>>4)*4.
+    const int xrow = VALU ? 0 : lane & 15;
     const int xk = (lane >> 4) * 4;
-    const float* xb[3][MT];
+    const float* xb[3][NT];
     int cb[3];
     int kstart = 0;
 #pragma unroll
@@ -66,27 +91,28 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         // the encoder LSTM reads one segment: its direction's previous hidden state
         const Seg& g = a.seg[EPI == EPI_ENC_LSTM ? (s == 0 ? dir : 2) : s];
         const bool live = EPI == EPI_ENC_LSTM ? s == 0 : s < a.nseg;
-        const float* p = live ? g.p + (g.par >= 0 ? (int64_t)((step + g.par) & 1) * g.pstride : 0) : nullptr;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < NT; ++mt) {
             const int b = mt * 16 + xrow;
-            xb[s][mt] = (live && b < a.B) ? p + (int64_t)b * g.ld + xk - kstart : nullptr;
+            xb[s][mt] = (live && b < a.B) ? g.p + (int64_t)b * g.ld + xk - kstart : nullptr;
         }
         kstart += live ? g.len : 0;
         cb[s] = kstart >> 4;  // first chunk past segment s
     }
 
     // two independent accumulator chains per m-tile (even / odd chunk) hide the MFMA latency
-    floatx4 acc[MT], acc2[MT];
+    floatx4 acc[NT], acc2[NT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = acc2[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < NT; ++mt) acc[mt] = acc2[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float vacc = 0.f, vacc2 = 0.f;  // VALU path
 
     const float4* __restrict__ Wp = reinterpret_cast<const float4*>(a.W) + (size_t)ntile * nchunks * 64 + lane;
-    // U chunks of loads (U KiB of weights per wave) in flight before the first MFMA
-    constexpr int U = MT == 1 ? 8 : (MT == 2 ? 4 : 2);
+    // U chunks of loads (U KiB of weights per wave) in flight before the first FMA; at batch
+    // <= 16 one round covers every decoder shape (<= 10 chunks per wave at 16 waves, K <= 2560)
+    constexpr int U = NT == 1 ? 10 : (NT == 2 ? 4 : 2);
     for (int c0 = cbeg; c0 < cend; c0 += U) {
         float4 wv[U];
-        float4 xv[U][MT];
+        float4 xv[U][NT];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int c = c0 + u;
@@ -94,46 +120,89 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                 wv[u] = Wp[(size_t)c * 64];  // default policy: the 72.7 MB weight set stays in the Infinity Cache across steps
                 const int s = c < cb[0] ? 0 : (c < cb[1] ? 1 : 2);
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
+                for (int mt = 0; mt < NT; ++mt) {
                     const float* p = s == 0 ? xb[0][mt] : (s == 1 ? xb[1][mt] : xb[2][mt]);
                     xv[u][mt] = p ? *reinterpret_cast<const float4*>(p + c * 16) : float4{0.f, 0.f, 0.f, 0.f};
                 }
             } else {
                 wv[u] = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) xv[u][mt] = float4{0.f, 0.f, 0.f, 0.f};
+                for (int mt = 0; mt < NT; ++mt) xv[u][mt] = float4{0.f, 0.f, 0.f, 0.f};
             }
         }
+        if (VALU) {
+            // batch 1: lane (row n = lane&15, k-group lane>>4) dots its 4 weights with x; the
+            // MFMA path would pad the batch to 16 rows and pay 16x the multiplies
 #pragma unroll
-        for (int u = 0; u < U; u += 2) {
+            for (int u = 0; u < U; u += 2) {
+                if (c0 + u < cend) {
+                    vacc = fmaf(wv[u].x, xv[u][0].x, vacc);
+                    vacc = fmaf(wv[u].y, xv[u][0].y, vacc);
+                    vacc = fmaf(wv[u].z, xv[u][0].z, vacc);
+                    vacc = fmaf(wv[u].w, xv[u][0].w, vacc);
+                }
+                if (c0 + u + 1 < cend) {
+                    vacc2 = fmaf(wv[u + 1].x, xv[u + 1][0].x, vacc2);
+                    vacc2 = fmaf(wv[u + 1].y, xv[u + 1][0].y, vacc2);
+                    vacc2 = fmaf(wv[u + 1].z, xv[u + 1][0].z, vacc2);
+                    vacc2 = fmaf(wv[u + 1].w, xv[u + 1][0].w, vacc2);
+                }
+            }
+        } else {
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                acc[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, acc[mt]);
-                acc2[mt] = mfma16x16x4(xv[u + 1][mt].x, wv[u + 1].x, acc2[mt]);
-                acc[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, acc[mt]);
-                acc2[mt] = mfma16x16x4(xv[u + 1][mt].y, wv[u + 1].y, acc2[mt]);
-                acc[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, acc[mt]);
-                acc2[mt] = mfma16x16x4(xv[u + 1][mt].z, wv[u + 1].z, acc2[mt]);
-                acc[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, acc[mt]);
-                acc2[mt] = mfma16x16x4(xv[u + 1][mt].w, wv[u + 1].w, acc2[mt]);
+            for (int u = 0; u < U; u += 2) {
+                if (c0 + u >= cend) break;  // no MFMAs on the zero padding of the last round
+#pragma unroll
+                for (int mt = 0; mt < NT; ++mt) {
+                    acc[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, acc[mt]);
+                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].x, wv[u + 1].x, acc2[mt]);
+                    acc[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, acc[mt]);
+                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].y, wv[u + 1].y, acc2[mt]);
+                    acc[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, acc[mt]);
+                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].z, wv[u + 1].z, acc2[mt]);
+                    acc[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, acc[mt]);
+                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].w, wv[u + 1].w, acc2[mt]);
+                }
             }
         }
     }
+    if (VALU) {
+        // sum the four k-groups (lanes n, n+16, n+32, n+48), then place row n's partial where the
+        // MFMA accumulator fragment keeps C[b=0][n] (lane n, component 0)
+        float v = vacc + vacc2;
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        acc[0] = floatx4{lane < 16 ? v : 0.f, 0.f, 0.f, 0.f};
+    } else {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] += acc2[mt];
+        for (int mt = 0; mt < NT; ++mt) acc[mt] += acc2[mt];
+    }
+
+    // Operands loaded in the prologue are consumed only from here on; the empty asm redefines
+    // them here so the compiler cannot hoist their first use (and its wait) above the loads.
+    asm volatile("" : "+v"(st_x), "+v"(st_y), "+v"(pre_done), "+v"(pre_bias[0]), "+v"(pre_bias[1]),
+                 "+v"(pre_bias[2]), "+v"(pre_bias[3]), "+v"(pre_cell));
+    if (st_y == 0) {
+        // every sentence is done: steps past the end are no-ops, but the fused stop launch
+        // still forwards {step+1, 0} so the next parity slot reads "done" as well
+        if (EPI == EPI_MEL_FUSED && ntile == 0 && tid == 0)
+            *reinterpret_cast<int2*>(a.mf.state_next) = make_int2(st_x + 1, 0);
+        return;
+    }
+    const int step = st_x;
 
     // Cross-wave K reduction in a fixed order.
-    __shared__ float red[MAX_WAVES][MT][64][4];
-    __shared__ float fin[MT * 16][17];
+    __shared__ float red[MAX_WAVES][NT][64][4];
+    __shared__ float fin[NT * 16][17];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int mt = 0; mt < NT; ++mt) {
         red[wave][mt][lane][0] = acc[mt].x;
         red[wave][mt][lane][1] = acc[mt].y;
         red[wave][mt][lane][2] = acc[mt].z;
         red[wave][mt][lane][3] = acc[mt].w;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < MT * 256; e += blockDim.x) {
+    for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
         const int mt = e >> 8, l = (e >> 2) & 63, r = e & 3;
         float s = 0.f;
         for (int w = 0; w < nw; ++w) s += red[w][mt][l][r];
@@ -144,16 +213,16 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     const bool track = a.hist != nullptr && step < a.hist_cap;
     if (EPI == EPI_LINEAR) {
         float* out = a.out ? a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0) : nullptr;
-        for (int e = threadIdx.x; e < a.B * 16; e += blockDim.x) {
-            const int b = e >> 4, col = e & 15;
+        if (tid < a.B * 16) {  // B <= 64: one element per thread
+            const int b = tid >> 4, col = tid & 15;
             const int n = ntile * 16 + col;
-            if (n >= a.N) continue;
-            float v = fin[b][col];
-            if (a.bias) v += a.bias[n];
-            if (a.act == ACT_RELU) v = fmaxf(v, 0.f);
-            if (out) out[(int64_t)b * a.ldo + n] = v;
-            if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
-            if (track && !(a.done && a.done[b])) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
+            if (n < a.N) {
+                float v = fin[b][col] + pre_bias[0];
+                if (a.act == ACT_RELU) v = fmaxf(v, 0.f);
+                if (out) out[(int64_t)b * a.ldo + n] = v;
+                if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
+                if (track && !pre_done) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
+            }
         }
     } else if (EPI == EPI_ENC_LSTM) {
         const EncLstm& E = a.enc;
@@ -174,37 +243,39 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     } else if (EPI == EPI_MEL_FUSED) {
         const MelFused& m = a.mf;
         const int nrow = m.nmel + PRE_DIM + 1;
-        for (int e = threadIdx.x; e < a.B * 16; e += blockDim.x) {
-            const int b = e >> 4, col = e & 15;
+        if (tid < a.B * 16) {
+            const int b = tid >> 4, col = tid & 15;
             const int n = ntile * 16 + col;
-            if (n >= nrow - 1) continue;  // stop row handled below
-            const float v = fin[b][col] + a.bias[n];
-            if (n < m.nmel) {
-                // unguarded by done[]: the stop WG of this same launch may set it; rows past
-                // n_steps are garbage the host masks out (tts_decoder_run zero-fills them)
-                if (track) a.hist[(int64_t)b * a.ldh + (int64_t)step * m.nmel + n] = v;
-            } else {
-                m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
+            if (n < nrow - 1) {  // stop row handled below
+                const float v = fin[b][col] + pre_bias[0];
+                if (n < m.nmel) {
+                    // unguarded by done[]: the stop WG of this same launch may set it; rows past
+                    // n_steps are garbage the host masks out (tts_decoder_run zero-fills them)
+                    if (track) a.hist[(int64_t)b * a.ldh + (int64_t)step * m.nmel + n] = v;
+                } else {
+                    m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
+                }
             }
         }
-        const int stop_tile = (nrow - 1) >> 4;
         if (ntile == stop_tile) {
             // stopnet + stop rule (tacotron2.py:219-224, 257-277): stop_flags[0] is always true;
             // [1] latches (tail > 0.8 and t > L); [2] = t > 2L; then 20 extra steps; the cap is
             // checked only in the `elif`, so a sentence whose flags are all set may pass it.
             __shared__ int sdone[64];
             const int col = (nrow - 1) & 15;
-            const int b = threadIdx.x;
+            const int b = tid;
+            asm volatile("" : "+v"(sr_done), "+v"(sr_len), "+v"(sr_flag), "+v"(sr_count), "+v"(sr_tail),
+                         "+v"(sr_bias));
             if (b < a.B) {
-                int nd = a.done[b];
+                int nd = sr_done;
                 if (!nd) {
-                    const float stv = sigmoidf_(fin[b][col] + a.bias[nrow - 1]);
+                    const float stv = sigmoidf_(fin[b][col] + sr_bias);
                     if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
-                    const int L = m.lens[b];
-                    const int f1 = m.flag1[b] | ((m.tail[b] > 0.8f && step > L) ? 1 : 0);
+                    const int L = sr_len;
+                    const int f1 = sr_flag | ((sr_tail > 0.8f && step > L) ? 1 : 0);
                     m.flag1[b] = f1;
                     if (f1 && step > 2 * L) {
-                        const int c = m.count[b] + 1;
+                        const int c = sr_count + 1;
                         m.count[b] = c;
                         if (c > 20) nd = 1;
                     } else if (step + 1 == m.max_steps) {
@@ -294,11 +365,13 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
 
 template <int EPI, int ROLE>
 static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
-    const int nchunks = a.K / 16;
-    const int nw = nchunks < MAX_WAVES ? nchunks : MAX_WAVES;
-    const dim3 grid((a.N + 15) / 16), block(nw * 64);
+    // always 16 waves (waves past K's chunk count contribute zeros): the epilogues give every
+    // (row, column) of the tile its own thread, B * 16 <= 1024
+    const dim3 grid((a.N + 15) / 16), block(MAX_WAVES * 64);
     const int mt = (a.B + 15) / 16;
-    if (mt <= 1)
+    if (a.B == 1)
+        hipLaunchKernelGGL((sgemm_kernel<0, EPI, ROLE>), grid, block, 0, s, a);
+    else if (mt <= 1)
         hipLaunchKernelGGL((sgemm_kernel<1, EPI, ROLE>), grid, block, 0, s, a);
     else if (mt <= 2)
         hipLaunchKernelGGL((sgemm_kernel<2, EPI, ROLE>), grid, block, 0, s, a);
