@@ -50,8 +50,11 @@ def kernel_algorithmic(name, B, L, frames_total, r=1):
     by = {
         "prenet2": 4 * (256 * 256 + B * (256 + 256)),
         "att_lstm": 4 * (4096 * 1792 + B * (1792 + 3 * 1024)),
-        "query": 4 * (128 * 1024 + B * (1024 + 128)),
-        "attention": 4 * B * (L * 640 + 2 * L + 128 + 512),
+        # query_layer GEMV + energy partials: W_q, h, P (128 per position) in; q and 8 partials out
+        "query": 4 * (128 * 1024 + B * (1024 + 128 + L * (128 + 8))),
+        # energies from partials, forward attention: 8 partials + alpha[j], alpha[j-1] in, alpha and
+        # the alignment row out; the context touches only the <= 5 surviving encoder rows
+        "attention": 4 * B * (L * (8 + 2 + 2) + 5 * 512 + 512),
         "dec_lstm": 4 * (4096 * 2560 + B * (2560 + 3 * 1024)),
         # fused mel projection (nm rows) + folded prenet L1 (256 rows) + folded stopnet (1 row)
         "mel_fused": 4 * ((nm + 257) * 1536 + B * (1536 + nm + 256 + 1)),

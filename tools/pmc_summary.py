@@ -18,7 +18,8 @@ LABELS = [
     (r"sgemm_kernel<\d+, 0, 0>", "prenet2"),
     (r"sgemm_kernel<\d+, 1, 1>", "att_lstm"),
     (r"sgemm_kernel<\d+, 0, 2>", "query"),
-    (r"attention_kernel", "attention"),
+    (r"query_energy_kernel", "query"),
+    (r"attention_kernel|attention_fm_kernel", "attention"),
     (r"sgemm_kernel<\d+, 1, 3>", "dec_lstm"),
     (r"sgemm_kernel<\d+, 2, 5>", "mel_fused"),
     (r"sgemm_kernel<\d+, 3, 6>", "enc_lstm"),

@@ -373,15 +373,212 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     }
 }
 
+// Latency path for the synthesis configuration (synthesize.py:86): forward attention with the
+// eval mask and sigmoid normalisation, no location features, no windowing, no transition agent.
+// Same results as attention_kernel up to fp32 rounding, with one barrier instead of nine:
+//   - the energies arrive as 8 partial sums per position from query_energy_kernel (the 128 tanh
+//     per position run on 8 compute units in the query launch, not on this one);
+//     prev_alpha[j] and prev_alpha[j-1] come straight from global memory;
+//   - the sigmoid normaliser cancels in the forward-attention renormalisation
+//     (alpha = m*s/S / sum(m*s/S)), so it is not reduced;
+//   - one block reduction gives both max(alpha) (for the 0.01*val entry) and the sum of the
+//     surviving window [n-1, n+2]; every thread then knows the <= 5 nonzero weights (read from
+//     LDS after that reduction's barrier), so the context, the tail, the next argmax and the
+//     outputs need no further synchronisation.
+__global__ __launch_bounds__(ATT_THREADS) void attention_fm_kernel(const AttnArgs a) {
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int Lc = a.Lcap;
+    const int64_t row = (int64_t)b * Lc;
+    // ---- phase 0: loads that depend only on the arguments
+    int st_x = a.step[0], st_y = a.step[1];
+    const int L = a.lens[b];
+    const int n = a.nidx[b];
+    const float u = a.u[b];
+    const float vb = a.v_b[0];
+    const int done = a.done[b];
+    const int j = tid;
+    const bool in = j < L;
+    float ep[QE_TILES];
+#pragma unroll
+    for (int k = 0; k < QE_TILES; ++k) ep[k] = j < Lc ? a.epart[((int64_t)b * QE_TILES + k) * Lc + j] : 0.f;
+    const float aold_j = in ? a.alpha[row + j] : 0.f;
+    const float aold_p = (in && j > 0) ? a.alpha[row + j - 1] : 0.f;
+    // the surviving positions after the mask: (n-2) mod L and [n-1, n+2] (Python slicing of
+    // common_layers.py:211-213, including the negative-index wrap for n < 2)
+    const int cx = (n - 2 + L) % L;
+    const int clo = n >= 1 ? n - 1 : L - 1;
+    const int chi = min(n + 2, L - 1);
+    const float* encb = a.enc + row * ENC;
+    float ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tid < ENC) {
+        ex = encb[(int64_t)cx * ENC + tid];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (clo + k <= chi) erow[k] = encb[(int64_t)(clo + k) * ENC + tid];
+    }
+    extern __shared__ __align__(16) float sm[];
+    float* an = sm;         // [Lc] unnormalised forward weights
+    float* scr = an + Lc;   // [2 * ATT_WAVES]
+    asm volatile("" : "+v"(st_x), "+v"(st_y));
+    if (st_y == 0) return;  // every sentence done (uniform)
+    const int t = st_x;
+    // ---- energy (partials from query_energy_kernel), sigmoid, forward mix, mask
+    // (common_layers.py:178-182, 199-213, 241-243)
+    float anj = 0.f;
+    if (in) {
+        float e = 0.f;
+#pragma unroll
+        for (int k = 0; k < QE_TILES; ++k) e += ep[k];
+        const float sg = sigmoidf_(e + vb);
+        const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - u, aold_j), __fmul_rn(u, aold_p)), 1e-8f);
+        anj = __fmul_rn(mix, sg);
+        an[j] = anj;
+    }
+    const bool win = in && j >= clo && j <= chi && j != cx;
+    // one barrier: DPP wave reductions, then every thread folds the 16 wave results in order
+    const float ws = wave_sum_dpp(win ? anj : 0.f);
+    const float wm = wave_max_dpp(in ? anj : -INFINITY);
+    if (lane == 0) {
+        scr[2 * wave] = ws;
+        scr[2 * wave + 1] = wm;
+    }
+    __syncthreads();
+    float rs = 0.f, rm = -INFINITY;
+    for (int k = 0; k < ATT_WAVES; ++k) {
+        rs += scr[2 * k];
+        rm = fmaxf(rm, scr[2 * k + 1]);
+    }
+    const float vx = 0.01f * rm;  // alpha[(n-2)] = 0.01 * val
+    const float denom = rs + vx;
+    auto weight = [&](int p) -> float {  // normalised weight of position p (0 outside the survivors)
+        if (p == cx) return vx / denom;
+        return (p >= clo && p <= chi) ? an[p] / denom : 0.f;
+    };
+    const float w = in ? weight(j) : 0.f;
+    if (in) a.alpha[row + j] = w;
+    if (!done && t < a.hist_cap && a.align_hist && j < a.Lalign)
+        a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + j] = w;
+    if (tid == 0) {
+        a.tail[b] = L >= 2 ? weight(L - 2) + weight(L - 1) : weight(0);  // tacotron2.py:268
+        // next step's n = argmax(prev_alpha) = 1 + first argmax of alpha[0..L-2] (0 if all zero)
+        float bv = 0.f;
+        int bi = -1;
+        auto consider = [&](int p) {
+            const float wp = weight(p);
+            if (p <= L - 2 && wp > bv) { bv = wp; bi = p; }
+        };
+        if (cx < clo) consider(cx);
+        for (int p = clo; p <= chi; ++p) consider(p);
+        if (cx > chi) consider(cx);
+        a.nidx[b] = bi >= 0 ? bi + 1 : 0;
+    }
+    // ---- context over the survivors, in index order (bmm, common_layers.py:217)
+    if (tid < ENC) {
+        float ctx = 0.f;
+        if (cx < clo) ctx += weight(cx) * ex;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (clo + k <= chi) ctx += weight(clo + k) * (clo + k == cx ? ex : erow[k]);
+        if (cx > chi) ctx += weight(cx) * ex;
+        a.ctx[(int64_t)b * XA + tid] = ctx;
+    }
+}
+
+static bool attention_fast(const AttnArgs& a) {
+    return a.forward_attn && a.forward_attn_mask && a.attn_norm == 1 && !a.location_attn && !a.windowing &&
+           !a.trans_agent;
+}
+bool attention_uses_epart(const AttnArgs& a) { return attention_fast(a); }
+
+// ------------------------------------------------------------------ query + energy partials
+__global__ __launch_bounds__(1024) void query_energy_kernel(const QEArgs a) {
+    const int tile = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int Lc = a.Lcap;
+    constexpr int NCH = HATT / 16;      // k-chunks of 16
+    constexpr int CPW = NCH / 16;       // chunks per wave (16 waves)
+    // ---- phase 0: weights, activations, P rows of this thread's position, v, step state
+    int st_y = a.step[1];
+    const int L = a.lens[b];
+    const int j = tid;
+    float pt[16];
+    const float* Pt = a.Pt + ((int64_t)b * ADIM + tile * 16) * Lc;
+#pragma unroll
+    for (int dd = 0; dd < 16; ++dd) pt[dd] = (a.energies && j < Lc) ? Pt[(int64_t)dd * Lc + j] : 0.f;
+    const float4* Wp = reinterpret_cast<const float4*>(a.Wq) + ((size_t)tile * NCH + wave * CPW) * 64 + lane;
+    const float* hb = a.h + (int64_t)b * HATT + (lane >> 4) * 4;
+    float4 wv[CPW], xv[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        wv[c] = Wp[(size_t)c * 64];
+        xv[c] = *reinterpret_cast<const float4*>(hb + (wave * CPW + c) * 16);
+    }
+    float acc = 0.f, acc2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPW; c += 2) {
+        acc = fmaf(wv[c].x, xv[c].x, acc);
+        acc = fmaf(wv[c].y, xv[c].y, acc);
+        acc = fmaf(wv[c].z, xv[c].z, acc);
+        acc = fmaf(wv[c].w, xv[c].w, acc);
+        acc2 = fmaf(wv[c + 1].x, xv[c + 1].x, acc2);
+        acc2 = fmaf(wv[c + 1].y, xv[c + 1].y, acc2);
+        acc2 = fmaf(wv[c + 1].z, xv[c + 1].z, acc2);
+        acc2 = fmaf(wv[c + 1].w, xv[c + 1].w, acc2);
+    }
+    float s = acc + acc2;
+    s += __shfl_xor(s, 16, 64);  // the four k-groups of row (lane & 15)
+    s += __shfl_xor(s, 32, 64);
+    asm volatile("" : "+v"(st_y));
+    if (st_y == 0) return;  // every sentence done (uniform)
+    __shared__ float red[16][16];
+    __shared__ float qs[16];
+    if (lane < 16) red[wave][lane] = s;
+    __syncthreads();
+    if (tid < 16) {
+        float q = 0.f;
+        for (int w = 0; w < 16; ++w) q += red[w][tid];  // fixed order: deterministic
+        qs[tid] = q;
+        a.q[(int64_t)b * ADIM + tile * 16 + tid] = q;
+    }
+    if (!a.energies) return;
+    __syncthreads();
+    if (j < L) {
+        float e = 0.f;
+#pragma unroll
+        for (int dd = 0; dd < 16; ++dd) e += a.v[tile * 16 + dd] * tanh_fast(qs[dd] + pt[dd]);
+        a.epart[((int64_t)b * QE_TILES + tile) * Lc + j] = e;
+    }
+}
+
+hipError_t launch_query_energy(const QEArgs& a, int B, hipStream_t s) {
+    hipLaunchKernelGGL(query_energy_kernel, dim3(QE_TILES, B), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+static size_t attention_fm_smem_bytes(int Lcap) {
+    return ((size_t)Lcap + 2 * ATT_WAVES) * sizeof(float);
+}
+
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(attention_kernel, dim3(a.B), dim3(ATT_THREADS), attention_smem_bytes(a.Lcap, a.location_attn),
-                       s, a);
+    if (attention_fast(a)) {
+        hipLaunchKernelGGL(attention_fm_kernel, dim3(a.B), dim3(ATT_THREADS), attention_fm_smem_bytes(a.Lcap), s, a);
+    } else {
+        hipLaunchKernelGGL(attention_kernel, dim3(a.B), dim3(ATT_THREADS),
+                           attention_smem_bytes(a.Lcap, a.location_attn), s, a);
+    }
     return hipGetLastError();
 }
 
 hipError_t attention_prepare(int Lcap, int location) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_smem_bytes(Lcap, location));
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)attention_smem_bytes(Lcap, location));
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_fm_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_fm_smem_bytes(Lcap));
 }
 
 }  // namespace tts

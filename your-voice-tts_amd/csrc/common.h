@@ -45,6 +45,34 @@ __device__ __forceinline__ float wave_max(float v) {
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
 }
+// DPP wave reductions (VALU data-parallel-primitive lanes moves: no LDS round trip per level as
+// __shfl_xor's ds_bpermute has).  Inclusive row scans by row_shr 1/2/4/8, then row_bcast:15 and
+// row_bcast:31 carry rows into lane 63; the total is read from lane 63 (wave-uniform result).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_move(float v, float identity) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(identity), __float_as_int(v), CTRL, ROW_MASK,
+                                                      0xf, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    v += dpp_move<0x111, 0xf>(v, 0.f);  // row_shr:1
+    v += dpp_move<0x112, 0xf>(v, 0.f);  // row_shr:2
+    v += dpp_move<0x114, 0xf>(v, 0.f);  // row_shr:4
+    v += dpp_move<0x118, 0xf>(v, 0.f);  // row_shr:8
+    v += dpp_move<0x142, 0xa>(v, 0.f);  // row_bcast:15 into rows 1, 3
+    v += dpp_move<0x143, 0xc>(v, 0.f);  // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+    const float id = -INFINITY;
+    v = fmaxf(v, dpp_move<0x111, 0xf>(v, id));
+    v = fmaxf(v, dpp_move<0x112, 0xf>(v, id));
+    v = fmaxf(v, dpp_move<0x114, 0xf>(v, id));
+    v = fmaxf(v, dpp_move<0x118, 0xf>(v, id));
+    v = fmaxf(v, dpp_move<0x142, 0xa>(v, id));
+    v = fmaxf(v, dpp_move<0x143, 0xc>(v, id));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // (value, index) max with first-index tie break (torch.argmax / max(dim) semantics).
 __device__ __forceinline__ void wave_argmax(float& v, int& i) {
 #pragma unroll

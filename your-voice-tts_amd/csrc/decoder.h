@@ -33,6 +33,7 @@ struct AttnArgs {
     const float* enc;      // [B][Lcap][512]
     const int* lens;       // [B]
     const float* h_att;    // [B][1024] this step's attention-LSTM output
+    const float* epart;    // [B][ADIM/16][Lcap] energy partials from query_energy_kernel (fast path)
     // state
     float* alpha;          // [B][Lcap]
     float* att_w;          // [B][Lcap]
@@ -66,6 +67,27 @@ struct InitArgs {
     float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; int* nidx; float* tail;
     int* flag1; int* count; int* done; int* n_steps; int* step; int* n_active;
 };
+
+// Processed query + energy partials (one workgroup per (16 attention dims, sentence)):
+//   q[b][d] = W_q h_att[b]  (query_layer, common_layers.py:170/179)
+//   epart[b][tile][j] = sum_{d in tile} v[d] tanh(q[b][d] + P[b][j][d])  (get_attention, :178-182)
+// The attention launch sums the ADIM/16 partials per position instead of evaluating 128 tanh
+// per position on one compute unit.
+constexpr int QE_TILES = ADIM / 16;
+struct QEArgs {
+    const float* Wq;    // sgemm-packed W_q [QE_TILES][HATT/16 chunks][64 lanes][4]
+    const float* h;     // [B][HATT] h_att_t
+    const float* v;     // [ADIM]
+    const float* Pt;    // [B][ADIM][Lcap]
+    const int* lens;
+    int Lcap;
+    int energies;       // 0: q only (the general attention kernel evaluates the energies itself)
+    float* q;           // [B][ADIM]
+    float* epart;       // [B][QE_TILES][Lcap]
+    const int* step;    // int2 {step, n_active}
+};
+hipError_t launch_query_energy(const QEArgs& a, int B, hipStream_t s);
+bool attention_uses_epart(const AttnArgs& a);
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s);

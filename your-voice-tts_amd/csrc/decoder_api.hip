@@ -47,7 +47,8 @@ struct tts_decoder {
     // workspace
     int Lcap = 0, Bcap = 0, hist_cap = 0;
     float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
-    float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr;
+    float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr, *epart = nullptr;
+    bool fast_attention = false;  // attention_uses_epart(): energies evaluated in the query launch
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
@@ -137,15 +138,15 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_ATT_LSTM, s));
     }
-    // 3) processed query = query_layer(h_att_t)   (common_layers.py:170/179)
+    // 3) processed query = query_layer(h_att_t) (common_layers.py:170/179) and, for the fast
+    //    attention path, the energy partials v . tanh(q + P_j) over 16 dims per workgroup
     {
-        SGemmArgs a = g;
-        a.seg[0] = Seg{h_att_cur, HATT, HATT};
-        a.nseg = 1;
-        a.W = d->W_q; a.K = HATT; a.N = ADIM;
-        a.out = d->q; a.ldo = ADIM;
+        QEArgs a{};
+        a.Wq = d->W_q; a.h = h_att_cur; a.v = d->v; a.Pt = d->Pt; a.lens = d->lens; a.Lcap = d->Lcap;
+        a.energies = d->fast_attention ? 1 : 0;
+        a.q = d->q; a.epart = d->epart; a.step = st_cur;
         MARK();
-        TTS_HIP(sgemm_launch(a, ROLE_QUERY, s));
+        TTS_HIP(launch_query_energy(a, B, s));
     }
     // 4) attention (energies, norm, forward attention, context -> ctx_t)
     {
@@ -158,6 +159,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
         a.h_att = h_att_cur;
+        a.epart = d->epart;
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
         a.nidx = d->nidx; a.tail = d->tail;
         a.ctx = ctx_cur;  // kernel writes ctx[b*XA + d]
@@ -371,6 +373,14 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->mem, (size_t)Bc * nmel));
     CK(dmalloc(d, &d->pre1, (size_t)Bc * PRE));
     CK(dmalloc(d, &d->q, (size_t)Bc * ADIM));
+    CK(dmalloc(d, &d->epart, (size_t)Bc * QE_TILES * Lc));
+    {
+        AttnArgs probe{};
+        probe.attn_norm = cfg->attn_norm; probe.forward_attn = cfg->forward_attn; probe.trans_agent = cfg->trans_agent;
+        probe.forward_attn_mask = cfg->forward_attn_mask; probe.location_attn = cfg->location_attn;
+        probe.windowing = cfg->windowing;
+        d->fast_attention = attention_uses_epart(probe);
+    }
     CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_cum, (size_t)Bc * Lc));
