@@ -229,8 +229,10 @@ def main():
         kd = model.profile_step_kernels(reps=50)
         kg = ap.profile_gl_kernels(reps=20)
         launches = {k: steps for k in kd}
+        # one GL iteration = overlap-add launch (frames -> float32 signal) + per-frame
+        # STFT/iSTFT launch; priced together against SURVEY 8(d)'s bytes per frame-iteration
         launches["gl_iter"] = args.iters
-        allk = {**kd, "gl_iter": kg["gl_iter"]}
+        allk = {**kd, "gl_iter": kg["gl_iter"] + kg["gl_ola"]}
         for k, ms in allk.items():
             kind, alg = kernel_algorithmic(k, B, Lmean, frames_total)
             kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],

@@ -152,8 +152,9 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
 tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
 
 /* Measurement only: re-runs `reps` GL iterations of the last tts_gl_run's batch eagerly with
- * HIP events around each kernel on its stream; returns mean ms of [iteration kernel, final
- * overlap-add kernel].  Clobbers the internal frame buffers (not the caller's outputs). */
+ * HIP events around each kernel on its stream; returns mean ms of [per-frame STFT/iSTFT kernel,
+ * overlap-add kernel] (one iteration launches both).  Clobbers the internal frame and signal
+ * buffers (not the caller's outputs). */
 #define TTS_GL_KERNELS 2
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels);
 

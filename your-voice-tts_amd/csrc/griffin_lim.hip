@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
 // ---------------------------------------------------------------- GL iteration
 struct IterArgs {
     const double* S;      // [B][Fmax][1025]
-    const double* prev;   // frames of the previous iteration (null for the initial iSTFT)
+    const float* y;       // [B][Nmax] the previous iteration's float32 signal (gl_ola_kernel)
+    int64_t Nmax;
     double* next;         // frames written by this iteration
     const int* F;
     int Fmax;
@@ -223,15 +224,12 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     if (!INIT) {
         // ---- STFT frame f of the previous iteration's float32 signal (librosa stft, centre reflect pad)
         const int N = g.hop * (Fb - 1);
-        const double* fr = a.prev + (int64_t)b * a.Fmax * g.winp;
+        const float* yb = a.y + (int64_t)b * a.Nmax;
         double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
         for (int n = tid; n < NFFT; n += GL_THREADS) {
             const double w = a.c.win[n];
             double v = 0.0;
-            if (w != 0.0) {
-                const int p = reflect_idx(f * g.hop + n - NFFT / 2, N);
-                v = w * (double)ola_sample(fr, p + NFFT / 2, Fb, g, a.c.win2);
-            }
+            if (w != 0.0) v = w * (double)yb[reflect_idx(f * g.hop + n - NFFT / 2, N)];
             xr[n] = v;
         }
         __syncthreads();
@@ -529,22 +527,36 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.c = GLConst{g->win, g->win2, g->tw};
     ia.phase_u = phase_u;
     ia.seed = seed;
-    ia.prev = nullptr;
+    ia.y = g->y;
+    ia.Nmax = Nmax;
     ia.next = g->frames;
     const dim3 grid(Fmax, B), block(GL_THREADS);
     hipLaunchKernelGGL(gl_iter_kernel<true>, grid, block, 0, s, ia);
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_t0, s));
+    FinArgs fa{};
+    fa.F = g->F;
+    fa.Fmax = Fmax;
+    fa.B = B;
+    fa.g = geo;
+    fa.c = ia.c;
+    fa.y = g->y;
+    fa.Nmax = Nmax;
+    const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
     if (iters > 0) {
+        // one iteration = overlap-add of the previous frames into the float32 signal (every
+        // sample once) + one workgroup per frame for STFT -> phase -> iSTFT of that signal
         GraphKey key{B, Fmax, iters};
         auto it = g->graphs.find(key);
         if (it == g->graphs.end()) {
             hipGraph_t graph = nullptr;
             TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             for (int i = 0; i < iters; ++i) {
+                FinArgs o = fa;
+                o.frames = g->frames + (i & 1) * fstride;
+                hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, o);
                 IterArgs a = ia;
                 a.phase_u = nullptr;
-                a.prev = g->frames + (i & 1) * fstride;
                 a.next = g->frames + ((i + 1) & 1) * fstride;
                 hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
             }
@@ -560,16 +572,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
     TTS_HIP(hipEventRecord(g->ev_t1, s));
-    FinArgs fa{};
     fa.frames = g->frames + (iters & 1) * fstride;
-    fa.F = g->F;
-    fa.Fmax = Fmax;
-    fa.B = B;
-    fa.g = geo;
-    fa.c = ia.c;
-    fa.y = g->y;
-    fa.Nmax = Nmax;
-    hipLaunchKernelGGL(gl_ola_kernel, dim3((Nmax + 255) / 256, B), dim3(256), 0, s, fa);
+    hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, fa);
     TTS_HIP(hipGetLastError());
     hipLaunchKernelGGL(preemph_scan_kernel, dim3(B), dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop,
                        g->cfg.preemphasis, g->cfg.preemphasis != 0.0 ? 1 : 0, wav);
@@ -578,7 +582,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
     TTS_HIP(hipEventSynchronize(g->ev_t1));
     TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
-    g->last_launches = iters;
+    g->last_launches = 2 * iters;
     g->have_last = true;
     g->last_iter = ia;
     g->last_fin = fa;
@@ -596,23 +600,23 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
     const dim3 grid(ia.Fmax, ia.B), block(GL_THREADS);
     double it_ms = 0.0, ola_ms = 0.0;
     for (int r = 0; r < reps; ++r) {
+        // one GL iteration as tts_gl_run launches it: overlap-add -> per-frame STFT/iSTFT
+        FinArgs f = g->last_fin;
+        f.frames = g->frames + (r & 1) * g->last_fstride;
         IterArgs a = ia;
         a.phase_u = nullptr;
-        a.prev = g->frames + (r & 1) * g->last_fstride;
         a.next = g->frames + ((r + 1) & 1) * g->last_fstride;
         TTS_HIP(hipEventRecord(ev[0], s));
-        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+        hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[1], s));
-        FinArgs f = g->last_fin;
-        f.frames = a.next;
-        hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
+        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[2], s));
         TTS_HIP(hipEventSynchronize(ev[2]));
         float a_ms = 0.f, b_ms = 0.f;
-        TTS_HIP(hipEventElapsedTime(&a_ms, ev[0], ev[1]));
-        TTS_HIP(hipEventElapsedTime(&b_ms, ev[1], ev[2]));
+        TTS_HIP(hipEventElapsedTime(&b_ms, ev[0], ev[1]));
+        TTS_HIP(hipEventElapsedTime(&a_ms, ev[1], ev[2]));
         it_ms += a_ms;
         ola_ms += b_ms;
     }
