@@ -51,12 +51,30 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 }
 __device__ __forceinline__ double2 cconj(double2 a) { return double2{a.x, -a.y}; }
 
-// Stockham radix-4, 5 passes, 256 threads x 1 butterfly.  Returns the buffer holding the result.
-template <bool INV>
-__device__ double2* fft1024(double2* src, double2* dst, const double2* __restrict__ tw) {
+// Per-thread twiddles of the four twiddled Stockham passes (Ns = 4, 16, 64, 256): loaded once per
+// kernel with the other operands, so the FFT passes wait only on LDS.
+struct FftTw {
+    double2 w[4][3];
+};
+__device__ __forceinline__ FftTw load_fft_tw(const double2* __restrict__ tw) {
+    FftTw t;
     const int j = threadIdx.x;
 #pragma unroll
-    for (int Ns = 1; Ns < NH; Ns *= 4) {
+    for (int p = 0; p < 4; ++p) {
+        const int Ns = 4 << (2 * p);
+        const int k = j & (Ns - 1);
+#pragma unroll
+        for (int r = 1; r < 4; ++r) t.w[p][r - 1] = tw[k * r * (512 / Ns)];
+    }
+    return t;
+}
+
+// Stockham radix-4, 5 passes, 256 threads x 1 butterfly.  Returns the buffer holding the result.
+template <bool INV>
+__device__ double2* fft1024(double2* src, double2* dst, const FftTw& tw) {
+    const int j = threadIdx.x;
+#pragma unroll
+    for (int Ns = 1, p = -1; Ns < NH; Ns *= 4, ++p) {
         const int k = j & (Ns - 1);
         double2 v[4];
 #pragma unroll
@@ -64,7 +82,7 @@ __device__ double2* fft1024(double2* src, double2* dst, const double2* __restric
         if (Ns > 1) {
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
-                double2 w = tw[k * r * (512 / Ns)];
+                double2 w = tw.w[p][r - 1];
                 if (INV) w = cconj(w);
                 v[r] = cmul(v[r], w);
             }
@@ -220,43 +238,73 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     __shared__ __align__(16) double2 buf1[NH];
     __shared__ __align__(16) double2 X[NB + 1];
     const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    // ---- phase 0: every global operand of the frame is issued before anything waits (one memory
+    // round trip per frame instead of one per FFT pass): twiddles, window, |S|, the input samples
+    constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;   // bins per thread (5)
+    constexpr int PN = NFFT / GL_THREADS;                    // samples per thread (8)
+    const FftTw ftw = load_fft_tw(a.c.tw);
+    double2 tk[PK];
+    double sk[PK];
+#pragma unroll
+    for (int i = 0; i < PK; ++i) {
+        const int k = tid + i * GL_THREADS;
+        tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
+        sk[i] = k < NB ? Sf[k] : 0.0;
+    }
+    constexpr int PW = (NFFT + GL_THREADS - 1) / GL_THREADS;  // output samples per thread (<= 8)
+    double wo[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int n = tid + i * GL_THREADS;
+        wo[i] = n < g.win ? a.c.win[g.woff + n] : 0.0;
+    }
 
     if (!INIT) {
         // ---- STFT frame f of the previous iteration's float32 signal (librosa stft, centre reflect pad)
         const int N = g.hop * (Fb - 1);
         const float* yb = a.y + (int64_t)b * a.Nmax;
-        double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
-        for (int n = tid; n < NFFT; n += GL_THREADS) {
-            const double w = a.c.win[n];
-            double v = 0.0;
-            if (w != 0.0) v = w * (double)yb[reflect_idx(f * g.hop + n - NFFT / 2, N)];
-            xr[n] = v;
+        double wi[PN];
+        float yi[PN];
+#pragma unroll
+        for (int i = 0; i < PN; ++i) {
+            const int n = tid + i * GL_THREADS;
+            const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
+            wi[i] = sup ? a.c.win[n] : 0.0;
+            yi[i] = sup ? yb[reflect_idx(f * g.hop + n - NFFT / 2, N)] : 0.f;
         }
+        double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
+#pragma unroll
+        for (int i = 0; i < PN; ++i) xr[tid + i * GL_THREADS] = wi[i] * (double)yi[i];
         __syncthreads();
-        const double2* Z = fft1024<false>(buf0, buf1, a.c.tw);
+        const double2* Z = fft1024<false>(buf0, buf1, ftw);
         // real-FFT split; the STFT value is stored complex64 (librosa stft dtype) and its phase
         // exp(i angle(X)) (angle(0) = 0) is applied to |S| in float64 (utils/audio.py:187-188)
-        for (int k = tid; k < NB; k += GL_THREADS) {
+#pragma unroll
+        for (int i = 0; i < PK; ++i) {
+            const int k = tid + i * GL_THREADS;
+            if (k >= NB) break;
             const double2 zk = Z[k & (NH - 1)];
             const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
             const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
             const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};  // -i (zk - zc) / 2
-            const double2 t = a.c.tw[k];
+            const double2 t = tk[i];
             const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
             const double r = sqrt(xre * xre + xim * xim);
-            const double s = Sf[k];
+            const double s = sk[i];
             X[k] = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
         }
     } else {
         // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183)
-        for (int k = tid; k < NB; k += GL_THREADS) {
+#pragma unroll
+        for (int i = 0; i < PK; ++i) {
+            const int k = tid + i * GL_THREADS;
+            if (k >= NB) break;
             const double u = a.phase_u ? a.phase_u[((int64_t)b * NB + k) * a.Fmax + f]
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
             sincos(2.0 * M_PI * u, &sn, &cs);
-            const double s = Sf[k];
-            X[k] = double2{s * cs, s * sn};
+            X[k] = double2{sk[i] * cs, sk[i] * sn};
         }
     }
     __syncthreads();
@@ -266,22 +314,25 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         X[NB - 1].y = 0.0;
     }
     __syncthreads();
-    for (int k = tid; k < NH; k += GL_THREADS) {
+#pragma unroll
+    for (int i = 0; i < NH / GL_THREADS; ++i) {
+        const int k = tid + i * GL_THREADS;
         const double2 xk = X[k];
         const double2 xc = cconj(X[NH - k]);
         const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
         const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
-        const double2 O = cmul(D, cconj(a.c.tw[k]));
+        const double2 O = cmul(D, cconj(tk[i]));
         buf0[k] = double2{E.x - O.y, E.y + O.x};  // E + i O
     }
     __syncthreads();
-    const double2* z = fft1024<true>(buf0, buf1, a.c.tw);
+    const double2* z = fft1024<true>(buf0, buf1, ftw);
     // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft)
     double* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
     const double* zr = reinterpret_cast<const double*>(z);
-    for (int n = tid; n < g.win; n += GL_THREADS) {
-        const int m = g.woff + n;
-        out[n] = a.c.win[m] * (zr[m] * (1.0 / NH));
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int n = tid + i * GL_THREADS;
+        if (n < g.win) out[n] = wo[i] * (zr[g.woff + n] * (1.0 / NH));
     }
 }
 
