@@ -46,60 +46,58 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
             for (int j = 0; j < TN; ++j) acc[k][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const int* idsb = a.ids ? a.ids + (int64_t)b * a.Tmax : nullptr;
     float4 xr[XR], wr[WR];
-    auto gload = [&](int ci0) {
-#pragma unroll
-        for (int q = 0; q < XR; ++q) {
-            const int i = tid + q * 256;
-            float4 v = float4{0.f, 0.f, 0.f, 0.f};
-            if (i < XN) {
-                const int r = i / (BK / 4), c4 = i % (BK / 4);
-                const int t = t0 - PAD + r;
-                if (t >= 0 && t < Tb) {
-                    const float* src = idsb ? a.table + (int64_t)idsb[t] * a.Cin
-                                            : a.in + ((int64_t)b * a.Tmax + t) * a.Cin;
-                    v = *reinterpret_cast<const float4*>(src + ci0 + c4 * 4);
-                }
-            }
-            xr[q] = v;
-        }
-#pragma unroll
-        for (int q = 0; q < WR; ++q) {
-            const int i = tid + q * 256;
-            if (i < WN4) {
-                const int c4 = i % (BN / 4), rk = i / (BN / 4);  // rk = ci_local * KW + k
-                wr[q] = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0 * KW + rk)) * a.co_pad + c0 + c4 * 4);
-            }
-        }
-    };
-    auto lstore = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < XR; ++q) {
-            const int i = tid + q * 256;
-            if (i < XN) {
-                const int r = i / (BK / 4), c4 = i % (BK / 4);
-                xs[buf][r][c4 * 4 + 0] = xr[q].x;
-                xs[buf][r][c4 * 4 + 1] = xr[q].y;
-                xs[buf][r][c4 * 4 + 2] = xr[q].z;
-                xs[buf][r][c4 * 4 + 3] = xr[q].w;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < WR; ++q) {
-            const int i = tid + q * 256;
-            if (i < WN4) {
-                const int c4 = i % (BN / 4), rk = i / (BN / 4);
-                *reinterpret_cast<float4*>(&ws[buf][rk / KW][rk % KW][c4 * 4]) = wr[q];
-            }
-        }
-    };
+    // global -> registers for the K step starting at input channel CI0, and registers -> LDS
+    // stage BUF.  Every register of xr/wr is loaded unconditionally (clamped indices, a valid
+    // dummy row for padding frames) so the arrays stay in VGPRs across the pipelined loop; a
+    // guarded load leaves them partially defined and the compiler spills them to scratch.
+#define CONV_GLOAD(CI0)                                                                                          \
+    {                                                                                                            \
+        const int ci0_ = (CI0);                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                          \
+            const int i = min(tid + q * 256, XN - 1);                                                            \
+            const int r = i / (BK / 4), c4 = i % (BK / 4);                                                       \
+            const int t = t0 - PAD + r;                                                                          \
+            const bool ok = t >= 0 && t < Tb;                                                                    \
+            const int tc = ok ? t : 0;                                                                           \
+            const float* src = idsb ? a.table + (int64_t)idsb[tc] * a.Cin : a.in + ((int64_t)b * a.Tmax + tc) * a.Cin; \
+            const float4 v = *reinterpret_cast<const float4*>(src + ci0_ + c4 * 4);                              \
+            xr[q] = ok ? v : float4{0.f, 0.f, 0.f, 0.f};                                                         \
+        }                                                                                                        \
+        _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                          \
+            const int i = min(tid + q * 256, WN4 - 1);                                                           \
+            const int c4 = i % (BN / 4), rk = i / (BN / 4); /* rk = ci_local * KW + k */                         \
+            wr[q] = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0_ * KW + rk)) * a.co_pad + c0 + c4 * 4); \
+        }                                                                                                        \
+    }
+#define CONV_LSTORE(BUF)                                                                                         \
+    {                                                                                                            \
+        const int buf_ = (BUF);                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                          \
+            const int i = tid + q * 256;                                                                         \
+            if (i < XN) {                                                                                        \
+                const int r = i / (BK / 4), c4 = i % (BK / 4);                                                   \
+                xs[buf_][r][c4 * 4 + 0] = xr[q].x;                                                               \
+                xs[buf_][r][c4 * 4 + 1] = xr[q].y;                                                               \
+                xs[buf_][r][c4 * 4 + 2] = xr[q].z;                                                               \
+                xs[buf_][r][c4 * 4 + 3] = xr[q].w;                                                               \
+            }                                                                                                    \
+        }                                                                                                        \
+        _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                          \
+            const int i = tid + q * 256;                                                                         \
+            if (i < WN4) {                                                                                       \
+                const int c4 = i % (BN / 4), rk = i / (BN / 4);                                                  \
+                *reinterpret_cast<float4*>(&ws[buf_][rk / KW][rk % KW][c4 * 4]) = wr[q];                         \
+            }                                                                                                    \
+        }                                                                                                        \
+    }
     const int nsteps = a.Cin / BK;
-    gload(0);
-    lstore(0);
+    CONV_GLOAD(0);
+    CONV_LSTORE(0);
     __syncthreads();
     const int row = lane & 15, kq = lane >> 4;
     for (int st = 0; st < nsteps; ++st) {
         const int cur = st & 1;
-        if (st + 1 < nsteps) gload((st + 1) * BK);
+        CONV_GLOAD(min(st + 1, nsteps - 1) * BK);  // the last step reloads itself (unused)
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
 #pragma unroll
@@ -115,9 +113,11 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
                     for (int j = 0; j < TN; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
             }
         }
-        if (st + 1 < nsteps) lstore(cur ^ 1);
+        CONV_LSTORE(cur ^ 1);  // the other stage: every wave left it at the previous barrier
         __syncthreads();
     }
+#undef CONV_GLOAD
+#undef CONV_LSTORE
     // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)
     float* outb = a.out + (int64_t)b * a.Tmax * a.Cout;
     const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * a.Cout : nullptr;
