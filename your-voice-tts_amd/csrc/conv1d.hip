@@ -21,9 +21,16 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     constexpr int BN = CONV_BN;
     constexpr int TM = BM / WM / 16;
     constexpr int TN = BN / WN / 16;
-    const int b = blockIdx.z;
-    const int t0 = blockIdx.x * BM;
-    const int c0 = blockIdx.y * BN;
+    // 1-D grid, output-channel tile fastest: under round-robin workgroup placement XCD = bx % 8,
+    // so every XCD works on a fixed set of channel tiles and its L2 keeps their weight slabs
+    // (655 KB each at Cin = 512) across all the frame tiles it is given (speed only).
+    const int ntl = a.co_pad / BN;
+    const int ntile = blockIdx.x % ntl;
+    const int rest = blockIdx.x / ntl;
+    const int mtiles = (a.Tmax + BM - 1) / BM;
+    const int b = rest / mtiles;
+    const int t0 = (rest % mtiles) * BM;
+    const int c0 = ntile * BN;
     const int Tb = a.T[b];
     if (t0 >= Tb) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -173,10 +180,10 @@ template <int KW>
 hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
     const dim3 block(256);
     if (frames_hint <= 4096) {
-        const dim3 grid((a.Tmax + 15) / 16, a.co_pad / CONV_BN, B);
+        const dim3 grid(((a.Tmax + 15) / 16) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4>), grid, block, 0, s, a);
     } else {
-        const dim3 grid((a.Tmax + 63) / 64, a.co_pad / CONV_BN, B);
+        const dim3 grid(((a.Tmax + 63) / 64) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 64, 2, 2>), grid, block, 0, s, a);
     }
     return hipGetLastError();
