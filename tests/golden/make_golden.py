@@ -11,6 +11,11 @@ image and not on the numeric path) stubbed in ``sys.modules``; it is built with
 overrides, loaded with weights from ``weights.py``'s deterministic generator, put in eval
 mode and run through ``inference`` on seeded ids.  Inputs and outputs are saved.
 
+Tacotron / TacotronGST half (gst_*.npz, taco_*.npz): the reference ``Tacotron`` /
+``TacotronGST`` (``models/tacotron.py``, ``models/tacotrongst.py``) built the same way from
+``config_tacotron.json`` / ``config_tacotron_gst.json`` (+ per-case overrides), with
+``weights.tacotron_gst_weights`` and, for GST cases, a seeded synthetic style mel.
+
 GL half (gl_*.npz): the reference ``AudioProcessor`` (``utils/audio.py``) is imported with
 ``librosa``/``soundfile`` replaced by the oracle's librosa-0.6.2 restatement (librosa is
 absent), and ``np.complex`` aliased to ``complex`` (removed in numpy>=1.24; same meaning).  This
@@ -114,6 +119,64 @@ def make_model_fixtures():
         print(f"{name}: L={L} T={mel.shape[1]} flags={flags}")
 
 
+# name, config file, L, id seed, num_speakers, speaker id, (style frames, style seed) or None,
+# max_decoder_steps, overrides.  Small L exercise the stop rule (layers/tacotron.py:464-469): L=2
+# stops on the stop token at t=1, L=4/10 on the alignment tail, L=24 runs into the cap.
+TACO_CASES = [
+    ("gst_L24_style_spk", "config_tacotron_gst.json", 24, 21, 4, 1, (60, 31), 20, {}),
+    ("gst_L10_nostyle", "config_tacotron_gst.json", 10, 50, 0, None, None, 40, {}),
+    ("gst_L4_style", "config_tacotron_gst.json", 4, 44, 0, None, (33, 32), 40, {}),
+    ("gst_L2_nostyle", "config_tacotron_gst.json", 2, 42, 0, None, None, 40, {}),
+    ("taco_L10_loc_ta", "config_tacotron.json", 10, 50, 0, None, None, 40, dict(location_attn=True)),
+    ("taco_L12_softmax", "config_tacotron.json", 12, 23, 0, None, None, 16,
+     dict(attention_norm="softmax", use_forward_attn=False, transition_agent=False)),
+]
+
+
+def make_taco_fixtures():
+    import torch
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    from utils.generic_utils import load_config, setup_model
+    torch.set_num_threads(os.cpu_count())
+    for name, cfgname, L, seed, nspk, spk, style, cap, over in TACO_CASES:
+        C = load_config(os.path.join(REF, cfgname))
+        C.update(over)
+        gst = C.model == "TacotronGST"
+        model = setup_model(130, nspk, C)
+        sd = weights.tacotron_gst_weights(0, num_chars=130, num_speakers=nspk, r=C.r, memory_size=C.memory_size,
+                                          location_attn=C.location_attn, trans_agent=C.transition_agent, gst=gst)
+        assert list(model.state_dict().keys()) == list(sd.keys()), (set(model.state_dict()) ^ set(sd))
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        model.eval()
+        model.decoder.max_decoder_steps = cap
+        ids = weights.synthetic_ids(L, seed)
+        x = torch.from_numpy(ids)[None]
+        sm = weights.synthetic_style_mel(*style)[None] if style else None
+        sid = torch.tensor([spk]) if spk is not None else None
+        with torch.no_grad():
+            enc = model._add_speaker_embedding(model.encoder(model.embedding(x)), sid)
+            extra = {}
+            if sm is not None:
+                g = model.gst(torch.from_numpy(sm))
+                enc = enc + g.expand(-1, L, -1)
+                extra = dict(style_mel=sm[0], gst=g[0, 0].numpy())
+            if gst:
+                mel, lin, align, stop = model.inference(x, speaker_ids=sid, style_mel=(
+                    torch.from_numpy(sm) if sm is not None else None))
+            else:
+                mel, lin, align, stop = model.inference(x, speaker_ids=sid)
+        flags = dict(model=C.model, r=C.r, memory_size=C.memory_size, attn_norm=C.attention_norm,
+                     forward_attn=C.use_forward_attn, trans_agent=C.transition_agent,
+                     forward_attn_mask=C.forward_attn_mask, location_attn=C.location_attn, attn_win=C.windowing,
+                     max_decoder_steps=cap, num_speakers=nspk)
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), ids=ids, enc=enc[0].numpy(), mel=mel[0].numpy(),
+            linear=lin[0].numpy(), align=align[0].numpy(), stop=stop[0].numpy(),
+            speaker_id=np.array(-1 if spk is None else spk), flags=np.array(repr(flags)), **extra)
+        print(f"{name}: L={L} steps={align.shape[1]} frames={mel.shape[1]} flags={flags}")
+
+
 def make_gl_fixtures():
     _stub_text_deps()
     _stub_audio_deps()
@@ -167,8 +230,10 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "gl"]
+    which = sys.argv[1:] or ["model", "taco", "gl"]
     if "model" in which:
         make_model_fixtures()
+    if "taco" in which:
+        make_taco_fixtures()
     if "gl" in which:
         make_gl_fixtures()

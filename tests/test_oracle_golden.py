@@ -91,3 +91,46 @@ def test_librosa_restatement_properties(audio_cfg):
     assert D.dtype == np.complex64 and D.shape == (1025, 41)
     y2 = istft(D, 275, 1102)
     assert y2.shape == y.shape and rel_rms(y2, y) < 1e-5
+
+
+TACO_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gst_*.npz")) +
+                    glob.glob(os.path.join(GOLDEN, "taco_*.npz")))
+
+
+def taco_oracle(z, dtype=np.float64):
+    from oracle.tacotron_oracle import TacotronOracle
+    fl = golden_flags(z)
+    sd = weights_mod().tacotron_gst_weights(0, num_speakers=fl["num_speakers"], r=fl["r"],
+                                            memory_size=fl["memory_size"], location_attn=fl["location_attn"],
+                                            trans_agent=fl["trans_agent"], gst=fl["model"] == "TacotronGST")
+    return TacotronOracle(sd, dtype=dtype, **fl)
+
+
+@pytest.mark.parametrize("case", TACO_CASES)
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_tacotron_gst_oracle_matches_reference(case, dtype):
+    """Tacotron / TacotronGST restatement vs the reference (models/tacotron*.py) on its own fixtures."""
+    z = golden(case)
+    o = taco_oracle(z, dtype)
+    sid = int(z["speaker_id"])
+    enc = o.encoder(z["ids"], None if sid < 0 else sid, z["style_mel"] if "style_mel" in z else None)
+    assert rel_rms(enc, z["enc"]) < 1e-5
+    if "gst" in z:
+        assert rel_rms(o.gst(z["style_mel"]), z["gst"]) < 1e-5
+    mel, stop, align = o.decoder(z["enc"])
+    assert mel.shape == z["mel"].shape, "frame count differs from the reference"
+    np.testing.assert_array_equal(align.argmax(1), z["align"].argmax(1))
+    assert rel_rms(mel, z["mel"]) < 1e-5
+    assert np.abs(align - z["align"]).max() < 1e-5
+    assert np.abs(stop - z["stop"]).max() < 1e-5
+    assert rel_rms(o.postnet(z["mel"]), z["linear"]) < 1e-5
+
+
+def test_tacotron_stop_rule_variants():
+    """The fixtures cover each exit of layers/tacotron.py:464-469: stop token (L=2, one step),
+    alignment tail (L=4/10) and the max_decoder_steps cap (+1 step)."""
+    assert golden("gst_L2_nostyle")["align"].shape[0] == 1
+    z = golden("gst_L4_style")
+    assert z["align"][-1, -1] > 0.6 and z["align"].shape[0] < 41
+    z = golden("gst_L24_style_spk")
+    assert z["align"].shape[0] == golden_flags(z)["max_decoder_steps"] + 1

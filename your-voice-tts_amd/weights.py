@@ -123,6 +123,125 @@ def tacotron2_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 1,
     return s
 
 
+def _default_linear(fan_in):
+    """nn.Linear / nn.Conv default init (kaiming_uniform a=sqrt(5)): U(+-1/sqrt(fan_in))."""
+    return ("uniform", 1.0 / math.sqrt(fan_in))
+
+
+def tacotron_gst_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 5, memory_size: int = 5,
+                      location_attn: bool = False, trans_agent: bool = False, gst: bool = True):
+    """Ordered (key, shape, init) table of the reference ``TacotronGST`` (models/tacotrongst.py:10-45;
+    ``gst=False`` gives the plain ``Tacotron`` of models/tacotron.py:9-43): Tacotron ``Encoder`` /
+    ``CBHG`` / ``Decoder`` / ``PostCBHG`` (layers/tacotron.py:7-489) and ``GST``
+    (layers/gst_layers.py:6-168).  BatchNormConv1d convs have no bias (layers/tacotron.py:36-42)."""
+    s = []
+    add = lambda k, shape, init: s.append((k, tuple(shape), init))
+    add("embedding.weight", (num_chars, 256), ("uniform", 0.3 * math.sqrt(3.0)))  # normal(0, 0.3)
+    if num_speakers > 1:
+        add("speaker_embedding.weight", (num_speakers, 256), ("uniform", 0.3 * math.sqrt(3.0)))
+
+    def bn(prefix, c):
+        add(prefix + ".weight", (c,), ("range", (0.8, 1.2)))
+        add(prefix + ".bias", (c,), ("uniform", 0.1))
+        add(prefix + ".running_mean", (c,), ("uniform", 0.1))
+        add(prefix + ".running_var", (c,), ("range", (0.5, 1.5)))
+        add(prefix + ".num_batches_tracked", (), ("zero_i64", None))
+
+    def bn_conv(prefix, cin, cout, k):
+        add(prefix + ".conv1d.weight", (cout, cin, k), _default_linear(cin * k))
+        bn(prefix + ".bn", cout)
+
+    def gru(prefix, nin, h, bidir):
+        b = 1.0 / math.sqrt(h)
+        for sfx in ("", "_reverse") if bidir else ("",):
+            add(f"{prefix}.weight_ih_l0{sfx}", (3 * h, nin), ("uniform", b))
+            add(f"{prefix}.weight_hh_l0{sfx}", (3 * h, h), ("uniform", b))
+            add(f"{prefix}.bias_ih_l0{sfx}", (3 * h,), ("uniform", b))
+            add(f"{prefix}.bias_hh_l0{sfx}", (3 * h,), ("uniform", b))
+
+    def cbhg(prefix, cin, K, projections):
+        for k in range(1, K + 1):
+            bn_conv(f"{prefix}.conv1d_banks.{k - 1}", cin, 128, k)
+        ins = [K * 128] + projections[:-1]
+        for i, (a, b) in enumerate(zip(ins, projections)):
+            bn_conv(f"{prefix}.conv1d_projections.{i}", a, b, 3)
+        if projections[-1] != 128:
+            add(f"{prefix}.pre_highway.weight", (128, projections[-1]), _default_linear(projections[-1]))
+        for i in range(4):
+            for n in ("H", "T"):
+                add(f"{prefix}.highways.{i}.{n}.weight", (128, 128), _default_linear(128))
+                add(f"{prefix}.highways.{i}.{n}.bias", (128,), _default_linear(128))
+        gru(f"{prefix}.gru", 128, 128, True)
+
+    def prenet(prefix, nin, outs):
+        for i, (a, b) in enumerate(zip([nin] + outs[:-1], outs)):
+            add(f"{prefix}.layers.{i}.linear_layer.weight", (b, a), _lin(a, b))
+            add(f"{prefix}.layers.{i}.linear_layer.bias", (b,), _default_linear(a))
+
+    prenet("encoder.prenet", 256, [256, 128])
+    cbhg("encoder.cbhg.cbhg", 128, 16, [128, 128])
+    if gst:
+        filters = [1, 32, 32, 64, 64, 128, 128]
+        for i in range(6):
+            add(f"gst.encoder.convs.{i}.weight", (filters[i + 1], filters[i], 3, 3), _default_linear(filters[i] * 9))
+            add(f"gst.encoder.convs.{i}.bias", (filters[i + 1],), _default_linear(filters[i] * 9))
+        for i in range(6):
+            bn(f"gst.encoder.bns.{i}", filters[i + 1])
+        gru("gst.encoder.recurrence", 256, 128, False)
+        add("gst.style_token_layer.style_tokens", (10, 64), ("uniform", math.sqrt(3.0) / 8.0))  # orthogonal rows
+        add("gst.style_token_layer.attention.W_query.weight", (256, 128), _default_linear(128))
+        add("gst.style_token_layer.attention.W_key.weight", (256, 64), _default_linear(64))
+        add("gst.style_token_layer.attention.W_value.weight", (256, 64), _default_linear(64))
+    mem = 80 * memory_size
+    prenet("decoder.prenet", mem, [256, 128])
+    hb = 1.0 / math.sqrt(256)
+    add("decoder.attention_rnn.weight_ih", (768, 384), ("uniform", hb))
+    add("decoder.attention_rnn.weight_hh", (768, 256), ("uniform", hb))
+    add("decoder.attention_rnn.bias_ih", (768,), ("uniform", hb))
+    add("decoder.attention_rnn.bias_hh", (768,), ("uniform", hb))
+    add("decoder.attention_layer.query_layer.linear_layer.weight", (ATT_DIM, 256), _lin(256, ATT_DIM, TANH_GAIN))
+    add("decoder.attention_layer.inputs_layer.linear_layer.weight", (ATT_DIM, 256), _lin(256, ATT_DIM, TANH_GAIN))
+    add("decoder.attention_layer.v.linear_layer.weight", (1, ATT_DIM), _lin(ATT_DIM, 1))
+    add("decoder.attention_layer.v.linear_layer.bias", (1,), ("uniform", 1.0 / math.sqrt(ATT_DIM)))
+    if trans_agent:
+        tb = 1.0 / math.sqrt(512)
+        add("decoder.attention_layer.ta.weight", (1, 512), ("uniform", tb))
+        add("decoder.attention_layer.ta.bias", (1,), ("uniform", tb))
+    if location_attn:
+        add("decoder.attention_layer.location_layer.location_conv.weight",
+            (LOC_FILTERS, 2, LOC_KERNEL), ("uniform", 1.0 / math.sqrt(2 * LOC_KERNEL)))
+        add("decoder.attention_layer.location_layer.location_dense.linear_layer.weight",
+            (ATT_DIM, LOC_FILTERS), _lin(LOC_FILTERS, ATT_DIM, TANH_GAIN))
+    add("decoder.project_to_decoder_in.weight", (256, 512), _default_linear(512))
+    add("decoder.project_to_decoder_in.bias", (256,), _default_linear(512))
+    for i in range(2):
+        add(f"decoder.decoder_rnns.{i}.weight_ih", (768, 256), ("uniform", hb))
+        add(f"decoder.decoder_rnns.{i}.weight_hh", (768, 256), ("uniform", hb))
+        add(f"decoder.decoder_rnns.{i}.bias_ih", (768,), ("uniform", hb))
+        add(f"decoder.decoder_rnns.{i}.bias_hh", (768,), ("uniform", hb))
+    add("decoder.proj_to_mel.weight", (80 * r, 256), _default_linear(256))
+    add("decoder.proj_to_mel.bias", (80 * r,), _default_linear(256))
+    add("decoder.attention_rnn_init.weight", (1, 256), ("uniform", math.sqrt(3.0)))
+    add("decoder.memory_init.weight", (1, mem), ("uniform", math.sqrt(3.0)))
+    add("decoder.decoder_rnn_inits.weight", (2, 256), ("uniform", math.sqrt(3.0)))
+    add("decoder.stopnet.linear.weight", (1, 256 + 80 * r), _lin(256 + 80 * r, 1))
+    add("decoder.stopnet.linear.bias", (1,), _default_linear(256 + 80 * r))
+    cbhg("postnet.cbhg", 80, 8, [256, 80])
+    add("last_linear.0.weight", (1025, 256), _default_linear(256))
+    add("last_linear.0.bias", (1025,), _default_linear(256))
+    return s
+
+
+def tacotron_gst_weights(seed: int = 0, **spec_kw):
+    return generate(tacotron_gst_spec(**spec_kw), seed)
+
+
+def synthetic_style_mel(frames: int, seed: int) -> np.ndarray:
+    """Seeded style mel [frames, 80] ~ U[0, 1)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return rng.uniform(0.0, 1.0, size=(frames, N_MEL)).astype(np.float32)
+
+
 def generate(spec, seed: int = 0) -> "OrderedDict[str, np.ndarray]":
     """Deterministic weights for ``spec``: one PCG64 stream per key, seeded seed ^ crc32(key)."""
     out = OrderedDict()
