@@ -37,6 +37,7 @@ typedef struct tts_encoder tts_encoder;
 typedef struct tts_decoder tts_decoder;
 typedef struct tts_postnet tts_postnet;
 typedef struct tts_gl tts_gl;
+typedef struct tts_tacotron tts_tacotron;
 
 /* One weight tensor in the reference's own state_dict layout (fp32, contiguous, [dev]). */
 typedef struct tts_tensor {
@@ -157,6 +158,64 @@ tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
  * buffers (not the caller's outputs). */
 #define TTS_GL_KERNELS 2
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels);
+
+/* ---------------------------------------------------------------- Tacotron / TacotronGST
+ * SURVEY config 5 (config_tacotron_gst.json) and config_tacotron.json: the r-frames-per-step
+ * Tacotron family, models/tacotron.py / models/tacotrongst.py. */
+typedef struct tts_tacotron_config {
+    int r;                 /* frames per step                                                  */
+    int memory_size;       /* decoder memory queue (<= 0 means r); only memory_size == r       */
+    int attn_norm;         /* 0 = softmax, 1 = sigmoid                                         */
+    int forward_attn, trans_agent, forward_attn_mask, location_attn, windowing;
+    int gst;               /* 1: TacotronGST (gst.* weights present), 0: Tacotron              */
+    int num_speakers;      /* > 1: speaker_embedding.weight present                            */
+    int max_batch;         /* workspace capacity: sentences per call (<= 64)                   */
+    int max_len;           /* workspace capacity: encoder length (<= 1024, 512 with location)  */
+    int max_steps;         /* workspace capacity: decoder steps (max_decoder_steps)            */
+} tts_tacotron_config;
+
+/* Replaces construction + load_state_dict of TacotronGST / Tacotron (models/tacotrongst.py:10-45,
+ * models/tacotron.py:9-43).  `tensors` hold the model's state_dict entries (fp32 [dev]). */
+tts_status tts_tacotron_create(const tts_tacotron_config* cfg, const tts_tensor* tensors, int n_tensors,
+                               void* stream, tts_tacotron** out);
+void tts_tacotron_destroy(tts_tacotron* t);
+
+/* Replaces the embedding + Encoder (Prenet + CBHG, layers/tacotron.py:209-243) +
+ * _add_speaker_embedding + GST add of TacotronGST.inference (models/tacotrongst.py:65-73):
+ *   ids         [dev]  int32 [B][Lmax]
+ *   lens        [host] int32 [B], 1 <= lens[b] <= Lmax
+ *   speaker_ids [host] int32 [B] or NULL
+ *   style_mel   [dev]  fp32 [B][style_frames][80] or NULL (GST models only)
+ *   out         [dev]  fp32 [B][Lmax][256], every sentence encoded at its own length, rows past
+ *                      lens[b] zero. */
+tts_status tts_tacotron_encode(tts_tacotron* t, const int32_t* ids, const int32_t* lens, int B, int Lmax,
+                               const int32_t* speaker_ids, const float* style_mel, int style_frames, float* out,
+                               void* stream);
+
+/* Replaces Decoder.inference (layers/tacotron.py:439-470) for a padded batch with per-sentence
+ * batch-1 semantics (the reference's stop rule is batch-1, :464-469):
+ *   enc [dev] fp32 [B][Lmax][256]; lens [host] int32 [B] (>= 1)
+ *   mel [dev] fp32 [B][steps_cap*r][80]; stop [dev] fp32 [B][steps_cap] (sigmoid stop token);
+ *   align [dev] fp32 [B][steps_cap][Lmax] or NULL; n_steps [host] int32 [B] out.
+ * steps_cap >= max_steps + 1 (the reference stops once t > max_decoder_steps). */
+tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t* lens, int B, int Lmax,
+                               int max_steps, int steps_cap, float* mel, float* stop, float* align,
+                               int32_t* n_steps, void* stream);
+
+/* Replaces PostCBHG + last_linear + sigmoid (layers/tacotron.py:246-259, models/tacotrongst.py:43-45,
+ * 77-78): mel [dev] fp32 [B][Tmax][80], T [host] int32 [B] -> linear [dev] fp32 [B][Tmax][1025]
+ * (rows past T[b] zero). */
+tts_status tts_tacotron_postnet(tts_tacotron* t, const float* mel, const int32_t* T, int B, int Tmax,
+                                float* linear, void* stream);
+
+tts_status tts_tacotron_last_timing(tts_tacotron* t, float* loop_ms, int* steps_run);
+
+/* Measurement only: mean duration (ms) of each decoder-step kernel over up to `reps` eager steps
+ * of the last decode's batch, HIP events on the library stream, in launch order: prenet2,
+ * attention GRU, query, attention, project_to_decoder_in, decoder GRU 1, decoder GRU 2, mel,
+ * [prenet1 | stopnet]. */
+#define TTS_TACOTRON_STEP_KERNELS 9
+tts_status tts_tacotron_profile(tts_tacotron* t, int reps, float* kernel_ms, int n_kernels);
 
 const char* tts_last_error(void);
 const char* tts_version(void);

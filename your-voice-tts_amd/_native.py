@@ -16,6 +16,8 @@ TTS_GL_FROM_MEL = 0
 TTS_GL_FROM_LINEAR = 1
 DECODER_STEP_KERNELS = ("prenet2", "att_lstm", "query", "attention", "dec_lstm", "mel_fused")
 GL_KERNELS = ("gl_iter", "gl_ola")
+TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "dec_gru1", "dec_gru2", "mel",
+                         "pre1_stop")
 
 # every symbol include/tts_hip.h declares
 EXPORTS = (
@@ -24,6 +26,8 @@ EXPORTS = (
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
+    "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
+    "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_profile",
     "tts_last_error", "tts_version",
 )
 
@@ -36,6 +40,12 @@ class DecoderConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "r", "attn_norm", "forward_attn", "trans_agent", "forward_attn_mask", "location_attn",
         "windowing", "max_batch", "max_len", "max_steps")]
+
+
+class TacotronConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "r", "memory_size", "attn_norm", "forward_attn", "trans_agent", "forward_attn_mask", "location_attn",
+        "windowing", "gst", "num_speakers", "max_batch", "max_len", "max_steps")]
 
 
 class AudioConfig(ctypes.Structure):
@@ -79,11 +89,21 @@ def _declare(lib):
     FP = ctypes.POINTER(ctypes.c_float)
     lib.tts_decoder_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_gl_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
+    lib.tts_tacotron_create.argtypes = [ctypes.POINTER(TacotronConfig), ctypes.POINTER(TensorView), ctypes.c_int, vp,
+                                        ctypes.POINTER(vp)]
+    lib.tts_tacotron_destroy.argtypes = [vp]
+    lib.tts_tacotron_destroy.restype = None
+    lib.tts_tacotron_encode.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, I32P, vp, ctypes.c_int, vp, vp]
+    lib.tts_tacotron_decode.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
+                                        vp, I32P, vp]
+    lib.tts_tacotron_postnet.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.tts_tacotron_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    lib.tts_tacotron_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_last_error.restype = ctypes.c_char_p
     lib.tts_version.restype = ctypes.c_char_p
     for name in EXPORTS:
         fn = getattr(lib, name)
-        if name.endswith(("_create", "_run", "_timing", "_profile")):
+        if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet")):
             fn.restype = ctypes.c_int
 
 

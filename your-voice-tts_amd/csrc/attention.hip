@@ -65,16 +65,17 @@ hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int wid
 // ------------------------------------------------------------------ processed inputs
 // Pt[b][d][j] = sum_k W[d][k] enc[b][j][k]  (inputs_layer, common_layers.py:115-116, tacotron2.py:176)
 // Stored d-major so the per-step energy loop reads it coalesced along j.
+template <int ENC_>
 __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, const float* W, int Lmax, int Lcap,
                                                              float* Pt) {
     const int b = blockIdx.y;
     const int j0 = blockIdx.x * 16;
-    __shared__ __align__(16) float xs[16][ENC];
-    for (int i = threadIdx.x; i < 16 * ENC / 4; i += blockDim.x) {
-        const int r = i / (ENC / 4), c = i % (ENC / 4);
+    __shared__ __align__(16) float xs[16][ENC_];
+    for (int i = threadIdx.x; i < 16 * ENC_ / 4; i += blockDim.x) {
+        const int r = i / (ENC_ / 4), c = i % (ENC_ / 4);
         const int j = j0 + r;
         float4 v = float4{0.f, 0.f, 0.f, 0.f};
-        if (j < Lmax) v = reinterpret_cast<const float4*>(enc + ((int64_t)b * Lcap + j) * ENC)[c];
+        if (j < Lmax) v = reinterpret_cast<const float4*>(enc + ((int64_t)b * Lcap + j) * ENC_)[c];
         reinterpret_cast<float4*>(&xs[r][0])[c] = v;
     }
     __syncthreads();
@@ -83,8 +84,8 @@ __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, c
     float acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-    const float4* w4 = reinterpret_cast<const float4*>(W + (int64_t)d * ENC);
-    for (int k4 = 0; k4 < ENC / 4; ++k4) {
+    const float4* w4 = reinterpret_cast<const float4*>(W + (int64_t)d * ENC_);
+    for (int k4 = 0; k4 < ENC_ / 4; ++k4) {
         const float4 w = w4[k4];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -100,15 +101,23 @@ __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, c
 }
 
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt,
-                                 hipStream_t s) {
-    hipLaunchKernelGGL(project_inputs_kernel, dim3((Lmax + 15) / 16, B), dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
+                                 hipStream_t s, int enc_dim) {
+    const dim3 grid((Lmax + 15) / 16, B);
+    if (enc_dim == 512)
+        hipLaunchKernelGGL(project_inputs_kernel<512>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
+    else if (enc_dim == 256)
+        hipLaunchKernelGGL(project_inputs_kernel<256>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ attention step
 // One workgroup of 1024 threads per sentence; thread j owns encoder position j (L <= 1024).
+// The reduction area `red` holds at least one float per thread (context partials).
+__host__ __device__ static inline int red_stride(int Lcap) { return Lcap > ATT_THREADS / ATT_WAVES ? Lcap : ATT_THREADS / ATT_WAVES; }
 size_t attention_smem_bytes(int Lcap, int location) {
-    size_t f = 2 * ADIM + 3 * (size_t)Lcap + ATT_WAVES * (size_t)Lcap + 4 * ATT_WAVES;
+    size_t f = 2 * ADIM + 3 * (size_t)Lcap + ATT_WAVES * (size_t)red_stride(Lcap) + 4 * ATT_WAVES;
     if (location) f += 2 * ((size_t)Lcap + 32) + (size_t)NLOC * Lcap + ADIM * NLOC;
     return f * sizeof(float);
 }
@@ -147,6 +156,9 @@ __device__ __forceinline__ Red block_reduce(float s, float m, float y, int i, fl
     return r;
 }
 
+// ENC_ = encoder width, HATT_ = attention-RNN width (Tacotron2: 512 / 1024; Tacotron, TacotronGST:
+// 256 / 256, layers/tacotron.py:290-300).
+template <int ENC_, int HATT_>
 __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -177,16 +189,16 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         pv0[dd] = lane < L ? Pt[(int64_t)(d0 + dd) * Lc + lane] : 0.f;
         pv1[dd] = lane + 64 < L ? Pt[(int64_t)(d0 + dd) * Lc + lane + 64] : 0.f;
     }
-    const float* encb = a.enc + row * ENC;
+    const float* encb = a.enc + row * ENC_;
     const int cx = sparse ? (n - 2 + L) % L : 0;
     const int clo = sparse ? (n >= 1 ? n - 1 : L - 1) : 0;
     const int chi = sparse ? min(n + 2, L - 1) : -1;
     float ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f};
-    if (sparse && tid < ENC) {
-        ex = encb[(int64_t)cx * ENC + tid];
+    if (sparse && tid < ENC_) {
+        ex = encb[(int64_t)cx * ENC_ + tid];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (clo + k <= chi) erow[k] = encb[(int64_t)(clo + k) * ENC + tid];
+            if (clo + k <= chi) erow[k] = encb[(int64_t)(clo + k) * ENC_ + tid];
     }
     if (st.y == 0) return;
     const int t = st.x;
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     float* an = aold + Lc;
     float* wts = an + Lc;
     float* red = wts + Lc;
-    float* scr = red + ATT_WAVES * Lc;
+    float* scr = red + ATT_WAVES * red_stride(Lc);
     float* cat = scr + 4 * ATT_WAVES;
     float* locf = cat + 2 * (Lc + 32);
     float* wd = locf + NLOC * Lc;
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         for (int jj = tid; jj < a.Lalign; jj += blockDim.x)
             a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + jj] = jj < L ? wts[jj] : 0.f;
     if (tid == 0) {
-        a.tail[b] = L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0];
+        a.tail[b] = a.tail_rule ? wts[L - 1] : (L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0]);
         if (sparse) {
             // next step's n = argmax(prev_alpha) = 1 + first argmax of alpha[0..L-2], or 0 when
             // those are all zero; only the surviving positions can be nonzero (index order, strict >)
@@ -336,7 +348,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     // ---- context = w . inputs  (bmm, common_layers.py:217 / 253)
     float ctx = 0.f;
     if (sparse) {
-        if (tid < ENC) {
+        if (tid < ENC_) {
             if (cx < clo) ctx += wts[cx] * ex;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -344,30 +356,36 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             if (cx > chi) ctx += wts[cx] * ex;
         }
     } else {
-        const int d = tid & (ENC - 1), half = tid >> 9;
+        // PARTS interleaved position sets per channel, summed in part order
+        constexpr int PARTS = ATT_THREADS / ENC_;
+        const int d = tid % ENC_, part = tid / ENC_;
         float acc = 0.f;
-        int jj = half;
-        for (; jj + 6 < L; jj += 8) {
-            const float e0 = encb[(int64_t)jj * ENC + d];
-            const float e1 = encb[(int64_t)(jj + 2) * ENC + d];
-            const float e2 = encb[(int64_t)(jj + 4) * ENC + d];
-            const float e3 = encb[(int64_t)(jj + 6) * ENC + d];
+        int jj = part;
+        for (; jj + 3 * PARTS < L; jj += 4 * PARTS) {
+            const float e0 = encb[(int64_t)jj * ENC_ + d];
+            const float e1 = encb[(int64_t)(jj + PARTS) * ENC_ + d];
+            const float e2 = encb[(int64_t)(jj + 2 * PARTS) * ENC_ + d];
+            const float e3 = encb[(int64_t)(jj + 3 * PARTS) * ENC_ + d];
             acc += wts[jj] * e0;
-            acc += wts[jj + 2] * e1;
-            acc += wts[jj + 4] * e2;
-            acc += wts[jj + 6] * e3;
+            acc += wts[jj + PARTS] * e1;
+            acc += wts[jj + 2 * PARTS] * e2;
+            acc += wts[jj + 3 * PARTS] * e3;
         }
-        for (; jj < L; jj += 2) acc += wts[jj] * encb[(int64_t)jj * ENC + d];
+        for (; jj < L; jj += PARTS) acc += wts[jj] * encb[(int64_t)jj * ENC_ + d];
         red[tid] = acc;
         __syncthreads();
-        if (tid < ENC) ctx = red[tid] + red[tid + ENC];
+        if (tid < ENC_) {
+            ctx = red[tid];
+#pragma unroll
+            for (int p = 1; p < PARTS; ++p) ctx += red[p * ENC_ + tid];
+        }
     }
-    if (tid < ENC) a.ctx[(int64_t)b * XA + tid] = ctx;
+    if (tid < ENC_) a.ctx[(int64_t)b * a.ctx_ld + tid] = ctx;
     if (a.forward_attn && a.trans_agent) {
         // u = sigmoid(ta([context, query]))  (:220-222)
-        const float* h = a.h_att + (int64_t)b * HATT;
-        float p = tid < ENC ? a.ta_w[tid] * ctx : 0.f;
-        p += a.ta_w[ENC + tid] * h[tid];  // blockDim == HATT
+        const float* h = a.h_att + (int64_t)b * HATT_;
+        float p = tid < ENC_ ? a.ta_w[tid] * ctx : 0.f;
+        if (tid < HATT_) p += a.ta_w[ENC_ + tid] * h[tid];
         const Red r = block_reduce(p, -INFINITY, 0.f, 0, scr);
         if (tid == 0) a.u[b] = sigmoidf_(r.s + a.ta_b[0]);
     }
@@ -487,8 +505,8 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_fm_kernel(const AttnArg
 }
 
 static bool attention_fast(const AttnArgs& a) {
-    return a.forward_attn && a.forward_attn_mask && a.attn_norm == 1 && !a.location_attn && !a.windowing &&
-           !a.trans_agent;
+    return a.enc_dim == ENC && a.forward_attn && a.forward_attn_mask && a.attn_norm == 1 && !a.location_attn &&
+           !a.windowing && !a.trans_agent;
 }
 bool attention_uses_epart(const AttnArgs& a) { return attention_fast(a); }
 
@@ -565,17 +583,25 @@ static size_t attention_fm_smem_bytes(int Lcap) {
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (attention_fast(a)) {
         hipLaunchKernelGGL(attention_fm_kernel, dim3(a.B), dim3(ATT_THREADS), attention_fm_smem_bytes(a.Lcap), s, a);
-    } else {
-        hipLaunchKernelGGL(attention_kernel, dim3(a.B), dim3(ATT_THREADS),
+    } else if (a.enc_dim == ENC) {
+        hipLaunchKernelGGL((attention_kernel<ENC, HATT>), dim3(a.B), dim3(ATT_THREADS),
                            attention_smem_bytes(a.Lcap, a.location_attn), s, a);
+    } else if (a.enc_dim == 256) {
+        hipLaunchKernelGGL((attention_kernel<256, 256>), dim3(a.B), dim3(ATT_THREADS),
+                           attention_smem_bytes(a.Lcap, a.location_attn), s, a);
+    } else {
+        return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 hipError_t attention_prepare(int Lcap, int location) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)attention_smem_bytes(Lcap, location));
+    const int bytes = (int)attention_smem_bytes(Lcap, location);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<ENC, HATT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<256, 256>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_fm_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)attention_fm_smem_bytes(Lcap));

@@ -1,13 +1,19 @@
 // fp32 MFMA implicit-GEMM Conv1d over time-major activations [B][T][C] ("same" padding per
 // sentence length: rows t >= T_b read as zero), with a folded-BatchNorm epilogue.
-// Used by the Postnet (layers/tacotron2.py:30-45), the encoder convolutions (:48-76) and, with
-// KW = 1, the encoder LSTM input projection.
+// Used by the Tacotron2 Postnet (layers/tacotron2.py:30-45), encoder convolutions (:48-76) and,
+// with KW = 1, the encoder LSTM input projection; and by the Tacotron/TacotronGST CBHG stacks
+// (layers/tacotron.py:92-206): the conv bank as ONE conv of K taps (bank member k's weights
+// centred in the K-tap window, zeros elsewhere), the projections (KW = 3, max-pool fused into the
+// input staging), the Highway layers and every Linear (KW = 1).
 #pragma once
 #include "common.h"
 
 namespace tts {
 
-enum ConvAct { CONV_NONE = 0, CONV_RELU = 1, CONV_TANH = 2 };
+// CONV_HIGHWAY: GEMM columns interleave a Highway layer's rows (2c = H_c, 2c+1 = T_c) and the
+// epilogue writes out[t][c] = relu(H) * sigmoid(T) + resid[t][c] * (1 - sigmoid(T))
+// (layers/tacotron.py:86-89) into Cout/2 channels.
+enum ConvAct { CONV_NONE = 0, CONV_RELU = 1, CONV_TANH = 2, CONV_SIGMOID = 3, CONV_HIGHWAY = 4 };
 
 struct ConvArgs {
     const float* in;     // [B][Tmax][Cin] (ignored when ids is set)
@@ -17,9 +23,12 @@ struct ConvArgs {
     const float* W;      // packed [Cin][KW][co_pad]
     const float* scale;  // [Cout] (null = 1)
     const float* shift;  // [Cout] (null = 0)
-    const float* resid;  // [B][Tmax][Cout] or null: out = resid + y
+    const float* resid;  // [B][Tmax][out_ld] or null: out = resid + y (CONV_HIGHWAY: the layer input)
     const int* T;        // [B] valid frames per sentence
     int Tmax, Cin, Cout, co_pad, act;
+    int pool2;           // stage max(in[t], in[t+1]) with in[T_b] = 0: CBHG's ConstantPad1d([0, 1]) +
+                         // MaxPool1d(2, stride 1) (layers/tacotron.py:137-139, 188) fused into the next conv
+    int out_ld;          // row stride of out / resid in floats (0 = Cout)
 };
 
 constexpr int CONV_BN = 64;  // output channels per tile
@@ -27,13 +36,25 @@ inline int conv_co_pad(int Cout) { return (Cout + CONV_BN - 1) / CONV_BN * CONV_
 
 // W [Cout][Cin][KW] (PyTorch Conv1d layout) -> packed [Cin][KW][co_pad]
 hipError_t conv_pack(const float* W, int Cout, int Cin, int KW, float* out, hipStream_t s);
+// CBHG bank member W [Cout][Cin][k] into a KWmax-tap slab at channels [co_off, co_off + Cout):
+// tap j lands on slot j + (KWmax-1)/2 - (k-1)/2, which reproduces the member's own
+// ConstantPad1d([(k-1)/2, k/2]) (layers/tacotron.py:126-134) under the slab's centred window.
+// The caller zeroes the slab first.
+hipError_t conv_pack_bank(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad, float* out,
+                          hipStream_t s);
 // W [Cout][Cin] (Linear layout, rows stacked into Cout) -> packed [Cin][1][co_pad]
 hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,
                                hipStream_t s);
-// scale = gamma / sqrt(var + eps); shift = beta + (bias - mean) * scale
+// same, row n of W to packed column co_offset + n * stride (interleaved Highway H/T rows)
+hipError_t linear_pack_strided(const float* W, int Cout, int Cin, int co_offset, int stride, int co_pad, float* out,
+                               hipStream_t s);
+// dst[i * stride] = src[i], i < n
+hipError_t copy_strided(const float* src, int n, float* dst, int stride, hipStream_t s);
+// scale = gamma / sqrt(var + eps); shift = beta + (bias - mean) * scale (bias may be null)
 hipError_t fold_bn(const float* bias, const float* gamma, const float* beta, const float* mean, const float* var,
-                   int C, float* scale, float* shift, hipStream_t s);
-// KW in {1, 5}.  frames_hint = sum of T_b picks the tile height (small batches: 16 frames).
+                   int C, float eps, float* scale, float* shift, hipStream_t s);
+// KW in {1, 3, 5, 8, 16}; Cin must be a multiple of the K step (16 for KW <= 5, 8 for KW = 8, 4 for
+// KW = 16).  frames_hint = sum of T_b picks the tile height (small batches: 16 frames).
 hipError_t conv_launch(const ConvArgs& a, int KW, int B, int frames_hint, hipStream_t s);
 
 }  // namespace tts

@@ -3,11 +3,13 @@
 //   out[b][t][co] = act( scale[co] * sum_{k<KW} sum_ci in[b][t+k-PAD][ci] * W[co][ci][k] + shift[co] ) (+ resid)
 //
 // GEMM view: M = frames, N = output channels, K = (tap, input channel).  A workgroup owns a
-// BM x 64 output tile; per 16-channel K step it stages the BM+KW-1 input rows and the
-// 16 x KW x 64 weight slab in LDS, then each wave issues v_mfma_f32_16x16x4_f32 on its
-// (BM/WM) x (64/WN) sub-tile.  One accumulator set per tap keeps the fp32 fma chains short
-// (Cin long instead of KW*Cin).  Two tile shapes: BM=64 (2x2 waves of 32x32) for large batches,
-// BM=16 (1x4 waves of 16x16) so that a single sentence still spreads over >= 100 workgroups.
+// BM x 64 output tile; per BK-channel K step it stages the BM+KW-1 input rows and the
+// BK x KW x 64 weight slab in LDS (BK = 16 / 8 / 4 for KW <= 5 / 8 / 16: the slab stays <= 32 KB),
+// then each wave issues v_mfma_f32_16x16x4_f32 on its (BM/WM) x (64/WN) sub-tile.  For KW <= 5
+// one accumulator set per tap keeps the fp32 fma chains short (Cin long instead of KW*Cin); the
+// long CBHG bank slabs (KW 8 / 16) accumulate every tap into one set (register budget).  Two tile
+// shapes: BM=64 (2x2 waves of 32x32) for large batches, BM=16 (1x4 waves of 16x16) so that a single
+// sentence still spreads over >= 100 workgroups.
 #include "conv1d.h"
 
 namespace tts {
@@ -17,7 +19,8 @@ namespace {
 template <int KW, int BM, int WM, int WN>
 __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     constexpr int PAD = (KW - 1) / 2;
-    constexpr int BK = 16;
+    constexpr int BK = KW <= 5 ? 16 : (KW <= 8 ? 8 : 4);
+    constexpr int NACC = KW <= 5 ? KW : 1;  // accumulator sets (per tap for short kernels)
     constexpr int BN = CONV_BN;
     constexpr int TM = BM / WM / 16;
     constexpr int TN = BN / WN / 16;
@@ -44,9 +47,9 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     constexpr int XR = (XN + 255) / 256, WR = (WN4 + 255) / 256;
     __shared__ float xs[2][XROWS][BK + 1];
     __shared__ __align__(16) float ws[2][BK][KW][BN];
-    floatx4 acc[KW][TM][TN];
+    floatx4 acc[NACC][TM][TN];
 #pragma unroll
-    for (int k = 0; k < KW; ++k)
+    for (int k = 0; k < NACC; ++k)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -67,7 +70,14 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
             const bool ok = t >= 0 && t < Tb;                                                                    \
             const int tc = ok ? t : 0;                                                                           \
             const float* src = idsb ? a.table + (int64_t)idsb[tc] * a.Cin : a.in + ((int64_t)b * a.Tmax + tc) * a.Cin; \
-            const float4 v = *reinterpret_cast<const float4*>(src + ci0_ + c4 * 4);                              \
+            float4 v = *reinterpret_cast<const float4*>(src + ci0_ + c4 * 4);                                    \
+            if (a.pool2) { /* max(in[t], in[t+1]), in[T_b] = 0 */                                                \
+                const bool ok1 = ok && t + 1 < Tb;                                                               \
+                const float4 v1 = *reinterpret_cast<const float4*>(                                              \
+                    a.in + ((int64_t)b * a.Tmax + (ok1 ? t + 1 : tc)) * a.Cin + ci0_ + c4 * 4);                   \
+                const float4 p1 = ok1 ? v1 : float4{0.f, 0.f, 0.f, 0.f};                                         \
+                v = float4{fmaxf(v.x, p1.x), fmaxf(v.y, p1.y), fmaxf(v.z, p1.z), fmaxf(v.w, p1.w)};              \
+            }                                                                                                    \
             xr[q] = ok ? v : float4{0.f, 0.f, 0.f, 0.f};                                                         \
         }                                                                                                        \
         _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                          \
@@ -117,7 +127,10 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
+                    for (int j = 0; j < TN; ++j) {
+                        floatx4& c = acc[NACC == 1 ? 0 : k][i][j];
+                        c = mfma16x16x4(av[i], bv[j], c);
+                    }
             }
         }
         CONV_LSTORE(cur ^ 1);  // the other stage: every wave left it at the previous barrier
@@ -126,8 +139,9 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 #undef CONV_GLOAD
 #undef CONV_LSTORE
     // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)
-    float* outb = a.out + (int64_t)b * a.Tmax * a.Cout;
-    const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * a.Cout : nullptr;
+    const int ld = a.out_ld ? a.out_ld : a.Cout;
+    float* outb = a.out + (int64_t)b * a.Tmax * ld;
+    const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * ld : nullptr;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -136,17 +150,30 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int t = t0 + wt + i * 16 + (lane >> 4) * 4 + r;
                 const int co = c0 + wc + j * 16 + (lane & 15);
-                if (t < Tb && co < a.Cout) {
-                    float sum = acc[0][i][j][r];
+                const bool valid = t < Tb && co < a.Cout;
+                const int cc = co < a.Cout ? co : a.Cout - 1;
+                float sum = acc[0][i][j][r];
 #pragma unroll
-                    for (int k = 1; k < KW; ++k) sum += acc[k][i][j][r];
-                    float y = a.scale ? sum * a.scale[co] : sum;
-                    if (a.shift) y += a.shift[co];
-                    if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
-                    else if (a.act == CONV_TANH) y = tanhf(y);
-                    if (resb) y = resb[(int64_t)t * a.Cout + co] + y;
-                    outb[(int64_t)t * a.Cout + co] = y;
+                for (int k = 1; k < NACC; ++k) sum += acc[k][i][j][r];
+                float y = a.scale ? sum * a.scale[cc] : sum;
+                if (a.shift) y += a.shift[cc];
+                if (a.act == CONV_HIGHWAY) {
+                    // lanes l, l^1 hold columns 2c (H) and 2c+1 (T) of the same frame
+                    const float yt = __shfl_xor(y, 1, 64);
+                    if (valid && !(co & 1)) {
+                        const int c = co >> 1;
+                        const float hh = fmaxf(y, 0.f), tg = sigmoidf_(yt);
+                        const float x = resb[(int64_t)t * ld + c];
+                        outb[(int64_t)t * ld + c] = hh * tg + x * (1.f - tg);
+                    }
+                    continue;
                 }
+                if (!valid) continue;
+                if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+                else if (a.act == CONV_TANH) y = tanhf(y);
+                else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
+                if (resb) y = resb[(int64_t)t * ld + co] + y;
+                outb[(int64_t)t * ld + co] = y;
             }
 }
 
@@ -160,20 +187,37 @@ __global__ void conv_pack_kernel(const float* W, int Cout, int Cin, int KW, int 
     out[i] = co < Cout ? W[((int64_t)co * Cin + ci) * KW + k] : 0.f;
 }
 
-__global__ void linear_pack_kernel(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out) {
+__global__ void conv_pack_bank_kernel(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad,
+                                      float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)Cin * k * Cout) return;
+    const int co = i % Cout;
+    const int j = (i / Cout) % k;
+    const int ci = i / ((int64_t)Cout * k);
+    const int slot = j + (KWmax - 1) / 2 - (k - 1) / 2;
+    out[((int64_t)ci * KWmax + slot) * co_pad + co_off + co] = W[((int64_t)co * Cin + ci) * k + j];
+}
+
+__global__ void linear_pack_kernel(const float* W, int Cout, int Cin, int co_offset, int stride, int co_pad,
+                                   float* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)Cin * Cout) return;
     const int n = i % Cout, ci = i / Cout;
-    out[(int64_t)ci * co_pad + co_offset + n] = W[(int64_t)n * Cin + ci];
+    out[(int64_t)ci * co_pad + co_offset + (int64_t)n * stride] = W[(int64_t)n * Cin + ci];
+}
+
+__global__ void copy_strided_kernel(const float* src, int n, float* dst, int stride) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[(int64_t)i * stride] = src[i];
 }
 
 __global__ void fold_bn_kernel(const float* bias, const float* gamma, const float* beta, const float* mean,
-                               const float* var, int C, float* scale, float* shift) {
+                               const float* var, int C, float eps, float* scale, float* shift) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    const float sc = gamma[c] / sqrtf(var[c] + 1e-5f);
+    const float sc = gamma[c] / sqrtf(var[c] + eps);
     scale[c] = sc;
-    shift[c] = beta[c] + (bias[c] - mean[c]) * sc;
+    shift[c] = beta[c] + ((bias ? bias[c] : 0.f) - mean[c]) * sc;
 }
 
 template <int KW>
@@ -198,25 +242,51 @@ hipError_t conv_pack(const float* W, int Cout, int Cin, int KW, float* out, hipS
     return hipGetLastError();
 }
 
-hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,
+hipError_t conv_pack_bank(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad, float* out,
+                          hipStream_t s) {
+    if (k < 1 || k > KWmax) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)Cin * k * Cout;
+    hipLaunchKernelGGL(conv_pack_bank_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, k, KWmax, co_off,
+                       co_pad, out);
+    return hipGetLastError();
+}
+
+hipError_t linear_pack_strided(const float* W, int Cout, int Cin, int co_offset, int stride, int co_pad, float* out,
                                hipStream_t s) {
     const int64_t total = (int64_t)Cin * Cout;
-    hipLaunchKernelGGL(linear_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, co_offset, co_pad,
-                       out);
+    hipLaunchKernelGGL(linear_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, co_offset, stride,
+                       co_pad, out);
+    return hipGetLastError();
+}
+
+hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,
+                               hipStream_t s) {
+    return linear_pack_strided(W, Cout, Cin, co_offset, 1, co_pad, out, s);
+}
+
+hipError_t copy_strided(const float* src, int n, float* dst, int stride, hipStream_t s) {
+    hipLaunchKernelGGL(copy_strided_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, n, dst, stride);
     return hipGetLastError();
 }
 
 hipError_t fold_bn(const float* bias, const float* gamma, const float* beta, const float* mean, const float* var,
-                   int C, float* scale, float* shift, hipStream_t s) {
-    hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias, gamma, beta, mean, var, C, scale,
-                       shift);
+                   int C, float eps, float* scale, float* shift, hipStream_t s) {
+    hipLaunchKernelGGL(fold_bn_kernel, dim3((C + 255) / 256), dim3(256), 0, s, bias, gamma, beta, mean, var, C, eps,
+                       scale, shift);
     return hipGetLastError();
 }
 
 hipError_t conv_launch(const ConvArgs& a, int KW, int B, int frames_hint, hipStream_t s) {
-    if (KW == 5) return launch_kw<5>(a, B, frames_hint, s);
-    if (KW == 1) return launch_kw<1>(a, B, frames_hint, s);
-    return hipErrorInvalidValue;
+    const int bk = KW <= 5 ? 16 : (KW <= 8 ? 8 : 4);
+    if (a.Cin % bk || (a.act == CONV_HIGHWAY && (a.Cout & 1))) return hipErrorInvalidValue;
+    switch (KW) {
+        case 1: return launch_kw<1>(a, B, frames_hint, s);
+        case 3: return launch_kw<3>(a, B, frames_hint, s);
+        case 5: return launch_kw<5>(a, B, frames_hint, s);
+        case 8: return launch_kw<8>(a, B, frames_hint, s);
+        case 16: return launch_kw<16>(a, B, frames_hint, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace tts

@@ -20,19 +20,22 @@ struct AttnArgs {
     int attn_norm, forward_attn, trans_agent, forward_attn_mask, location_attn, windowing;
     int Lcap;  // row stride of per-position arrays
     int B;
+    int enc_dim;    // encoder width: 512 (Tacotron2) or 256 (Tacotron / TacotronGST, query width 256)
+    int ctx_ld;     // row stride of ctx (XA for Tacotron2)
+    int tail_rule;  // 0: tail = w[L-2] + w[L-1] (layers/tacotron2.py:268); 1: w[L-1] (layers/tacotron.py:465)
     // weights (reference layout)
     const float* v;        // [128]
     const float* v_b;      // [1]
-    const float* ta_w;     // [1536] = [ctx(512) | h_att(1024)]
+    const float* ta_w;     // [enc_dim + query width] = [ctx | h_att]
     const float* ta_b;     // [1]
     const float* loc_conv; // [32][2][31]
     const float* loc_dense;// [128][32]
     // inputs
     const float* q;        // [B][128] processed query
     const float* Pt;       // [B][128][Lcap] processed inputs, transposed
-    const float* enc;      // [B][Lcap][512]
+    const float* enc;      // [B][Lcap][enc_dim]
     const int* lens;       // [B]
-    const float* h_att;    // [B][1024] this step's attention-LSTM output
+    const float* h_att;    // [B][query width] this step's attention-RNN output
     const float* epart;    // [B][ADIM/16][Lcap] energy partials from query_energy_kernel (fast path)
     // state
     float* alpha;          // [B][Lcap]
@@ -43,7 +46,7 @@ struct AttnArgs {
     int* nidx;             // [B] argmax of prev_alpha for the next step (forward mask)
     float* tail;           // [B] att_w[L-2] + att_w[L-1]
     // outputs
-    float* ctx;            // [B] rows of stride XA: context written to ctx[b*XA + d]
+    float* ctx;            // [B] rows of stride ctx_ld: context written to ctx[b*ctx_ld + d]
     float* align_hist;     // [B][hist_cap][Lalign] or null
     int64_t align_ldb;     // stride per sentence
     int Lalign;
@@ -91,7 +94,9 @@ bool attention_uses_epart(const AttnArgs& a);
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
 hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s);
-hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s);
+// enc_dim 512 (Tacotron2) or 256 (Tacotron / TacotronGST)
+hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s,
+                                 int enc_dim = ENC);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 size_t attention_smem_bytes(int Lcap, int location);
 hipError_t attention_prepare(int Lcap, int location);  // raise the dynamic-LDS limit once

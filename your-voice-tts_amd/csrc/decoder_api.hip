@@ -154,7 +154,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         const tts_decoder_config& c = d->cfg;
         a.attn_norm = c.attn_norm; a.forward_attn = c.forward_attn; a.trans_agent = c.trans_agent;
         a.forward_attn_mask = c.forward_attn_mask; a.location_attn = c.location_attn; a.windowing = c.windowing;
-        a.Lcap = d->Lcap; a.B = B;
+        a.Lcap = d->Lcap; a.B = B; a.enc_dim = ENC; a.ctx_ld = XA; a.tail_rule = 0;
         a.v = d->v; a.v_b = d->v_b; a.ta_w = d->ta_w; a.ta_b = d->ta_b;
         a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
@@ -379,6 +379,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         probe.attn_norm = cfg->attn_norm; probe.forward_attn = cfg->forward_attn; probe.trans_agent = cfg->trans_agent;
         probe.forward_attn_mask = cfg->forward_attn_mask; probe.location_attn = cfg->location_attn;
         probe.windowing = cfg->windowing;
+        probe.enc_dim = ENC;
         d->fast_attention = attention_uses_epart(probe);
     }
     CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));

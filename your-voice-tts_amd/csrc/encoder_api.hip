@@ -177,7 +177,7 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         CK(emalloc(e, &e->sc[l], EDIM));
         CK(emalloc(e, &e->sh[l], EDIM));
         HK(conv_pack(w, EDIM, EDIM, 5, e->Wc[l], s));
-        HK(fold_bn(bias, g, be, mu, var, EDIM, e->sc[l], e->sh[l], s));
+        HK(fold_bn(bias, g, be, mu, var, EDIM, 1e-5f, e->sc[l], e->sh[l], s));
     }
     CK(emalloc(e, &e->Wp, (size_t)EDIM * 2 * EG));
     CK(emalloc(e, &e->bp, 2 * EG));

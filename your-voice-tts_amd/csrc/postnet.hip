@@ -71,7 +71,7 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
             return TTS_ERR_NOMEM;
         }
         hipError_t e = conv_pack(w, co, ci, 5, p->W[l], s);
-        if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, p->scale[l], p->shift[l], s);
+        if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, 1e-5f, p->scale[l], p->shift[l], s);
         if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     }
     hipError_t e = hipStreamSynchronize(s);

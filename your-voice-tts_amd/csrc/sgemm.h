@@ -21,7 +21,21 @@ struct Seg {
     int len;  // multiple of 16
 };
 
-enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2, EPI_ENC_LSTM = 3 };
+enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2, EPI_ENC_LSTM = 3, EPI_GRU = 4 };
+
+// EPI_GRU: torch GRUCell (gate rows r, z, n; ATen's h' = (h - n) * z + n) for the Tacotron decoder
+// (layers/tacotron.py:289, 304-305, 370-381).  A 16-row tile holds, for 4 hidden units u
+// (ROWMAP_GRU), [W_ir x + W_hr h | W_iz x + W_hz h | W_in x | W_hn h], so that
+// n = tanh(W_in x + b_in + r * (W_hn h + b_hn)) keeps its two halves apart.  Optional residual
+// output dout = h' + res (the decoder GRU stack's residual connection, :380-381).
+struct GruEpi {
+    const float* h;  // previous hidden state [b * ldh + unit]
+    int ldh;
+    const float* res;  // residual input [b * ldr + unit] or null
+    int ldr;
+    float* dout;  // h' + res, or null
+    int ldd;
+};
 
 // EPI_ENC_LSTM: one step s of the bidirectional encoder LSTM (layers/tacotron2.py:56-61, 82):
 // workgroups [0, tiles_per_dir) run the forward direction on seg[0] = h_fwd(s-1) at position s,
@@ -43,15 +57,20 @@ struct EncLstm {
 // uses EPI_MEL_FUSED).
 enum Role {
     ROLE_PRENET = 0, ROLE_ATT_LSTM = 1, ROLE_QUERY = 2, ROLE_DEC_LSTM = 3, ROLE_MEL = 4, ROLE_MEL_FUSED = 5,
-    ROLE_ENC_LSTM = 6
+    ROLE_ENC_LSTM = 6,
+    // Tacotron / TacotronGST decoder step (tacotron_api.hip)
+    ROLE_T_PRENET1 = 7, ROLE_T_PRENET2 = 8, ROLE_T_ATT_GRU = 9, ROLE_T_QUERY = 10, ROLE_T_PROJ = 11,
+    ROLE_T_DEC_GRU = 12, ROLE_T_MEL = 13, ROLE_T_PRE1_STOP = 14
 };
-enum Act { ACT_NONE = 0, ACT_RELU = 1 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2 };
 
 // EPI_MEL_FUSED: one GEMM over x = [h_dec | ctx] whose output rows are
 //   [0, nmel)            mel frame(s)                  -> history
 //   [nmel, nmel+256)     prenet layer-1 pre-activation -> relu -> pre1 (next step's prenet)
 //   nmel+256             stop-token logit              -> sigmoid -> history + stop rule
 // using weights folded at load time: W1' = W1 W_mel, w_stop' = [w_s_h | 0] + w_s_mel W_mel.
+// The Tacotron decoder uses it with nmel = 0 over x = [mel out | decoder out] (its mel has a
+// sigmoid, so nothing folds): rows [0, 256) = [W1 | 0], row 256 = the stopnet, rule = 1.
 struct MelFused {
     int nmel;
     float* pre1;
@@ -66,6 +85,7 @@ struct MelFused {
     int* n_steps;
     int* state_next;  // int2 {t+1, n_active} read by the next step (other parity slot)
     int max_steps;
+    int rule;  // 0: Tacotron2 stop rule (layers/tacotron2.py:267-277); 1: Tacotron (layers/tacotron.py:464-469)
 };
 
 struct SGemmArgs {
@@ -92,13 +112,17 @@ struct SGemmArgs {
     const int* n_active;  // unused (kept adjacent to step)
     MelFused mf;          // EPI_MEL_FUSED only
     EncLstm enc;          // EPI_ENC_LSTM only
+    GruEpi gru;           // EPI_GRU only
 };
 
 // Row maps used when repacking reference matrices.
-enum RowMap { ROWMAP_IDENTITY = 0, ROWMAP_LSTM = 1 };
+enum RowMap { ROWMAP_IDENTITY = 0, ROWMAP_LSTM = 1, ROWMAP_GRU = 2 };
 
 // Repack [A (N x K1) | B (N x K2)] (row-major, fp32, reference layout) into fragment order.
 // ROWMAP_LSTM: logical row ntile*16 + gate*4 + u  <-  reference row gate*H + ntile*4 + u.
+// ROWMAP_GRU (N = 4H, A = W_ih [3H][K1], B = W_hh [3H][K2]): logical gate g of unit
+// ntile*4 + u is [W_ir | W_hr], [W_iz | W_hz], [W_in | 0], [0 | W_hn] for g = 0..3; biases
+// b_ir + b_hr, b_iz + b_hz, b_in, b_hn.
 hipError_t sgemm_pack(const float* A, int K1, const float* Bm, int K2, int N, int rowmap, int H,
                       float* packed, hipStream_t s);
 // Logical-order bias: bias_l[n_l] = a[row(n_l)] (+ b[row(n_l)] if b), rows >= N are zero.

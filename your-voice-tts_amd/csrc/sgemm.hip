@@ -60,6 +60,14 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
         pre_cell = a.cell[(int64_t)b * a.ldc + ntile * 4 + u];
     }
+    float pre_res = 0.f;  // EPI_GRU: residual input of this (sentence, unit)
+    if (EPI == EPI_GRU && tid < a.B * 4) {
+        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
+        pre_cell = a.gru.h[(int64_t)b * a.gru.ldh + ntile * 4 + u];  // h_{t-1}
+        if (a.gru.res) pre_res = a.gru.res[(int64_t)b * a.gru.ldr + ntile * 4 + u];
+    }
     const int dir = EPI == EPI_ENC_LSTM ? ntile / a.enc.tiles_per_dir : 0;
     int enc_pos = -1;  // encoder position this thread's (b, unit) updates, -1 when idle
     if (EPI == EPI_ENC_LSTM && (int)threadIdx.x < a.B * 4) {
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     // Operands loaded in the prologue are consumed only from here on; the empty asm redefines
     // them here so the compiler cannot hoist their first use (and its wait) above the loads.
     asm volatile("" : "+v"(st_x), "+v"(st_y), "+v"(pre_done), "+v"(pre_bias[0]), "+v"(pre_bias[1]),
-                 "+v"(pre_bias[2]), "+v"(pre_bias[3]), "+v"(pre_cell));
+                 "+v"(pre_bias[2]), "+v"(pre_bias[3]), "+v"(pre_cell), "+v"(pre_res));
     if (st_y == 0) {
         // every sentence is done: steps past the end are no-ops, but the fused stop launch
         // still forwards {step+1, 0} so the next parity slot reads "done" as well
@@ -219,6 +227,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             if (n < a.N) {
                 float v = fin[b][col] + pre_bias[0];
                 if (a.act == ACT_RELU) v = fmaxf(v, 0.f);
+                else if (a.act == ACT_SIGMOID) v = sigmoidf_(v);
                 if (out) out[(int64_t)b * a.ldo + n] = v;
                 if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
                 if (track && !pre_done) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
@@ -272,14 +281,22 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                     const float stv = sigmoidf_(fin[b][col] + sr_bias);
                     if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
                     const int L = sr_len;
-                    const int f1 = sr_flag | ((sr_tail > 0.8f && step > L) ? 1 : 0);
-                    m.flag1[b] = f1;
-                    if (f1 && step > 2 * L) {
-                        const int c = sr_count + 1;
-                        m.count[b] = c;
-                        if (c > 20) nd = 1;
-                    } else if (step + 1 == m.max_steps) {
-                        nd = 1;
+                    if (m.rule == 1) {
+                        // Tacotron (layers/tacotron.py:459-469), t = step + 1 after the append:
+                        // t > L/4 and (stop > 0.6 [float32 compare] or alignment[-1].item() > 0.6
+                        // [double compare]); elif t > max_decoder_steps
+                        const int t1 = step + 1;
+                        if ((4 * t1 > L && (stv > 0.6f || (double)sr_tail > 0.6)) || t1 > m.max_steps) nd = 1;
+                    } else {
+                        const int f1 = sr_flag | ((sr_tail > 0.8f && step > L) ? 1 : 0);
+                        m.flag1[b] = f1;
+                        if (f1 && step > 2 * L) {
+                            const int c = sr_count + 1;
+                            m.count[b] = c;
+                            if (c > 20) nd = 1;
+                        } else if (step + 1 == m.max_steps) {
+                            nd = 1;
+                        }
                     }
                     if (nd) {
                         m.done[b] = 1;
@@ -294,6 +311,21 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                 for (int k = 0; k < a.B; ++k) na += sdone[k] ? 0 : 1;
                 *reinterpret_cast<int2*>(m.state_next) = make_int2(step + 1, na);
             }
+        }
+    } else if (EPI == EPI_GRU) {
+        // GRU cell (torch GRUCell, ATen form): r, z gates; n = tanh(W_in x + b_in + r (W_hn h + b_hn));
+        // h' = (h - n) z + n; optional residual dout = h' + res
+        float* out = a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0);
+        const int e = threadIdx.x;
+        if (e < a.B * 4) {
+            const int b = e >> 2, u = e & 3;
+            const int unit = ntile * 4 + u;
+            const float r = sigmoidf_(fin[b][u] + pre_bias[0]);
+            const float z = sigmoidf_(fin[b][4 + u] + pre_bias[1]);
+            const float n = tanhf((fin[b][8 + u] + pre_bias[2]) + r * (fin[b][12 + u] + pre_bias[3]));
+            const float h = (pre_cell - n) * z + n;
+            out[(int64_t)b * a.ldo + unit] = h;
+            if (a.gru.dout) a.gru.dout[(int64_t)b * a.gru.ldd + unit] = h + pre_res;
         }
     } else {
         // LSTM cell (torch LSTMCell, gate order i, f, g, o): c' = s(f)c + s(i)tanh(g); h' = s(o)tanh(c')
@@ -332,7 +364,17 @@ __global__ void sgemm_pack_kernel(const float* A, int K1, const float* Bm, int K
         row = gate * H + (nl >> 4) * 4 + u;
     }
     float v = 0.f;
-    if (nl < N) v = k < K1 ? A[(size_t)row * K1 + k] : Bm[(size_t)row * K2 + (k - K1)];
+    if (rowmap == ROWMAP_GRU) {
+        const int col = nl & 15, gate = col >> 2, unit = (nl >> 4) * 4 + (col & 3);
+        if (nl < N) {
+            if (k < K1)
+                v = gate < 3 ? A[(size_t)(gate * H + unit) * K1 + k] : 0.f;
+            else if (gate != 2)
+                v = Bm[(size_t)((gate == 3 ? 2 : gate) * H + unit) * K2 + (k - K1)];
+        }
+    } else if (nl < N) {
+        v = k < K1 ? A[(size_t)row * K1 + k] : Bm[(size_t)row * K2 + (k - K1)];
+    }
     packed[i] = v;
 }
 
@@ -345,7 +387,16 @@ __global__ void sgemm_bias_kernel(const float* a, const float* b, int N, int Npa
         row = gate * H + (nl >> 4) * 4 + u;
     }
     float v = 0.f;
-    if (nl < N) v = a[row] + (b ? b[row] : 0.f);
+    if (rowmap == ROWMAP_GRU) {
+        const int col = nl & 15, gate = col >> 2, unit = (nl >> 4) * 4 + (col & 3);
+        if (nl < N) {
+            if (gate < 2) v = a[gate * H + unit] + b[gate * H + unit];
+            else if (gate == 2) v = a[2 * H + unit];
+            else v = b[2 * H + unit];
+        }
+    } else if (nl < N) {
+        v = a[row] + (b ? b[row] : 0.f);
+    }
     out[nl] = v;
 }
 
@@ -389,6 +440,14 @@ hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s) {
         case ROLE_MEL: return launch_role<EPI_LINEAR, ROLE_MEL>(a, s);
         case ROLE_MEL_FUSED: return launch_role<EPI_MEL_FUSED, ROLE_MEL_FUSED>(a, s);
         case ROLE_ENC_LSTM: return launch_role<EPI_ENC_LSTM, ROLE_ENC_LSTM>(a, s);
+        case ROLE_T_PRENET1: return launch_role<EPI_LINEAR, ROLE_T_PRENET1>(a, s);
+        case ROLE_T_PRENET2: return launch_role<EPI_LINEAR, ROLE_T_PRENET2>(a, s);
+        case ROLE_T_ATT_GRU: return launch_role<EPI_GRU, ROLE_T_ATT_GRU>(a, s);
+        case ROLE_T_QUERY: return launch_role<EPI_LINEAR, ROLE_T_QUERY>(a, s);
+        case ROLE_T_PROJ: return launch_role<EPI_LINEAR, ROLE_T_PROJ>(a, s);
+        case ROLE_T_DEC_GRU: return launch_role<EPI_GRU, ROLE_T_DEC_GRU>(a, s);
+        case ROLE_T_MEL: return launch_role<EPI_LINEAR, ROLE_T_MEL>(a, s);
+        case ROLE_T_PRE1_STOP: return launch_role<EPI_MEL_FUSED, ROLE_T_PRE1_STOP>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -50,5 +50,12 @@ def setup_model(num_chars, num_speakers_or_c, c=None, **kw):
                          forward_attn=c.use_forward_attn, trans_agent=c.transition_agent,
                          forward_attn_mask=c.forward_attn_mask, location_attn=c.location_attn,
                          separate_stopnet=c.separate_stopnet, **kw)
-    raise NotImplementedError(f"model {c.model!r}: only Tacotron2 is on the MI355X path in this build "
-                              f"(TacotronGST is SURVEY config 5, not yet built)")
+    if model in ("tacotron", "tacotrongst"):  # utils/generic_utils.py:258-274
+        from .tacotron import Tacotron, TacotronGST
+        cls = TacotronGST if model == "tacotrongst" else Tacotron
+        return cls(num_chars=num_chars, num_speakers=num_speakers, r=c.r, linear_dim=1025, mel_dim=80,
+                   memory_size=c.memory_size, attn_win=c.windowing, attn_norm=c.attention_norm,
+                   prenet_type=c.prenet_type, prenet_dropout=c.prenet_dropout, forward_attn=c.use_forward_attn,
+                   trans_agent=c.transition_agent, forward_attn_mask=c.forward_attn_mask,
+                   location_attn=c.location_attn, separate_stopnet=c.separate_stopnet, **kw)
+    raise NotImplementedError(f"model {c.model!r} is not one of Tacotron2, Tacotron, TacotronGST")

@@ -9,12 +9,14 @@ dependencies are not installed here: callers pass character/phoneme ids, or give
 from __future__ import annotations
 
 import io
+import os
 import re
 import time
 
 import numpy as np
 import torch
 
+from . import _native
 from .audio import AudioProcessor
 
 # ------------------------------------------------------------------ sentence splitting
@@ -62,23 +64,25 @@ def wav_to_int16(wav):
 # ------------------------------------------------------------------ batched pipeline
 @torch.no_grad()
 def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed=0, phase="device",
-                     iters=None, keep_outputs=False):
+                     iters=None, keep_outputs=False, style_mel=None):
     """ids -> encoder -> HIP decoder -> HIP postnet -> HIP Griffin-Lim for a ragged batch.
 
     phase: "device" draws the initial GL phases on the GPU from ``seed``; "numpy" draws them
     sentence by sentence with np.random.rand(1025, T_b) in batch order, as the reference does
     when it synthesises the sentences one after another.  Returns (wavs: list of float64 numpy
     arrays, info dict)."""
-    out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
+    linear = hasattr(model, "linear_dim")  # Tacotron / TacotronGST: linear-spectrogram GL
+    out = model.inference_batch(ids_list, speaker_ids=speaker_ids, **({"style_mel": style_mel} if linear else {}))
     frames = out["frames"]
-    mel_post = out["mel_post"]
+    mel_post = out["linear"] if linear else out["mel_post"]
     phase_u = None
     if phase == "numpy":
         Fmax = mel_post.shape[1]
         phase_u = np.zeros((len(frames), ap.n_fft // 2 + 1, Fmax))
         for b, T in enumerate(frames):
             phase_u[b, :, :T] = np.random.rand(ap.n_fft // 2 + 1, T)
-    wav = ap.griffin_lim_batch(mel_post, frames, phase_u=phase_u, seed=seed, iters=iters)
+    mode = _native.TTS_GL_FROM_LINEAR if linear else _native.TTS_GL_FROM_MEL
+    wav = ap.griffin_lim_batch(mel_post, frames, mode=mode, phase_u=phase_u, seed=seed, iters=iters)
     lens = [ap.hop_length * (T - 1) for T in frames]
     info = dict(frames=frames, steps=out["steps"], samples=lens, **model.last_timing, **ap.last_gl_timing())
     if keep_outputs:
@@ -97,17 +101,34 @@ def _ids_tensor(text, CONFIG):
     return torch.as_tensor(np.asarray(text), dtype=torch.long).view(1, -1)
 
 
+def compute_style_mel(style_wav, ap, use_cuda=True):
+    """utils/synthesis.py:28-35: [1, frames, 80] style mel.  ``style_wav`` may be a wav path (read
+    as float64 like soundfile, analysed by ``ap.melspectrogram``) or an already computed mel
+    ([frames, 80] or [1, frames, 80])."""
+    if isinstance(style_wav, (str, bytes, os.PathLike)):
+        style = ap.melspectrogram(ap.load_wav(style_wav)).T  # [frames, 80]
+    else:
+        style = style_wav.cpu().numpy() if torch.is_tensor(style_wav) else np.asarray(style_wav)
+    style = torch.as_tensor(np.asarray(style, dtype=np.float32))
+    if style.dim() == 2:
+        style = style[None]
+    return style.cuda() if use_cuda else style
+
+
 def synthesis(model, text, CONFIG, use_cuda, ap, speaker_id=None, style_wav=None, truncated=False,
               enable_eos_bos_chars=False, trim_silence=False):
-    """utils/synthesis.py:78-124 (Tacotron2 path): returns
-    (wav, alignment [T,L], decoder_output [T,80], postnet_output [T,80], stop_tokens [1,T,1])."""
+    """utils/synthesis.py:78-124: returns (wav, alignment [T,L], decoder_output [T*r,80],
+    postnet_output [T*r,80] (Tacotron2) or [T*r,1025] (Tacotron / TacotronGST), stop_tokens)."""
     if truncated:
         return model.inference_truncated(_ids_tensor(text, CONFIG))
-    if style_wav is not None and CONFIG.model == "TacotronGST":
-        raise NotImplementedError("TacotronGST (SURVEY config 5) is not yet on the MI355X path")
     inputs = _ids_tensor(text, CONFIG)
     sid = None if speaker_id is None or speaker_id is False else torch.as_tensor([speaker_id])
-    decoder_output, postnet_output, alignments, stop_tokens = model.inference(inputs, speaker_ids=sid)
+    if CONFIG.model == "TacotronGST" and style_wav is not None:  # run_model (utils/synthesis.py:38-49)
+        style_mel = compute_style_mel(style_wav, ap, use_cuda)
+        decoder_output, postnet_output, alignments, stop_tokens = model.inference(
+            inputs, style_mel=style_mel, speaker_ids=sid)
+    else:
+        decoder_output, postnet_output, alignments, stop_tokens = model.inference(inputs, speaker_ids=sid)
     postnet_output = postnet_output[0].cpu().numpy()  # parse_outputs (utils/synthesis.py:52-56)
     decoder_output = decoder_output[0].cpu().numpy()
     alignment = alignments[0].cpu().numpy()
