@@ -11,7 +11,9 @@ every rank synthesises --batch sentences per step.
 
 Default workload = BASELINE.json configs[1]: one LJSpeech-length sentence (L=100 ids, seed 1,
 -> 222 frames), config_tacotron2.json + forward_attn_mask (synthesize.py:86), random-init weights
-from the deterministic generator (seed 0), GL 60 iterations.
+from the deterministic generator (seed 0), GL 60 iterations.  ``--model gst`` measures configs[4]
+instead: TacotronGST (config_tacotron_gst.json, 4 speakers, speaker b mod 4), B=32 sentences per
+GPU with L ~ U{60..160} (seed 4), style mel [B, 200, 80] ~ U[0,1) (seed 4), linear-spectrogram GL.
 
 Prints ONE JSON line on rank 0 (keys per the driver contract, plus roofline / cpu_baseline).
 """
@@ -63,7 +65,34 @@ def kernel_algorithmic(name, B, L, frames_total, r=1):
     return ("hbm", by[name])
 
 
+def kernel_algorithmic_gst(name, B, L, frames_total, r=5):
+    """Algorithmic bytes per launch of the TacotronGST decoder-step kernels (weights once per batch
+    step + per-sentence activations) and of the GL iteration."""
+    nm = 80 * r
+    by = {
+        "prenet2": 4 * (128 * 256 + B * (256 + 128)),
+        "att_gru": 4 * (3 * 256 * 640 + B * (640 + 2 * 256)),
+        "query": 4 * (128 * 256 + B * (256 + 128)),
+        "attention": 4 * B * (L * (128 + 256 + 3) + 128 + 256),
+        "proj": 4 * (256 * 512 + B * (512 + 256)),
+        "dec_gru1": 4 * (3 * 256 * 512 + B * (512 + 3 * 256)),
+        "dec_gru2": 4 * (3 * 256 * 512 + B * (512 + 3 * 256)),
+        "mel": 4 * (nm * 256 + B * (256 + 2 * nm)),
+        "pre1_stop": 4 * ((256 + 1) * (nm + 256) + B * (nm + 256 + 257)),
+        "gl_iter": GL_BYTES_PER_FRAME_ITER * frames_total,
+    }
+    return ("hbm", by[name])
+
+
 def build(args, device):
+    if args.model == "gst":
+        cfg = gu.default_config("config_tacotron_gst.json")
+        model = gu.setup_model(130, 4, cfg, max_batch=max(args.batch, 1), max_len=256)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in weights.tacotron_gst_weights(0, num_speakers=4).items()})
+        model.cuda().eval()
+        audio = dict(cfg.audio)
+        audio["griffin_lim_iters"] = args.iters
+        return cfg, model, audiomod.AudioProcessor(**audio)
     cfg = gu.default_config("config_tacotron2.json")
     cfg.forward_attn_mask = True  # synthesize.py:86
     model = gu.setup_model(130, cfg, max_batch=max(args.batch, 1), max_len=max(args.L, 256))
@@ -78,6 +107,12 @@ def build(args, device):
 def make_job(args, world, rank, max_steps):
     """The whole job's sentences (world x batch) and this rank's LPT share (sharding.py)."""
     n = world * args.batch
+    if args.model == "gst":
+        # configs[4]: L ~ U{60..160} (seed 4); every sentence costs up to the 500-step cap
+        lens = weights.synthetic_lengths(n, 4)
+        ids = [weights.synthetic_ids(int(L), 200 + b) for b, L in enumerate(lens)]
+        mine = sharding.lpt_partition([len(x) for x in ids], world, capacity=args.batch)[rank]
+        return ids, mine
     if args.lengths == "fixed":
         ids = [weights.synthetic_ids(args.L, 1) for _ in range(n)]  # configs[1]: L=100, seed 1
     else:
@@ -89,10 +124,28 @@ def make_job(args, world, rank, max_steps):
     return ids, mine
 
 
+_STYLE = {}
+
+
+def gst_inputs(n, device):
+    """configs[4] style mels [n, 200, 80] ~ U[0,1) (seed 4) in HBM and speakers b mod 4."""
+    if n not in _STYLE:
+        rng = np.random.Generator(np.random.PCG64(4))
+        _STYLE[n] = torch.from_numpy(rng.uniform(0, 1, size=(n, 200, 80)).astype(np.float32)).to(device)
+    return _STYLE[n], [b % 4 for b in range(n)]
+
+
 @torch.no_grad()
 def run_step(model, ap, ids, mine, world, seed):
-    out = model.inference_batch([ids[i] for i in mine])
-    wav = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=seed)
+    if hasattr(model, "linear_dim"):  # TacotronGST: linear spectrogram -> inv_spectrogram GL
+        style, spk = gst_inputs(len(ids), model.device)
+        sel = torch.as_tensor(mine, dtype=torch.long, device=model.device)
+        out = model.inference_batch([ids[i] for i in mine], speaker_ids=[spk[i] for i in mine],
+                                    style_mel=style.index_select(0, sel))
+        wav = ap.griffin_lim_batch(out["linear"], out["frames"], mode=audiomod._native.TTS_GL_FROM_LINEAR, seed=seed)
+    else:
+        out = model.inference_batch([ids[i] for i in mine])
+        wav = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=seed)
     if world > 1:
         # finished waveforms only, gather-v to rank 0 over RCCL (point-to-point, one link per peer)
         rows = [wav[k, :ap.hop_length * (T - 1)] for k, T in enumerate(out["frames"])]
@@ -100,15 +153,47 @@ def run_step(model, ap, ids, mine, world, seed):
     return out["frames"], wav
 
 
+def _threads():
+    try:
+        from threadpoolctl import threadpool_info
+        return max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:
+        return 1
+
+
+def cpu_baseline_gst(args):
+    """Oracle TacotronGST (fp32) + linear GL (fp64) on the host for ONE config-5 sentence (sentence 0:
+    its L, speaker 0, style mel 0), full 500-step cap and 60 GL iterations."""
+    from oracle.griffin_lim_oracle import AudioOracle
+    from oracle.tacotron_oracle import TacotronOracle
+    cfg = gu.default_config("config_tacotron_gst.json")
+    o = TacotronOracle(weights.tacotron_gst_weights(0, num_speakers=4), dtype=np.float32, r=cfg.r,
+                       memory_size=cfg.memory_size, attn_norm=cfg.attention_norm, forward_attn=cfg.use_forward_attn,
+                       trans_agent=cfg.transition_agent, forward_attn_mask=cfg.forward_attn_mask,
+                       location_attn=cfg.location_attn, attn_win=cfg.windowing, max_decoder_steps=500)
+    ap = AudioOracle(**{**cfg.audio, "griffin_lim_iters": args.iters})
+    L = int(weights.synthetic_lengths(1, 4)[0])
+    ids = weights.synthetic_ids(L, 200)
+    style = np.random.Generator(np.random.PCG64(4)).uniform(0, 1, size=(1, 200, 80)).astype(np.float32)[0]
+    t0 = time.time()
+    res = o.inference(ids, 0, style)
+    np.random.seed(0)
+    ap.inv_spectrogram(res["linear"].T)
+    dt = time.time() - t0
+    T = res["mel"].shape[0]
+    return dict(value=T / dt, unit="mel-frames/s", cores=int(_threads()), kind="port",
+                sample=f"1 config-5 sentence (L={L}, {T} frames): numpy oracle TacotronGST (fp32) + linear GL "
+                       f"{args.iters} iters (fp64, scipy.fftpack) on the host, {dt:.1f} s",
+                rtf=dt / (275 * (T - 1) / 22050.0))
+
+
 def cpu_baseline(args, seconds_target=12.0):
     """Oracle (numpy restatement of the reference path) on the host: decoder + postnet + GL."""
     from oracle.griffin_lim_oracle import AudioOracle
     from oracle.tacotron2_oracle import Tacotron2Oracle
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:
-        threads = 1
+    if args.model == "gst":
+        return cpu_baseline_gst(args)
+    threads = _threads()
     cfg = gu.default_config("config_tacotron2.json")
     o = Tacotron2Oracle(weights.tacotron2_weights(0), dtype=np.float32, attn_norm=cfg.attention_norm,
                         forward_attn=cfg.use_forward_attn, trans_agent=cfg.transition_agent,
@@ -156,6 +241,7 @@ def main():
     ap_.add_argument("--iters", type=int, default=60)
     ap_.add_argument("--no-cpu-baseline", action="store_true")
     ap_.add_argument("--no-profile", action="store_true")
+    ap_.add_argument("--model", choices=["tacotron2", "gst"], default="tacotron2")
     args = ap_.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -207,12 +293,21 @@ def main():
         return
 
     # ---- per-stage wall times (rank 0, one extra untimed step) and per-kernel profile
+    gst = args.model == "gst"
     torch.cuda.synchronize()
     s0 = time.perf_counter()
-    out = model.inference_batch(ids)
+    if gst:
+        style, spk = gst_inputs(len(all_ids), device)
+        sel = torch.as_tensor(mine, dtype=torch.long, device=device)
+        out = model.inference_batch(ids, speaker_ids=[spk[i] for i in mine], style_mel=style.index_select(0, sel))
+    else:
+        out = model.inference_batch(ids)
     torch.cuda.synchronize()
     s1 = time.perf_counter()
-    ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=7)
+    if gst:
+        ap.griffin_lim_batch(out["linear"], out["frames"], mode=audiomod._native.TTS_GL_FROM_LINEAR, seed=7)
+    else:
+        ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=7)
     torch.cuda.synchronize()
     s2 = time.perf_counter()
     dec_ms = model.last_timing.get("decoder_loop_ms", 0.0)
@@ -226,7 +321,7 @@ def main():
         Lmean = float(np.mean([len(x) for x in ids]))
         steps = max(out["steps"])
         frames_total = sum(out["frames"])
-        kd = model.profile_step_kernels(reps=50)
+        kd = model.profile_step_kernels(reps=50 if not gst else 20)
         kg = ap.profile_gl_kernels(reps=20)
         launches = {k: steps for k in kd}
         # one GL iteration = overlap-add launch (frames -> float32 signal) + per-frame
@@ -234,12 +329,12 @@ def main():
         launches["gl_iter"] = args.iters
         allk = {**kd, "gl_iter": kg["gl_iter"] + kg["gl_ola"]}
         for k, ms in allk.items():
-            kind, alg = kernel_algorithmic(k, B, Lmean, frames_total)
+            kind, alg = (kernel_algorithmic_gst if gst else kernel_algorithmic)(k, B, Lmean, frames_total)
             kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],
                               algorithmic_bytes=alg, achieved_gbs=alg / (ms * 1e-3) / 1e9 if ms > 0 else None)
         dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
         kdom = kernels[dom]
-        traffic = load_traffic(dom)
+        traffic = load_traffic(("gst_" if gst else "") + dom)
         roofline = dict(bound="hbm", kernel=dom, achieved=kdom["achieved_gbs"], peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=kdom["achieved_gbs"] / HBM_PEAK_GBS, traffic=traffic,
                         algorithmic_bytes_per_launch=kdom["algorithmic_bytes"], mean_launch_ms=kdom["mean_ms"])
@@ -247,8 +342,16 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
 
+    if gst:
+        workload = (f"configs[4]: TacotronGST batch={args.batch} per GPU, L ~ U{{60..160}}, style mel [B,200,80], "
+                    f"4 speakers, linear GL {args.iters} iters")
+    elif args.batch == 1:
+        workload = f"configs[1]: Tacotron2 single sentence, HIP decoder loop + HIP Griffin-Lim {args.iters} iters"
+    else:
+        workload = f"Tacotron2 batch={args.batch} per GPU, {args.lengths} lengths"
     rec = {
-        "metric": "mel-frames/sec + RTF, Tacotron2 + 60-iter Griffin-Lim, LJSpeech",
+        "metric": ("mel-frames/sec + RTF, TacotronGST + 60-iter Griffin-Lim (configs[4])" if gst else
+                   "mel-frames/sec + RTF, Tacotron2 + 60-iter Griffin-Lim, LJSpeech"),
         "value": value,
         "unit": "mel-frames/s",
         "n_gpus": world,
@@ -260,12 +363,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic ids, random-init weights (deterministic generator, seed 0)",
-        "config": {"workload": ("configs[1]: Tacotron2 single sentence, HIP decoder loop + HIP Griffin-Lim "
-                                f"{args.iters} iters" if args.batch == 1 else
-                                f"Tacotron2 batch={args.batch} per GPU, {args.lengths} lengths"),
-                   "sentences_per_gpu": args.batch, "L": args.L if args.lengths == "fixed" else "U{60..160}",
+        "config": {"workload": workload,
+                   "sentences_per_gpu": args.batch,
+                   "L": args.L if (args.lengths == "fixed" and not gst) else "U{60..160}",
                    "frames_per_step": frames_per_step, "gl_iters": args.iters,
-                   "model_config": "config_tacotron2.json + forward_attn_mask (synthesize.py:86)",
+                   "model_config": ("config_tacotron_gst.json, num_speakers=4" if gst else
+                                    "config_tacotron2.json + forward_attn_mask (synthesize.py:86)"),
                    "parallelism": (f"sentence-sharded x{world} (LPT), RCCL gather-v of waveforms to rank 0"
                                    if world > 1 else "single GPU")},
         "rtf": rtf,
