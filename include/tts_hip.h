@@ -58,6 +58,11 @@ void tts_encoder_destroy(tts_encoder* e);
  *                lens[b] are zero. */
 tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
                            float* out, void* stream);
+/* Same with the BiLSTM state carried (Encoder.inference_truncated, layers/tacotron2.py:85-93):
+ *   state_in  [dev] fp32 [4][B][256] = (h_fwd, h_bwd, c_fwd, c_bwd) initial state, or NULL (zeros)
+ *   state_out [dev] fp32 [4][B][256] final state (h_n, c_n per direction), or NULL. */
+tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
+                                 const float* state_in, float* state_out, float* out, void* stream);
 
 /* Decoder flags: the arguments of layers/tacotron2.py:98-100 (Decoder.__init__) that change
  * inference numerics, as mapped from the JSON config by utils/generic_utils.py:275-288. */
@@ -96,6 +101,14 @@ void tts_decoder_destroy(tts_decoder* d);
 tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
                            int max_steps, int steps_cap, float* mel, float* stop, float* align,
                            int32_t* n_steps, void* stream);
+
+/* Continuous mode: replaces Decoder.inference_truncated (layers/tacotron2.py:287-328).  Same
+ * arguments as tts_decoder_run, batch 1 only; the attention-LSTM / decoder-LSTM states, the
+ * context and the memory (last mel frame) carry over from the previous batch-1 run on this handle,
+ * the attention and stop-rule state restart. */
+tts_status tts_decoder_run_continue(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
+                                    int max_steps, int steps_cap, float* mel, float* stop, float* align,
+                                    int32_t* n_steps, void* stream);
 
 /* Per-step timing of the last tts_decoder_run (ms of GPU time of the step loop, steps run). */
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run);

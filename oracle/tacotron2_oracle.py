@@ -70,30 +70,36 @@ class Tacotron2Oracle:
         return _sig(o) * np.tanh(c2), c2
 
     # ------------------------------------------------------------------ encoder
-    def encoder(self, ids, speaker_id=None):
+    def encoder(self, ids, speaker_id=None, state=None, return_state=False):
         """Tacotron2.inference embedding + Encoder.inference (models/tacotron2.py:63-66,
-        layers/tacotron2.py:78-83).  ids [L] -> [L, 512]."""
+        layers/tacotron2.py:78-83).  ids [L] -> [L, 512].  ``state`` = (h [2,256], c [2,256]) is the
+        BiLSTM's initial state (Encoder.inference_truncated, :85-93; None = zeros)."""
         x = self.w["embedding.weight"][ids].T  # [512, L]
         for i in range(3):
             x = self._conv_bn(f"encoder.convolutions.{i}", x, "relu")
         x = x.T  # [L, 512]
         L = x.shape[0]
         out = np.zeros((L, 512), dtype=self.dt)
+        hN = np.zeros((2, 256), self.dt)
+        cN = np.zeros((2, 256), self.dt)
         for d, sfx, order in ((0, "", range(L)), (1, "_reverse", range(L - 1, -1, -1))):
-            h = np.zeros(256, self.dt)
-            c = np.zeros(256, self.dt)
+            h = np.zeros(256, self.dt) if state is None else state[0][d].astype(self.dt)
+            c = np.zeros(256, self.dt) if state is None else state[1][d].astype(self.dt)
             p = [self.w[f"encoder.lstm.{n}_l0{sfx}"] for n in ("weight_ih", "weight_hh", "bias_ih", "bias_hh")]
             for t in order:
                 h, c = self._lstm_cell(x[t], h, c, *p)
                 out[t, d * 256:(d + 1) * 256] = h
+            hN[d], cN[d] = h, c
         if speaker_id is not None and "speaker_embedding.weight" in self.w:
             out = out + self.w["speaker_embedding.weight"][speaker_id][None, :]
-        return out
+        return (out, (hN, cN)) if return_state else out
 
     # ------------------------------------------------------------------ decoder
-    def decoder(self, memory_in):
+    def decoder(self, memory_in, carry=None, return_carry=False):
         """Decoder.inference (layers/tacotron2.py:249-285) for one sentence.
-        memory_in [L, 512] -> mel [T*r, 80], stop [T], align [T, L]."""
+        memory_in [L, 512] -> mel [T*r, 80], stop [T], align [T, L].  ``carry`` = (h_att, c_att,
+        h_dec, c_dec, ctx, memory) continues from a previous call (Decoder.inference_truncated,
+        :287-328: RNN states, context and the last mel frame kept; attention restarts)."""
         w = self.w
         dt = self.dt
         inputs = memory_in.astype(dt)
@@ -113,6 +119,8 @@ class Tacotron2Oracle:
         u = 0.5
         win_idx = -1
         memory = w["decoder.go_frame_init.weight"][0].copy()
+        if carry is not None:
+            h_att, c_att, h_dec, c_dec, ctx, memory = [np.array(v, dtype=dt) for v in carry]
         outs, stops, aligns = [], [], []
         flag1 = False
         stop_count = 0
@@ -206,6 +214,8 @@ class Tacotron2Oracle:
             memory = mel
             t += 1
         mel = np.stack(outs).reshape(-1, 80)  # [T*r, 80]
+        if return_carry:
+            return mel, np.array(stops), np.stack(aligns), (h_att, c_att, h_dec, c_dec, ctx, outs[-1])
         return mel, np.array(stops), np.stack(aligns)
 
     def postnet(self, mel):
@@ -221,6 +231,16 @@ class Tacotron2Oracle:
         enc = self.encoder(np.asarray(ids), speaker_id)
         mel, stop, align = self.decoder(enc)
         return dict(enc=enc, mel=mel, mel_post=self.postnet(mel), stop=stop, align=align)
+
+    def inference_truncated(self, ids_seq):
+        """Tacotron2.inference_truncated (models/tacotron2.py:75-89) over consecutive texts: the
+        encoder BiLSTM state and the decoder carry pass from one call to the next."""
+        enc_state, carry, res = None, None, []
+        for ids in ids_seq:
+            enc, enc_state = self.encoder(np.asarray(ids), None, enc_state, return_state=True)
+            mel, stop, align, carry = self.decoder(enc, carry, return_carry=True)
+            res.append(dict(enc=enc, mel=mel, mel_post=self.postnet(mel), stop=stop, align=align))
+        return res
 
     def infer_batch(self, ids_list):
         return [self.inference(ids) for ids in ids_list]

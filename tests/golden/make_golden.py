@@ -177,6 +177,33 @@ def make_taco_fixtures():
         print(f"{name}: L={L} steps={align.shape[1]} frames={mel.shape[1]} flags={flags}")
 
 
+def make_truncated_fixture():
+    """Tacotron2.inference_truncated over three consecutive texts (continuous mode,
+    models/tacotron2.py:75-89): encoder BiLSTM state and decoder states carry over."""
+    import torch
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    from utils.generic_utils import load_config, setup_model
+    C = load_config(os.path.join(REF, "config_tacotron2.json"))
+    C.num_speakers = 0
+    C.forward_attn_mask = True
+    model = setup_model(130, 0, C)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in weights.tacotron2_weights(0, num_chars=130).items()})
+    model.eval()
+    out = {}
+    for i, (L, seed) in enumerate(((12, 61), (9, 62), (15, 63))):
+        ids = weights.synthetic_ids(L, seed)
+        with torch.no_grad():
+            mel, mel_post, align, stop = model.inference_truncated(torch.from_numpy(ids)[None])
+        out.update({f"ids{i}": ids, f"mel{i}": mel[0].numpy(), f"mel_post{i}": mel_post[0].numpy(),
+                    f"align{i}": align[0].numpy(), f"stop{i}": stop[0, :, 0].numpy()})
+        print(f"trunc_t2_3texts text {i}: L={L} T={mel.shape[1]}")
+    flags = dict(attn_norm=C.attention_norm, forward_attn=C.use_forward_attn, trans_agent=C.transition_agent,
+                 forward_attn_mask=C.forward_attn_mask, location_attn=C.location_attn, attn_win=C.windowing,
+                 max_decoder_steps=model.decoder.max_decoder_steps)
+    np.savez_compressed(os.path.join(HERE, "trunc_t2_3texts.npz"), flags=np.array(repr(flags)), **out)
+
+
 def make_gl_fixtures():
     _stub_text_deps()
     _stub_audio_deps()
@@ -230,10 +257,12 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "taco", "gl"]
+    which = sys.argv[1:] or ["model", "taco", "truncated", "gl"]
     if "model" in which:
         make_model_fixtures()
     if "taco" in which:
         make_taco_fixtures()
+    if "truncated" in which:
+        make_truncated_fixture()
     if "gl" in which:
         make_gl_fixtures()

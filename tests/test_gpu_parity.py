@@ -236,3 +236,20 @@ def test_native_errors_are_raised():
     bad["decoder.attention_rnn.weight_ih"] = torch.zeros(4096, 700)
     with pytest.raises(RuntimeError):
         m.load_state_dict(bad)
+
+
+def test_inference_truncated_vs_reference():
+    """Tacotron2.inference_truncated over three consecutive texts (continuous mode) vs the
+    reference: encoder BiLSTM state, decoder LSTM states, context and memory carry over."""
+    z = golden("trunc_t2_3texts")
+    m = _model(golden_flags(z))
+    for i in range(3):
+        mel, mel_post, align, stop = m.inference_truncated(torch.from_numpy(z[f"ids{i}"])[None])
+        assert mel.shape[1] == z[f"mel{i}"].shape[0]
+        np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z[f"align{i}"].argmax(1))
+        assert rel_rms(mel[0].cpu().numpy(), z[f"mel{i}"]) < MEL_RTOL
+        assert rel_rms(mel_post[0].cpu().numpy(), z[f"mel_post{i}"]) < MEL_RTOL
+    # a fresh inference() afterwards is unaffected
+    z0 = golden("t2_fwdmask_L12")
+    mel, mel_post, _, _ = m.inference(torch.from_numpy(z0["ids"])[None])
+    assert rel_rms(mel_post[0].cpu().numpy(), z0["mel_post"]) < MEL_RTOL

@@ -134,3 +134,20 @@ def test_tacotron_stop_rule_variants():
     assert z["align"][-1, -1] > 0.6 and z["align"].shape[0] < 41
     z = golden("gst_L24_style_spk")
     assert z["align"].shape[0] == golden_flags(z)["max_decoder_steps"] + 1
+
+
+def test_tacotron2_truncated_oracle_matches_reference():
+    """Continuous mode (Tacotron2.inference_truncated over three texts): encoder BiLSTM state and
+    decoder states carry over (models/tacotron2.py:75-89)."""
+    z = golden("trunc_t2_3texts")
+    fl = golden_flags(z)
+    o = Tacotron2Oracle(weights_mod().tacotron2_weights(0), dtype=np.float32, **fl)
+    res = o.inference_truncated([z[f"ids{i}"] for i in range(3)])
+    for i, r in enumerate(res):
+        assert r["mel"].shape == z[f"mel{i}"].shape
+        np.testing.assert_array_equal(r["align"].argmax(1), z[f"align{i}"].argmax(1))
+        assert rel_rms(r["mel"], z[f"mel{i}"]) < 1e-5
+        assert rel_rms(r["mel_post"], z[f"mel_post{i}"]) < 1e-5
+    # the carry matters: text 1 alone differs from text 1 after text 0
+    alone = o.inference(z["ids1"])
+    assert rel_rms(alone["mel"], z["mel1"]) > 1e-3

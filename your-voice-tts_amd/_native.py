@@ -21,8 +21,9 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 
 # every symbol include/tts_hip.h declares
 EXPORTS = (
-    "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run",
-    "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_last_timing",
+    "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state",
+    "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue",
+    "tts_decoder_last_timing",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
@@ -75,6 +76,8 @@ def _declare(lib):
     lib.tts_decoder_destroy.restype = None
     lib.tts_decoder_run.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, vp,
                                     I32P, vp]
+    lib.tts_encoder_run_state.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]
+    lib.tts_decoder_run_continue.argtypes = lib.tts_decoder_run.argtypes
     lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_postnet_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
     lib.tts_postnet_destroy.argtypes = [vp]
@@ -103,7 +106,8 @@ def _declare(lib):
     lib.tts_version.restype = ctypes.c_char_p
     for name in EXPORTS:
         fn = getattr(lib, name)
-        if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet")):
+        if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet", "_state",
+                          "_continue")):
             fn.restype = ctypes.c_int
 
 

@@ -14,14 +14,16 @@ __global__ void decoder_init_kernel(const InitArgs a) {
     // step 0 reads the "previous" ping-pong slot (parity 1) for h_att / h_dec and xa[0] for ctx.
     float* ha = a.h_att + a.h_pstride + (int64_t)b * HATT;
     float* hd = a.h_dec + a.h_pstride + (int64_t)b * HDEC;
-    for (int k = threadIdx.x; k < HATT; k += blockDim.x) {
+    for (int k = threadIdx.x; k < HATT && !a.keep; k += blockDim.x) {
         ha[k] = a.att_init[k];  // attention_rnn_init (tacotron2.py:162-163)
         a.c_att[(int64_t)b * HATT + k] = 0.f;
         hd[k] = a.dec_init[k];  // decoder_rnn_inits (tacotron2.py:167-168)
         a.c_dec[(int64_t)b * HDEC + k] = 0.f;
     }
-    for (int k = threadIdx.x; k < ENC; k += blockDim.x) a.xa[(int64_t)b * XA + PRE + k] = 0.f;  // context = 0
-    for (int k = threadIdx.x; k < a.nmel; k += blockDim.x) a.mem[(int64_t)b * a.nmel + k] = a.go[k];  // go frame
+    if (!a.keep) {
+        for (int k = threadIdx.x; k < ENC; k += blockDim.x) a.xa[(int64_t)b * XA + PRE + k] = 0.f;  // context = 0
+        for (int k = threadIdx.x; k < a.nmel; k += blockDim.x) a.mem[(int64_t)b * a.nmel + k] = a.go[k];  // go frame
+    }
     // Attention.init_states / init_forward_attn (common_layers.py:139-161): alpha = [1, 1e-7, ...]
     for (int j = threadIdx.x; j < a.Lcap; j += blockDim.x) {
         const int64_t o = (int64_t)b * a.Lcap + j;

@@ -57,6 +57,7 @@ struct AttnArgs {
 
 struct InitArgs {
     int B, Lcap, nmel;
+    int keep;  // continuous mode: keep h / c / context / memory, restart attention and stop state
     const int* lens;
     const float* att_init;  // [1024]
     const float* dec_init;  // [1024]

@@ -58,6 +58,7 @@ struct tts_decoder {
     float last_ms = 0.f;
     int last_steps = 0;
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
+    int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
     InitArgs last_init{};
 };
 
@@ -236,6 +237,11 @@ tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s) {
 }
 
 }  // namespace
+
+namespace {
+tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax, int max_steps,
+                       int steps_cap, float* mel, float* stop, float* align, int32_t* n_steps, void* stream, bool keep);
+}
 
 extern "C" {
 
@@ -430,6 +436,23 @@ void tts_decoder_destroy(tts_decoder* d) {
 
 tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax, int max_steps,
                            int steps_cap, float* mel, float* stop, float* align, int32_t* n_steps, void* stream) {
+    return decoder_run(d, enc, lens, B, Lmax, max_steps, steps_cap, mel, stop, align, n_steps, stream, false);
+}
+
+tts_status tts_decoder_run_continue(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
+                                    int max_steps, int steps_cap, float* mel, float* stop, float* align,
+                                    int32_t* n_steps, void* stream) {
+    TTS_CHECK(d && B == 1, TTS_ERR_UNSUPPORTED, "continuous (truncated) decoding is batch-1, as the reference's");
+    TTS_CHECK(d->last_B == 1 && d->last_steps_done > 0, TTS_ERR_INVALID,
+              "tts_decoder_run_continue needs a previous batch-1 tts_decoder_run / _continue");
+    return decoder_run(d, enc, lens, B, Lmax, max_steps, steps_cap, mel, stop, align, n_steps, stream, true);
+}
+
+}  // extern "C"
+
+namespace {
+tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax, int max_steps,
+                       int steps_cap, float* mel, float* stop, float* align, int32_t* n_steps, void* stream, bool keep) {
     TTS_CHECK(d && enc && lens && mel && stop && n_steps, TTS_ERR_INVALID, "null argument");
     TTS_CHECK(B >= 1 && B <= d->Bcap, TTS_ERR_INVALID, "batch exceeds decoder capacity");
     TTS_CHECK(Lmax >= 2 && Lmax <= d->Lcap, TTS_ERR_INVALID, "Lmax exceeds decoder capacity");
@@ -456,8 +479,25 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
     ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
     ia.step = d->state; ia.n_active = d->state + 1;
+    if (keep) {
+        // Decoder.inference_truncated (layers/tacotron2.py:287-328): attention / stop state restart,
+        // the RNN states, context and memory (the last mel frame) carry over.  The last step of the
+        // previous run (parity (n-1) & 1) left h_att / h_dec in its slot, the context in the other
+        // parity's xa row, and relu(W1 mel_last) in pre1 (the fused mel launch computes the next
+        // step's prenet layer 1): move them to the slots step 0 reads.
+        const int pl = (d->last_steps_done - 1) & 1;
+        const size_t hp = (size_t)d->Bcap * HATT;
+        if (pl != 1) {
+            TTS_HIP(hipMemcpyAsync(d->h_att + hp, d->h_att, HATT * sizeof(float), hipMemcpyDeviceToDevice, s));
+            TTS_HIP(hipMemcpyAsync(d->h_dec + hp, d->h_dec, HDEC * sizeof(float), hipMemcpyDeviceToDevice, s));
+        }
+        if (1 - pl != 0)
+            TTS_HIP(hipMemcpyAsync(d->xa + PRE, d->xa + (size_t)d->Bcap * XA + PRE, ENC * sizeof(float),
+                                   hipMemcpyDeviceToDevice, s));
+        ia.keep = 1;
+    }
     TTS_HIP(launch_decoder_init(ia, s));
-    { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+    if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
     auto key = std::make_tuple(B, Lmax, max_steps);
     auto it = d->graphs.find(key);
     if (it == d->graphs.end()) {
@@ -520,8 +560,13 @@ tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens
     d->last_max_steps = max_steps;
     d->last_first = first;
     d->last_init = ia;
+    d->last_init.keep = 0;
+    d->last_steps_done = B == 1 ? (int)n_steps[0] : 0;
     return TTS_OK;
 }
+}  // namespace
+
+extern "C" {
 
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run) {
     TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");

@@ -50,9 +50,8 @@ tts_status emalloc(tts_encoder* e, T** p, size_t n) {
 
 tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s) {
     // outputs past L_b and the initial LSTM state are zero
+    // outputs past L_b are zero; the initial LSTM state is set outside the graph (tts_encoder_run_state)
     TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
-    TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * (size_t)e->Bcap * EH, s));
-    TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * (size_t)e->Bcap * EH, s));
     float* bufs[2] = {e->act0, e->act1};
     for (int l = 0; l < 3; ++l) {
         ConvArgs a{};
@@ -213,8 +212,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
     return TTS_OK;
 }
 
-tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax, float* out,
-                           void* stream) {
+tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
+                                 const float* state_in, float* state_out, float* out, void* stream) {
     TTS_CHECK(e && ids && lens && out, TTS_ERR_INVALID, "null argument");
     TTS_CHECK(B >= 1 && B <= e->Bcap && Lmax >= 1 && Lmax <= e->Lcap, TTS_ERR_INVALID,
               "batch / length exceeds encoder capacity");
@@ -226,6 +225,18 @@ tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* le
     TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
     TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
     TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    // initial state (h_0, c_0) of both directions: step 0 reads the parity-1 h slots
+    const size_t hs = (size_t)e->Bcap * EH;  // per-direction stride
+    const size_t row = (size_t)B * EH * sizeof(float);
+    if (state_in) {  // [h_fwd, h_bwd, c_fwd, c_bwd] x [B][256]
+        for (int d = 0; d < 2; ++d) {
+            TTS_HIP(hipMemcpyAsync(e->h + 2 * hs + d * hs, state_in + (size_t)d * B * EH, row, hipMemcpyDeviceToDevice, s));
+            TTS_HIP(hipMemcpyAsync(e->c + d * hs, state_in + (size_t)(2 + d) * B * EH, row, hipMemcpyDeviceToDevice, s));
+        }
+    } else {
+        TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * hs, s));
+        TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * hs, s));
+    }
     auto key = std::make_pair(B, Lmax);
     auto git = e->graphs.find(key);
     if (git == e->graphs.end()) {
@@ -243,9 +254,26 @@ tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* le
     }
     TTS_HIP(hipGraphLaunch(git->second, s));
     TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
+    if (state_out) {
+        // h_n of each direction: sentence b wrote its last state at step L_b - 1 (slot (L_b-1) & 1)
+        for (int b = 0; b < B; ++b) {
+            const float* hsrc = e->h + (size_t)((lens[b] - 1) & 1) * 2 * hs + (size_t)b * EH;
+            for (int d = 0; d < 2; ++d) {
+                TTS_HIP(hipMemcpyAsync(state_out + ((size_t)d * B + b) * EH, hsrc + d * hs, EH * sizeof(float),
+                                       hipMemcpyDeviceToDevice, s));
+                TTS_HIP(hipMemcpyAsync(state_out + ((size_t)(2 + d) * B + b) * EH, e->c + d * hs + (size_t)b * EH,
+                                       EH * sizeof(float), hipMemcpyDeviceToDevice, s));
+            }
+        }
+    }
     TTS_HIP(hipEventRecord(e->ev_out, s));
     TTS_HIP(hipStreamWaitEvent(cs, e->ev_out, 0));
     return TTS_OK;
+}
+
+tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax, float* out,
+                           void* stream) {
+    return tts_encoder_run_state(e, ids, lens, B, Lmax, nullptr, nullptr, out, stream);
 }
 
 }  // extern "C"

@@ -10,6 +10,9 @@
 namespace tts {
 
 constexpr int MAX_WAVES = 16;
+#ifndef TTS_NT_ROLES
+#define TTS_NT_ROLES 0
+#endif
 constexpr int PRE_DIM = 256;  // prenet width (layers/tacotron2.py:108)
 __device__ const int kOneActive[2] = {0, 1};  // {step 0, 1 active} for launches without step state
 
@@ -125,7 +128,14 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         for (int u = 0; u < U; ++u) {
             const int c = c0 + u;
             if (c < cend) {
-                wv[u] = Wp[(size_t)c * 64];  // default policy: the 72.7 MB weight set stays in the Infinity Cache across steps
+                if ((TTS_NT_ROLES >> ROLE) & 1) {
+                    // non-temporal (stream) policy: this matrix passes through L2 without evicting
+                    // the default-policy matrices that stay resident there across steps
+                    const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(Wp + (size_t)c * 64));
+                    wv[u] = float4{t[0], t[1], t[2], t[3]};
+                } else {
+                    wv[u] = Wp[(size_t)c * 64];
+                }
                 const int s = c < cb[0] ? 0 : (c < cb[1] ? 1 : 2);
 #pragma unroll
                 for (int mt = 0; mt < NT; ++mt) {

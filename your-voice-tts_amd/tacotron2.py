@@ -63,6 +63,8 @@ class Tacotron2:
         self._params = OrderedDict(
             (k, torch.from_numpy(v)) for k, v in weights.generate(self._spec, seed).items())
         self._native = None  # (decoder handle, postnet handle, key)
+        self._enc_state = None  # inference_truncated: encoder BiLSTM state [4, 1, 256] (h_f, h_b, c_f, c_b)
+        self._trunc_started = False  # inference_truncated: decoder states carried on the native handle
         self.last_lengths = None
         self.last_timing = {}
 
@@ -115,6 +117,8 @@ class Tacotron2:
 
     def _drop_native(self):
         self._lstm = None
+        self._enc_state = None
+        self._trunc_started = False
         if self._native is not None:
             lib = _native.load_library()
             lib.tts_decoder_destroy(self._native[0])
@@ -186,7 +190,7 @@ class Tacotron2:
 
     # ------------------------------------------------------------------ inference
     @torch.no_grad()
-    def inference_batch(self, ids_list, speaker_ids=None, enc=None, lens=None):
+    def inference_batch(self, ids_list, speaker_ids=None, enc=None, lens=None, _continue=False):
         """Ragged batch: ids_list = list of 1-D id sequences.  Returns a dict of padded CUDA
         tensors (mel, mel_post [B,T,80]; align [B,Tsteps,L]; stop [B,Tsteps]) plus per-sentence
         ``frames`` (n_steps*r) and ``steps``."""
@@ -217,10 +221,11 @@ class Tacotron2:
         align = torch.zeros(B, cap, Lmax, device=dev)
         n_steps = (ctypes.c_int32 * B)()
         stream = _native.stream_handle()
-        _native.check(lib.tts_decoder_run(hdec, ctypes.c_void_p(enc.data_ptr()), _native.i32_array(lens), B, Lmax,
-                                          max_steps, cap, ctypes.c_void_p(mel.data_ptr()),
-                                          ctypes.c_void_p(stop.data_ptr()), ctypes.c_void_p(align.data_ptr()),
-                                          n_steps, stream), "tts_decoder_run")
+        run = lib.tts_decoder_run_continue if _continue else lib.tts_decoder_run
+        _native.check(run(hdec, ctypes.c_void_p(enc.data_ptr()), _native.i32_array(lens), B, Lmax,
+                          max_steps, cap, ctypes.c_void_p(mel.data_ptr()),
+                          ctypes.c_void_p(stop.data_ptr()), ctypes.c_void_p(align.data_ptr()),
+                          n_steps, stream), "tts_decoder_run")
         steps = [int(n_steps[b]) for b in range(B)]
         for s in steps:
             if s >= max_steps:
@@ -257,7 +262,36 @@ class Tacotron2:
         _native.check(lib.tts_decoder_profile(hdec, int(reps), ms, n), "tts_decoder_profile")
         return dict(zip(_native.DECODER_STEP_KERNELS, [float(v) for v in ms]))
 
+    @torch.no_grad()
     def inference_truncated(self, text, speaker_ids=None):
-        raise NotImplementedError("inference_truncated (continuous mode) is SURVEY 8(f) row 4, not yet built")
+        """models/tacotron2.py:75-89, continuous inference over consecutive calls (batch 1): the
+        encoder BiLSTM state (layers/tacotron2.py:85-93) and the decoder's RNN states, context and
+        memory (:287-328) carry over; attention and stop rule restart.  Returns the same tuple as
+        ``inference``."""
+        _native.lib()
+        text = torch.as_tensor(text)
+        if text.dim() == 1:
+            text = text.unsqueeze(0)
+        if text.shape[0] != 1:
+            raise ValueError("inference_truncated is batch-1 (the reference keeps one state per module)")
+        L = int(text.shape[1])
+        lib, _, _ = self._handles(L, 1)
+        if self.flags["forward_attn_mask"] and L < 2:
+            raise ValueError("encoder length must be >= 2 with forward_attn_mask")
+        ids32 = text.to(self.device, dtype=torch.int32).contiguous()
+        enc = torch.empty(1, L, 512, device=self.device)
+        state_out = torch.empty(4, 1, 256, device=self.device)
+        st_in = self._enc_state
+        _native.check(lib.tts_encoder_run_state(
+            self._native[3], ctypes.c_void_p(ids32.data_ptr()), _native.i32_array([L]), 1, L,
+            ctypes.c_void_p(st_in.data_ptr()) if st_in is not None else None, ctypes.c_void_p(state_out.data_ptr()),
+            ctypes.c_void_p(enc.data_ptr()), _native.stream_handle()), "tts_encoder_run_state")
+        self._enc_state = state_out
+        if speaker_ids is not None and "speaker_embedding.weight" in self._params:
+            enc = enc + F.embedding(torch.as_tensor(speaker_ids, device=self.device).view(-1),
+                                    self._params["speaker_embedding.weight"])[:, None, :]
+        out = self.inference_batch(None, enc=enc, lens=[L], _continue=self._trunc_started)
+        self._trunc_started = True
+        return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
     __call__ = inference
