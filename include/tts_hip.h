@@ -162,6 +162,16 @@ void tts_gl_destroy(tts_gl* g);
 tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
                       const double* phase_u, uint64_t seed, int iters, double* wav, void* stream);
 
+/* Mel analysis for GST style wavs: AudioProcessor.melspectrogram (utils/audio.py:146-152) as used by
+ * compute_style_mel (utils/synthesis.py:28-35): pre-emphasis FIR, librosa 0.6.2 stft (float64 FFT,
+ * complex64 result), |D|, mel projection (float64), amp->dB, _normalize.
+ *   mel_basis [host] fp64 [num_mels][n_fft/2+1] (librosa filters.mel), set once per handle
+ *   wav [dev] fp64 [B][Nmax]; N [host] int32 [B] (>= 2); mel [dev] fp32 [B][Fmax][num_mels]
+ *   (frame-major; sentence b has 1 + N[b]/hop frames, the rest zero). */
+tts_status tts_gl_set_mel_basis(tts_gl* g, const double* mel_basis);
+tts_status tts_gl_melspectrogram(tts_gl* g, const double* wav, const int32_t* N, int B, int64_t Nmax, float* mel,
+                                 int Fmax, void* stream);
+
 /* Time of the last tts_gl_run's iteration loop (ms, GPU) and kernel launches in it. */
 tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
 

@@ -223,6 +223,32 @@ class AudioOracle:
         y = self.griffin_lim(self.linear_magnitude(spec), phase_u, iters)
         return self.inv_preemphasis(y) if self.preemphasis != 0 else y
 
+    # ---- forward half used by compute_style_mel (utils/synthesis.py:28-35)
+    def apply_preemphasis(self, x):  # utils/audio.py:128-131
+        if self.preemphasis == 0:
+            raise RuntimeError(" !! Preemphasis is applied with factor 0.0. ")
+        return scipy.signal.lfilter([1, -self.preemphasis], [1], x)
+
+    def amp_to_db(self, x):  # utils/audio.py:121-123
+        min_level = np.exp(self.min_level_db / 20 * np.log(10))
+        return 20 * np.log10(np.maximum(min_level, x))
+
+    def normalize(self, S):  # utils/audio.py:79-94
+        if not self.signal_norm:
+            return S
+        S_norm = (S - self.min_level_db) / -self.min_level_db
+        if self.symmetric_norm:
+            S_norm = (2 * self.max_norm) * S_norm - self.max_norm
+            return np.clip(S_norm, -self.max_norm, self.max_norm) if self.clip_norm else S_norm
+        S_norm = self.max_norm * S_norm
+        return np.clip(S_norm, 0, self.max_norm) if self.clip_norm else S_norm
+
+    def melspectrogram(self, y):  # utils/audio.py:146-152
+        y = self.apply_preemphasis(y) if self.preemphasis != 0 else y
+        D = stft(y, self.n_fft, self.hop_length, self.win_length)
+        S = self.amp_to_db(np.dot(self.mel_basis(), np.abs(D))) - self.ref_level_db
+        return self.normalize(S)
+
     @staticmethod
     def wav_to_int16(wav):  # utils/audio.py:56-58 (the value save_wav writes)
         wav = np.asarray(wav)

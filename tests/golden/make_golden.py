@@ -254,6 +254,13 @@ def make_gl_fixtures():
     buf.seek(0)
     _, pcm = scipy.io.wavfile.read(buf)
     np.savez_compressed(os.path.join(HERE, "save_wav.npz"), wav=wav, pcm=pcm)
+    # forward analysis of compute_style_mel (utils/synthesis.py:28-35): AudioProcessor.melspectrogram
+    # on a seeded float64 waveform (1.3 s: chirp + noise), librosa stft/mel via the restatement
+    rng2 = np.random.Generator(np.random.PCG64(8))
+    n = 28717
+    tt = np.arange(n) / 22050.0
+    y = 0.3 * np.sin(2 * np.pi * (220 + 800 * tt) * tt) + 0.05 * rng2.standard_normal(n)
+    np.savez_compressed(os.path.join(HERE, "melspec.npz"), wav=y, mel=ap.melspectrogram(y))
 
 
 if __name__ == "__main__":

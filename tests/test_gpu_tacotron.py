@@ -178,3 +178,44 @@ def test_gst_synthesis_linear_griffin_lim(audio_cfg):
     np.random.seed(5)
     ref = AudioOracle(**{**C.audio, "griffin_lim_iters": 10}).inv_spectrogram(z["linear"].T)
     assert rel_rms(wav, ref) < 1e-4
+
+
+def test_melspectrogram_vs_reference_glue(audio_cfg):
+    """HIP mel analysis (pre-emphasis FIR, float64 STFT, |D| complex64, mel, dB, normalise) vs the
+    reference AudioProcessor.melspectrogram fixture."""
+    z = golden("melspec")
+    ap = load_pkg("audio").AudioProcessor(**audio_cfg)
+    mel = ap.melspectrogram(z["wav"])
+    assert mel.shape == z["mel"].shape
+    assert np.abs(mel - z["mel"]).max() < 1e-5
+
+
+def test_style_wav_synthesis_vs_oracle(tmp_path):
+    """synthesis(..., style_wav=path) on a TacotronGST: wav file -> load_wav (+ trim) -> HIP mel
+    analysis -> [1, 80, T] style mel read as rows of 80 values by the GST (gst_layers.py:60) ->
+    encoder; the encoder output is checked against the oracle on the same wav."""
+    import scipy.io.wavfile
+    from oracle.griffin_lim_oracle import AudioOracle
+    from oracle.tacotron_oracle import TacotronOracle
+    gu = load_pkg("generic_utils")
+    C = gu.default_config("config_tacotron_gst.json")
+    rng = np.random.Generator(np.random.PCG64(12))
+    n = 22050
+    t = np.arange(n) / 22050.0
+    y = (0.4 * np.sin(2 * np.pi * 330 * t) * (t > 0.2) * (t < 0.8) + 0.001 * rng.standard_normal(n))
+    path = str(tmp_path / "style.wav")
+    scipy.io.wavfile.write(path, 22050, (y * 32767).astype(np.int16))
+    ap = load_pkg("audio").AudioProcessor(**C.audio)
+    x = ap.load_wav(path)
+    assert 0 < len(x) < n  # trimmed (do_trim_silence is on in config_tacotron_gst.json)
+    style = load_pkg("synthesis").compute_style_mel(path, ap)
+    assert style.shape == (1, 80, 1 + len(x) // 275)
+    ref_mel = AudioOracle(**C.audio).melspectrogram(x)
+    assert np.abs(style[0].cpu().numpy() - ref_mel).max() < 1e-5
+    fl = golden_flags(golden("gst_L10_nostyle"))
+    m = _model(fl)
+    ids = weights_mod().synthetic_ids(14, 3)
+    enc = m.encode(torch.from_numpy(ids)[None].cuda(), [14], None, style)
+    o = TacotronOracle(weights_mod().tacotron_gst_weights(0), dtype=np.float32, **fl)
+    ref = o.encoder(ids, None, ref_mel.astype(np.float32).reshape(-1, 80))
+    assert rel_rms(enc[0].cpu().numpy(), ref) < RTOL

@@ -151,3 +151,13 @@ def test_tacotron2_truncated_oracle_matches_reference():
     # the carry matters: text 1 alone differs from text 1 after text 0
     alone = o.inference(z["ids1"])
     assert rel_rms(alone["mel"], z["mel1"]) > 1e-3
+
+
+def test_melspectrogram_oracle_matches_reference_glue(audio_cfg):
+    """AudioProcessor.melspectrogram (utils/audio.py:146-152; compute_style_mel's analysis) vs the
+    reference run with the librosa restatement (glue pinned, librosa internals unpinned)."""
+    z = golden("melspec")
+    ap = AudioOracle(**audio_cfg)
+    mel = ap.melspectrogram(z["wav"])
+    assert mel.shape == z["mel"].shape == (80, 1 + len(z["wav"]) // 275)
+    assert np.abs(mel - z["mel"]).max() < 1e-12

@@ -27,6 +27,7 @@ EXPORTS = (
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
+    "tts_gl_set_mel_basis", "tts_gl_melspectrogram",
     "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
     "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_profile",
     "tts_last_error", "tts_version",
@@ -88,6 +89,8 @@ def _declare(lib):
     lib.tts_gl_destroy.restype = None
     lib.tts_gl_run.argtypes = [vp, ctypes.c_int, vp, I32P, ctypes.c_int, ctypes.c_int, vp, ctypes.c_uint64,
                                ctypes.c_int, vp, vp]
+    lib.tts_gl_set_mel_basis.argtypes = [vp, vp]
+    lib.tts_gl_melspectrogram.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int64, vp, ctypes.c_int, vp]
     lib.tts_gl_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     FP = ctypes.POINTER(ctypes.c_float)
     lib.tts_decoder_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
@@ -107,7 +110,7 @@ def _declare(lib):
     for name in EXPORTS:
         fn = getattr(lib, name)
         if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet", "_state",
-                          "_continue")):
+                          "_continue", "_basis", "_melspectrogram")):
             fn.restype = ctypes.c_int
 
 

@@ -81,6 +81,7 @@ class AudioProcessor:
         self.do_trim_silence = do_trim_silence
         self.n_fft, self.hop_length, self.win_length = self._stft_parameters()
         self._gl = None
+        self._mel_basis_set = False
 
     def _stft_parameters(self):  # utils/audio.py:114-119
         n_fft = (self.num_freq - 1) * 2
@@ -173,6 +174,63 @@ class AudioProcessor:
         ms = (ctypes.c_float * n)()
         _native.check(lib.tts_gl_profile(h, int(reps), ms, n), "tts_gl_profile")
         return dict(zip(_native.GL_KERNELS, [float(v) for v in ms]))
+
+    # ---------------------------------------------------------------- mel analysis (GST style wavs)
+    def melspectrogram_batch(self, wav, N):
+        """wav: CUDA float64 [B, Nmax]; N: samples per sentence.  Returns (CUDA float32
+        [B, Fmax, num_mels] frame-major, frames per sentence = 1 + N // hop)."""
+        lib, h = self._handle()
+        if not self._mel_basis_set:
+            basis = np.ascontiguousarray(self._build_mel_basis(), dtype=np.float64)
+            _native.check(lib.tts_gl_set_mel_basis(h, basis.ctypes.data_as(ctypes.c_void_p)), "tts_gl_set_mel_basis")
+            self._mel_basis_set = True
+        wav = wav.to(torch.float64).contiguous()
+        B, Nmax = wav.shape
+        F = [1 + int(n) // self.hop_length for n in N]
+        mel = torch.empty(B, max(F), self.num_mels, device=wav.device)
+        _native.check(lib.tts_gl_melspectrogram(h, ctypes.c_void_p(wav.data_ptr()), _native.i32_array(N), B, Nmax,
+                                                ctypes.c_void_p(mel.data_ptr()), max(F), _native.stream_handle()),
+                      "tts_gl_melspectrogram")
+        return mel, F
+
+    def melspectrogram(self, y):  # utils/audio.py:146-152 -> ndarray [num_mels, frames]
+        self._handle()  # raises without a GPU / library: no CPU fallback
+        y = np.asarray(y, dtype=np.float64)
+        mel, F = self.melspectrogram_batch(torch.from_numpy(y).cuda()[None], [len(y)])
+        return mel[0, :F[0]].T.double().cpu().numpy()
+
+    def trim_silence(self, wav):
+        """utils/audio.py:212-217 on the host: drop 0.1 s margins, then librosa 0.6.2
+        effects.trim(top_db=40, frame_length=1024, hop_length=256) restated (rms of centre-padded
+        frames, power_to_db against the max, keep frames above -top_db)."""
+        margin = int(self.sample_rate * 0.1)
+        wav = wav[margin:-margin]
+        frame_length, hop_length, top_db = 1024, 256, 40
+        yp = np.pad(wav, frame_length // 2, mode="reflect")
+        n_frames = 1 + (len(yp) - frame_length) // hop_length
+        idx = np.arange(frame_length)[:, None] + hop_length * np.arange(n_frames)[None, :]
+        mse = np.sqrt(np.mean(np.abs(yp[idx]) ** 2, axis=0)) ** 2
+        db = 10.0 * np.log10(np.maximum(1e-10, mse)) - 10.0 * np.log10(np.maximum(1e-10, mse.max()))
+        nz = np.flatnonzero(db > -top_db)
+        if nz.size == 0:
+            return wav[0:0]
+        return wav[int(nz[0]) * hop_length:min(len(wav), (int(nz[-1]) + 1) * hop_length)]
+
+    def load_wav(self, filename, sr=None):
+        """utils/audio.py:235-246 with soundfile's float64 conversion (PCM / 2**(bits-1))."""
+        file_sr, x = scipy.io.wavfile.read(filename)
+        if x.dtype == np.int16:
+            x = x / 32768.0
+        elif x.dtype == np.int32:
+            x = x / 2147483648.0
+        elif x.dtype == np.uint8:
+            x = (x.astype(np.float64) - 128.0) / 128.0
+        else:
+            x = x.astype(np.float64)
+        if self.do_trim_silence:
+            x = self.trim_silence(x)
+        assert self.sample_rate == file_sr, "%s vs %s" % (self.sample_rate, file_sr)
+        return x
 
     def _single(self, spec_nT, mode):
         self._handle()  # raises without a GPU / library: no CPU fallback

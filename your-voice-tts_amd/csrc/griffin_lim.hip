@@ -417,6 +417,87 @@ __global__ __launch_bounds__(SCAN_THREADS) void preemph_scan_kernel(const float*
     }
 }
 
+
+// ---------------------------------------------------------------- mel analysis
+// AudioProcessor.melspectrogram (utils/audio.py:146-152) for the GST style wav
+// (utils/synthesis.py:28-35): pre-emphasis FIR (lfilter([1, -c], [1]), :128-131) -> librosa 0.6.2
+// stft (centre reflect pad, periodic Hann, float64 FFT, complex64 result) -> |D| (float32) ->
+// mel_basis . |D| (float64) -> 20 log10(max(min_level, .)) - ref_level_db -> _normalize (:79-94).
+// One workgroup per (sentence, frame); output frame-major [B][Fmax][num_mels] float32.
+struct MelArgs {
+    const double* wav;  // [B][Nmax]
+    int64_t Nmax;
+    const int* N;       // [B] samples
+    int Fmax;
+    Geo g;
+    GLConst c;
+    const double* basis;  // [num_mels][1025]
+    int n_mels;
+    double coef;          // pre-emphasis (0: none)
+    double min_level, min_db, ref_db, max_norm;
+    int signal_norm, symmetric, clip;
+    float* mel;           // [B][Fmax][n_mels]
+};
+
+__global__ __launch_bounds__(GL_THREADS) void mel_analysis_kernel(const MelArgs a) {
+    const int b = blockIdx.y, f = blockIdx.x;
+    const int N = a.N[b];
+    const int F = 1 + N / a.g.hop;
+    if (f >= F) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ __align__(16) double2 buf0[NH];
+    __shared__ __align__(16) double2 buf1[NH];
+    __shared__ float mag[NB + 3];
+    const FftTw ftw = load_fft_tw(a.c.tw);
+    const double* y = a.wav + (int64_t)b * a.Nmax;
+    constexpr int PN = NFFT / GL_THREADS;
+    double* xr = reinterpret_cast<double*>(buf0);
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+        const int n = tid + i * GL_THREADS;
+        // np.pad(y_pre, n_fft // 2, mode='reflect') of the pre-emphasised signal
+        const int p = reflect_idx(f * a.g.hop + n - NFFT / 2, N);
+        double v = y[p];
+        if (a.coef != 0.0 && p > 0) v = v - a.coef * y[p - 1];
+        xr[n] = a.c.win[n] * v;
+    }
+    __syncthreads();
+    const double2* Z = fft1024<false>(buf0, buf1, ftw);
+    for (int k = tid; k < NB; k += GL_THREADS) {
+        const double2 zk = Z[k & (NH - 1)];
+        const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
+        const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
+        const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};
+        const double2 t = a.c.tw[k];
+        const float re = (float)(E.x + (t.x * O.x - t.y * O.y));  // stft result is complex64
+        const float im = (float)(E.y + (t.x * O.y + t.y * O.x));
+        mag[k] = hypotf(re, im);  // np.abs on complex64
+    }
+    __syncthreads();
+    // mel bands: each wave owns bands wave, wave+4, ...; lanes stride the 1025 bins, float64
+    for (int m = wave; m < a.n_mels; m += GL_THREADS / 64) {
+        const double* row = a.basis + (int64_t)m * NB;
+        double acc = 0.0;
+        for (int k = lane; k < NB; k += 64) acc += row[k] * (double)mag[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) {
+            double S = 20.0 * log10(fmax(a.min_level, acc)) - a.ref_db;
+            if (a.signal_norm) {
+                S = (S - a.min_db) / -a.min_db;
+                if (a.symmetric) {
+                    S = (2.0 * a.max_norm) * S - a.max_norm;
+                    if (a.clip) S = fmin(fmax(S, -a.max_norm), a.max_norm);
+                } else {
+                    S = a.max_norm * S;
+                    if (a.clip) S = fmin(fmax(S, 0.0), a.max_norm);
+                }
+            }
+            a.mel[((int64_t)b * a.Fmax + f) * a.n_mels + m] = (float)S;
+        }
+    }
+}
+
 struct GraphKey {
     int B, Fmax, iters;
     bool operator<(const GraphKey& o) const { return std::tie(B, Fmax, iters) < std::tie(o.B, o.Fmax, o.iters); }
@@ -429,7 +510,9 @@ struct tts_gl {
     Geo g{};
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
-    double *win = nullptr, *win2 = nullptr, *pinv = nullptr;
+    double *win = nullptr, *win2 = nullptr, *pinv = nullptr, *basis = nullptr;
+    int* NS = nullptr;  // mel analysis: samples per sentence
+    int NS_cap = 0;
     double2* tw = nullptr;
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
@@ -453,7 +536,7 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F})
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS})
         if (p) (void)hipFree(p);
     for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1})
         if (e) (void)hipEventDestroy(e);
@@ -674,6 +757,61 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
     for (auto& e : ev) (void)hipEventDestroy(e);
     kernel_ms[0] = (float)(it_ms / reps);
     kernel_ms[1] = (float)(ola_ms / reps);
+    return TTS_OK;
+}
+
+
+tts_status tts_gl_set_mel_basis(tts_gl* g, const double* mel_basis) {
+    TTS_CHECK(g && mel_basis, TTS_ERR_INVALID, "null argument");
+    const size_t n = (size_t)g->cfg.num_mels * NB;
+    if (!g->basis) TTS_HIP(hipMalloc(&g->basis, n * sizeof(double)));
+    TTS_HIP(hipMemcpy(g->basis, mel_basis, n * sizeof(double), hipMemcpyHostToDevice));
+    return TTS_OK;
+}
+
+tts_status tts_gl_melspectrogram(tts_gl* g, const double* wav, const int32_t* N, int B, int64_t Nmax, float* mel,
+                                 int Fmax, void* stream) {
+    TTS_CHECK(g && wav && N && mel && B >= 1 && Fmax >= 1, TTS_ERR_INVALID, "bad melspectrogram arguments");
+    TTS_CHECK(g->basis, TTS_ERR_INVALID, "tts_gl_melspectrogram needs tts_gl_set_mel_basis first");
+    for (int b = 0; b < B; ++b) {
+        TTS_CHECK(N[b] >= 2 && N[b] <= Nmax, TTS_ERR_INVALID, "N[b] out of range [2, Nmax]");
+        TTS_CHECK(1 + N[b] / g->g.hop <= Fmax, TTS_ERR_INVALID, "Fmax < 1 + N[b] / hop");
+    }
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t s = g->stream;
+    if (B > g->NS_cap) {
+        TTS_HIP(hipStreamSynchronize(s));
+        if (g->NS) TTS_HIP(hipFree(g->NS));
+        g->NS = nullptr;
+        TTS_HIP(hipMalloc(&g->NS, B * sizeof(int)));
+        g->NS_cap = B;
+    }
+    TTS_HIP(hipEventRecord(g->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(s, g->ev_in, 0));
+    TTS_HIP(hipMemcpyAsync(g->NS, N, B * sizeof(int), hipMemcpyHostToDevice, s));
+    TTS_HIP(hipMemsetAsync(mel, 0, sizeof(float) * (size_t)B * Fmax * g->cfg.num_mels, s));
+    MelArgs a{};
+    a.wav = wav;
+    a.Nmax = Nmax;
+    a.N = g->NS;
+    a.Fmax = Fmax;
+    a.g = g->g;
+    a.c = GLConst{g->win, g->win2, g->tw};
+    a.basis = g->basis;
+    a.n_mels = g->cfg.num_mels;
+    a.coef = g->cfg.preemphasis;
+    a.min_db = g->cfg.min_level_db;
+    a.min_level = std::exp((double)g->cfg.min_level_db / 20.0 * std::log(10.0));  // utils/audio.py:122
+    a.ref_db = g->cfg.ref_level_db;
+    a.max_norm = g->cfg.max_norm;
+    a.signal_norm = g->cfg.signal_norm;
+    a.symmetric = g->cfg.symmetric_norm;
+    a.clip = g->cfg.clip_norm;
+    a.mel = mel;
+    hipLaunchKernelGGL(mel_analysis_kernel, dim3(Fmax, B), dim3(GL_THREADS), 0, s, a);
+    TTS_HIP(hipGetLastError());
+    TTS_HIP(hipEventRecord(g->ev_out, s));
+    TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
     return TTS_OK;
 }
 

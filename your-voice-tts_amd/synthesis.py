@@ -102,11 +102,12 @@ def _ids_tensor(text, CONFIG):
 
 
 def compute_style_mel(style_wav, ap, use_cuda=True):
-    """utils/synthesis.py:28-35: [1, frames, 80] style mel.  ``style_wav`` may be a wav path (read
-    as float64 like soundfile, analysed by ``ap.melspectrogram``) or an already computed mel
-    ([frames, 80] or [1, frames, 80])."""
+    """utils/synthesis.py:28-35: ``style_wav`` a wav path -> FloatTensor(ap.melspectrogram(
+    ap.load_wav(path))).unsqueeze(0), i.e. [1, 80, frames] (the GST reads it with a view as rows of
+    80 values, layers/gst_layers.py:60, exactly like the reference); or an already computed style
+    mel tensor / array, passed through."""
     if isinstance(style_wav, (str, bytes, os.PathLike)):
-        style = ap.melspectrogram(ap.load_wav(style_wav)).T  # [frames, 80]
+        style = ap.melspectrogram(ap.load_wav(style_wav))  # [80, frames] float64 -> float32 below
     else:
         style = style_wav.cpu().numpy() if torch.is_tensor(style_wav) else np.asarray(style_wav)
     style = torch.as_tensor(np.asarray(style, dtype=np.float32))

@@ -182,10 +182,16 @@ class TacotronGST:
             sm = torch.as_tensor(style_mel, dtype=torch.float32).to(self.device)
             if sm.dim() == 2:
                 sm = sm[None]
+            # ReferenceEncoder.forward views its input as [B, 1, -1, num_mel] (gst_layers.py:60), so
+            # compute_style_mel's [1, 80, T] tensor is read as rows of 80 consecutive values
+            if sm[0].numel() % 80:
+                raise ValueError(f"style_mel of {sm[0].numel()} values per sentence is not a whole number of "
+                                 f"80-value rows")
+            sm = sm.contiguous().view(sm.shape[0], -1, 80)
             if sm.shape[0] == 1 and B > 1:
                 sm = sm.expand(B, -1, -1)  # gst_outputs broadcast over the batch (:71-73)
-            if sm.shape[0] != B or sm.shape[2] != 80:
-                raise ValueError(f"style_mel must be [B or 1, frames, 80], got {tuple(sm.shape)}")
+            if sm.shape[0] != B:
+                raise ValueError(f"style_mel batch {sm.shape[0]} != {B}")
             sm = sm.contiguous()
             Ts = sm.shape[1]
         _native.check(lib.tts_tacotron_encode(
