@@ -204,6 +204,27 @@ def make_truncated_fixture():
     np.savez_compressed(os.path.join(HERE, "trunc_t2_3texts.npz"), flags=np.array(repr(flags)), **out)
 
 
+TEXTS = ["Hello world.", "It took me quite a long time to develop a voice, and now that I have it I'm not going "
+         "to be silent.", "  Mixed   CASE\twhitespace;  (and) punctuation: ok?  ", "Turn left on {HH AW1 S S T AH0 N} Street.",
+         "Numbers 1234 & symbols #%* are dropped!"]
+
+
+def make_text_fixture():
+    """text_to_sequence / sequence_to_text with basic_cleaners (utils/text/__init__.py:77-112) and
+    the symbol tables (utils/text/symbols.py), from the reference module itself."""
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    import importlib
+    text = importlib.import_module("utils.text")
+    symbols = importlib.import_module("utils.text.symbols")
+    seqs = [np.array(text.text_to_sequence(t, ["basic_cleaners"]), dtype=np.int64) for t in TEXTS]
+    back = [text.sequence_to_text(list(s)) for s in seqs]
+    np.savez_compressed(os.path.join(HERE, "text_basic.npz"), texts=np.array(TEXTS), back=np.array(back),
+                        symbols=np.array(symbols.symbols), phonemes=np.array(symbols.phonemes),
+                        **{f"seq{i}": s for i, s in enumerate(seqs)})
+    print("text_basic:", [len(s) for s in seqs])
+
+
 def make_gl_fixtures():
     _stub_text_deps()
     _stub_audio_deps()
@@ -264,12 +285,14 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "taco", "truncated", "gl"]
+    which = sys.argv[1:] or ["model", "taco", "truncated", "text", "gl"]
     if "model" in which:
         make_model_fixtures()
     if "taco" in which:
         make_taco_fixtures()
     if "truncated" in which:
         make_truncated_fixture()
+    if "text" in which:
+        make_text_fixture()
     if "gl" in which:
         make_gl_fixtures()

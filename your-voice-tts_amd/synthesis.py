@@ -93,11 +93,19 @@ def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed
 
 
 # ------------------------------------------------------------------ reference call sites
+def text_to_seqvec(text, CONFIG):
+    """utils/synthesis.py:11-25 (host): ids of a sentence.  Character configs go through
+    text.text_to_sequence; phoneme configs need phonemizer/espeak (not installed) and raise."""
+    from . import text as _text
+    if CONFIG.get("use_phonemes", False):
+        return _text.phoneme_to_sequence(text, [CONFIG.text_cleaner], CONFIG.phoneme_language,
+                                         CONFIG.get("enable_eos_bos_chars", False))
+    return _text.text_to_sequence(text, [CONFIG.text_cleaner])
+
+
 def _ids_tensor(text, CONFIG):
     if isinstance(text, str):
-        raise NotImplementedError(
-            "text front-end (phonemizer/espeak, utils/text) is outside the MI355X path: pass ids "
-            "(e.g. from the reference's phoneme_to_sequence) instead of a string")
+        text = text_to_seqvec(text, CONFIG)
     return torch.as_tensor(np.asarray(text), dtype=torch.long).view(1, -1)
 
 
@@ -178,9 +186,8 @@ class Synthesizer:
         if len(sens) == 0:
             sens = [text + "."]
         sens = [s.strip() for s in sens if len(s) >= 3]  # server/synthesizer.py:134-136
-        if self.input_adapter is None:
-            raise NotImplementedError("Synthesizer needs an input_adapter (text front-end is off the path)")
-        ids = [np.asarray(self.input_adapter(s)) for s in sens]
+        adapter = self.input_adapter or (lambda sen: text_to_seqvec(sen, self.tts_config))
+        ids = [np.asarray(adapter(s)) for s in sens]
         wavs = []
         if ids:
             outs, _ = synthesize_batch(self.tts_model, self.ap, ids, seed=self.seed, phase="numpy")
