@@ -65,6 +65,12 @@ def kernel_algorithmic(name, B, L, frames_total, r=1):
     return ("hbm", by[name])
 
 
+def decoder_step_algorithmic(B, L):
+    """algorithmic bytes of one decoder step at batch B (weights once per batch-step,
+    inputs + processed inputs, state / outputs) — 72.99 MB at B=1, L=100."""
+    return 4 * 18183458 + 4 * B * L * 640 + 4 * B * (3 * 1024 + 2 * 1024 + 512 + 80 + L)
+
+
 def kernel_algorithmic_gst(name, B, L, frames_total, r=5):
     """Algorithmic bytes per launch of the TacotronGST decoder-step kernels (weights once per batch
     step + per-sentence activations) and of the GL iteration."""
@@ -321,7 +327,10 @@ def main():
         Lmean = float(np.mean([len(x) for x in ids]))
         steps = max(out["steps"])
         frames_total = sum(out["frames"])
-        kd = model.profile_step_kernels(reps=50 if not gst else 20)
+        resident = (not gst) and model.last_timing.get("resident", False)
+        # resident batch-1 decoder: ONE launch runs every step (csrc/resident_decoder.hip), timed
+        # with HIP events on the library stream around that launch; otherwise the per-step kernels
+        kd = {} if resident else model.profile_step_kernels(reps=50 if not gst else 20)
         kg = ap.profile_gl_kernels(reps=20)
         launches = {k: steps for k in kd}
         # one GL iteration = overlap-add launch (frames -> float32 signal) + per-frame
@@ -332,6 +341,11 @@ def main():
             kind, alg = (kernel_algorithmic_gst if gst else kernel_algorithmic)(k, B, Lmean, frames_total)
             kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],
                               algorithmic_bytes=alg, achieved_gbs=alg / (ms * 1e-3) / 1e9 if ms > 0 else None)
+        if resident:
+            alg = decoder_step_algorithmic(B, Lmean) * steps
+            kernels["resident_decoder"] = dict(mean_ms=dec_ms, launches_per_step=1, ms_per_step=dec_ms,
+                                               decoder_steps=steps, us_per_decoder_step=1000 * dec_ms / steps,
+                                               algorithmic_bytes=alg, achieved_gbs=alg / (dec_ms * 1e-3) / 1e9)
         dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
         kdom = kernels[dom]
         traffic = load_traffic(("gst_" if gst else "") + dom)

@@ -113,6 +113,14 @@ tts_status tts_decoder_run_continue(tts_decoder* d, const float* enc, const int3
 /* Per-step timing of the last tts_decoder_run (ms of GPU time of the step loop, steps run). */
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run);
 
+/* Which implementation ran the last tts_decoder_run / _continue (no reference counterpart):
+ * *resident = 1 for the resident single-launch batch-1 decoder (every step weight held on chip
+ * by 256 workgroups, hand-offs in device memory), 0 for the per-step multi-launch hipGraph path.
+ * The resident path serves B = 1, L <= 256 under the synthesis attention configuration (forward
+ * attention + mask, sigmoid norm) on a GPU with >= 256 compute units; TTS_RESIDENT=0 in the
+ * environment at tts_decoder_create disables it. */
+tts_status tts_decoder_last_path(tts_decoder* d, int* resident);
+
 /* Measurement only (no reference counterpart): re-runs up to `reps` steps of the last
  * tts_decoder_run's batch eagerly, with a HIP event before/after every kernel on the stream it
  * is launched on, and returns the mean duration (ms) of each step kernel, in launch order:

@@ -13,6 +13,7 @@
 // The host synchronises only at chunk boundaries: the first chunk is the reference's lower
 // bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <tuple>
@@ -20,6 +21,7 @@
 #include <vector>
 
 #include "decoder.h"
+#include "resident.h"
 #include "sgemm.h"
 
 using namespace tts;
@@ -49,6 +51,11 @@ struct tts_decoder {
     float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
     float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr, *epart = nullptr;
     bool fast_attention = false;  // attention_uses_epart(): energies evaluated in the query launch
+    // resident (persistent, one launch per sentence) batch-1 decoder, resident.h
+    bool resident = false;
+    ResWeights rw{};
+    unsigned long long* gran = nullptr;  // [2][GR_TOTAL] granules, then int status[4]
+    long long res_ticks = 0;
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
@@ -59,6 +66,7 @@ struct tts_decoder {
     int last_steps = 0;
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
+    int last_resident = 0;    // the last run used the resident decoder
     InitArgs last_init{};
 };
 
@@ -318,8 +326,29 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         hipError_t _e = (x);                                             \
         if (_e != hipSuccess) return fail(hip_fail(_e, #x, __FILE__, __LINE__)); \
     } while (0)
+    {
+        AttnArgs probe{};
+        probe.attn_norm = cfg->attn_norm; probe.forward_attn = cfg->forward_attn; probe.trans_agent = cfg->trans_agent;
+        probe.forward_attn_mask = cfg->forward_attn_mask; probe.location_attn = cfg->location_attn;
+        probe.windowing = cfg->windowing;
+        probe.enc_dim = ENC;
+        d->fast_attention = attention_uses_epart(probe);
+    }
     // packed GEMM weights
     const int nfused = nmel + PRE + 1;
+    {
+        // the resident decoder needs one workgroup per CU on >= 256 CUs and fits the fused rows in
+        // two rows per CU; TTS_RESIDENT=0 disables it (multi-launch path for every batch)
+        const char* env = getenv("TTS_RESIDENT");
+        int dev = 0, ncu = 0, rate_khz = 0;
+        if (d->fast_attention && nfused < 2 * RES_CUS && !(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= RES_CUS &&
+            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0 &&
+            resident_prepare() == hipSuccess) {
+            d->resident = true;
+            d->res_ticks = (long long)rate_khz * 50;  // 50 ms per hand-off wait
+        }
+    }
     CK(dmalloc(d, &d->W_pre1, sgemm_packed_floats(PRE, nmel)));
     HK(sgemm_pack(pre0, nmel, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre1, s));
     CK(dmalloc(d, &d->W_pre2, sgemm_packed_floats(PRE, PRE)));
@@ -344,6 +373,23 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         if (e == hipSuccess) e = sgemm_pack(wf, HDEC + ENC, nullptr, 0, nfused, ROWMAP_IDENTITY, 0, d->W_melf, s);
         if (e == hipSuccess) e = dmalloc(d, &d->b_melf, (nfused + 15) / 16 * 16) ? hipErrorOutOfMemory : hipSuccess;
         if (e == hipSuccess) e = sgemm_pack_bias(bf, nullptr, nfused, ROWMAP_IDENTITY, 0, d->b_melf, s);
+        if (e == hipSuccess && d->resident) {
+            size_t nwa, nwdl, nwdc, nws;
+            resident_weight_floats(&nwa, &nwdl, &nwdc, &nws);
+            float *pa = nullptr, *pdl = nullptr, *pdc = nullptr, *pws = nullptr;
+            if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) || dmalloc(d, &pws, nws) ||
+                dmalloc(d, &d->rw.ba, RES_CUS * 16) || dmalloc(d, &d->rw.bd, RES_CUS * 16) ||
+                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
+                e = hipErrorOutOfMemory;
+            if (e == hipSuccess) {
+                d->rw.wa = reinterpret_cast<float4*>(pa);
+                d->rw.wdl = reinterpret_cast<float4*>(pdl);
+                d->rw.wdc = reinterpret_cast<float4*>(pdc);
+                d->rw.ws = reinterpret_cast<float4*>(pws);
+                ResSrc src{a_wih, a_whh, a_bih, a_bhh, d_wih, d_whh, d_bih, d_bhh, pre1, wq, wf, bf, nfused};
+                e = resident_pack(src, d->rw, s);
+            }
+        }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         (void)hipFree(wf);
         (void)hipFree(bf);
@@ -380,14 +426,6 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->pre1, (size_t)Bc * PRE));
     CK(dmalloc(d, &d->q, (size_t)Bc * ADIM));
     CK(dmalloc(d, &d->epart, (size_t)Bc * QE_TILES * Lc));
-    {
-        AttnArgs probe{};
-        probe.attn_norm = cfg->attn_norm; probe.forward_attn = cfg->forward_attn; probe.trans_agent = cfg->trans_agent;
-        probe.forward_attn_mask = cfg->forward_attn_mask; probe.location_attn = cfg->location_attn;
-        probe.windowing = cfg->windowing;
-        probe.enc_dim = ENC;
-        d->fast_attention = attention_uses_epart(probe);
-    }
     CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_cum, (size_t)Bc * Lc));
@@ -498,6 +536,35 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     }
     TTS_HIP(launch_decoder_init(ia, s));
     if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+    int run = 0;  // steps enqueued; the next step has parity run & 1
+    d->last_resident = 0;
+    if (d->resident && B == 1 && lens[0] <= RES_LMAX) {
+        d->last_resident = 1;
+        // one persistent launch runs every step (resident.h); same state / history buffers
+        ResArgs ra{};
+        ra.w = d->rw;
+        ra.L = lens[0]; ra.Lcap = d->Lcap; ra.nmel = d->nmel; ra.nrows = d->nmel + PRE + 1;
+        ra.max_steps = max_steps; ra.hist_cap = d->hist_cap; ra.Lalign = Lmax; ra.timeout_ticks = d->res_ticks;
+        ra.v = d->v; ra.v_b = d->v_b; ra.Pt = d->Pt; ra.enc = d->enc;
+        ra.h_att = d->h_att; ra.c_att = d->c_att; ra.h_dec = d->h_dec; ra.c_dec = d->c_dec; ra.xa = d->xa;
+        ra.hps = (int64_t)d->Bcap * HATT; ra.xps = (int64_t)d->Bcap * XA;
+        ra.pre1 = d->pre1; ra.alpha = d->alpha; ra.nidx = d->nidx; ra.u = d->u; ra.flag1 = d->flag1; ra.count = d->count;
+        ra.done = d->done; ra.n_steps = d->n_steps;
+        ra.mel_hist = d->mel_hist; ra.stop_hist = d->stop_hist; ra.align_hist = d->align_hist;
+        ra.gran = d->gran;
+        ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
+        TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
+        TTS_HIP(hipEventRecord(d->ev_t0, s));
+        TTS_HIP(launch_resident(ra, s));
+        TTS_HIP(hipEventRecord(d->ev_t1, s));
+        TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
+        TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        TTS_HIP(hipStreamSynchronize(s));
+        TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP,
+                  d->host_flags[0] == 100 ? "decoder did not stop within max_steps + 20 (internal error)"
+                                          : "resident decoder: a hand-off wait timed out (internal error)");
+        run = n_steps[0];
+    } else {
     auto key = std::make_tuple(B, Lmax, max_steps);
     auto it = d->graphs.find(key);
     if (it == d->graphs.end()) {
@@ -510,7 +577,6 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     }
     const Graphs& g = it->second;
     TTS_HIP(hipEventRecord(d->ev_t0, s));
-    int run = 0;  // steps enqueued; the next step has parity run & 1
     auto launch_steps = [&](int n) -> tts_status {
         while (n > 0) {
             if ((run & 1) == 0 && n >= CHUNK) {
@@ -539,6 +605,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     TTS_HIP(hipEventRecord(d->ev_t1, s));
     TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     TTS_HIP(hipStreamSynchronize(s));
+    }
     int nmax = 0;
     for (int b = 0; b < B; ++b) nmax = std::max(nmax, (int)n_steps[b]);
     const size_t nm = d->nmel;
@@ -572,6 +639,12 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
     TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
     *loop_ms = d->last_ms;
     *steps_run = d->last_steps;
+    return TTS_OK;
+}
+
+tts_status tts_decoder_last_path(tts_decoder* d, int* resident) {
+    TTS_CHECK(d && resident, TTS_ERR_INVALID, "null argument");
+    *resident = d->last_resident;
     return TTS_OK;
 }
 

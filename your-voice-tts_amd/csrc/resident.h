@@ -1,0 +1,88 @@
+// Resident (persistent) decoder for batch-1 synthesis: the whole decoder loop of
+// Decoder.inference (layers/tacotron2.py:249-285) as ONE launch whose 256 workgroups (one per
+// compute unit) keep every step weight on chip — 16 gate rows of both LSTMs per CU (the
+// attention LSTM's in VGPRs, the decoder LSTM's recurrent/attention half in LDS, its context
+// half in VGPRs) plus a prenet-2 row, a query row and up to two fused mel/prenet-1/stop rows.
+// A step then streams no weights at all; its cost is the six dependent hand-offs
+//   pre1 -> prenet2 -> h_att -> query -> [attention on one CU] -> ctx -> h_dec -> pre1
+// carried by 8-byte {tag, value} granules (agent-scope relaxed atomics, sc1: the hand-off form
+// that needs no fences, MI355X_MICROARCH.md "Valid forms").  Every wait is bounded: a wave
+// that does not see its data within the timeout flags an error and the grid drains.
+//
+// Scope: B = 1, the synthesis attention configuration (forward attention + eval mask,
+// sigmoid norm, no location / windowing / transition agent — attention_uses_epart()), L <= 256,
+// nmel + 257 <= 512 (r <= 3).  Reads its initial state from, and leaves its final state in,
+// the multi-launch path's buffers (same slots), so continuous mode and profiling interoperate.
+#pragma once
+#include "decoder.h"
+
+namespace tts {
+
+constexpr int RES_CUS = 256;
+constexpr int RES_THREADS = 512;
+constexpr int RES_WAVES = RES_THREADS / 64;
+constexpr int RES_LMAX = 256;
+constexpr int RES_ATT_CU = RES_CUS - 1;  // runs the attention step (no query row: CU >= 128)
+
+// granule slots (u64 {tag << 32 | float bits}) per step parity
+constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_PRE2 = 320, GR_HATT = 576, GR_Q = 1600, GR_CTX = 1728,
+              GR_TAIL = 2240, GR_HDEC = 2304, GR_TOTAL = 3328;
+
+struct ResWeights {
+    float4* wa;   // [256 CU][14 i4][512 thr]   attention LSTM rows over [prenet | ctx | h_att]
+    float4* wdl;  // [256 CU][16 i4][16 row][32 ks]  decoder LSTM rows over [h_att | h_dec] (LDS image)
+    float4* wdc;  // [256 CU][4 i4][512 thr]    decoder LSTM rows over ctx
+    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  wave 0 prenet-2 row, wave 1 query row, waves 2/3 fused rows
+    float* ba;    // [256][16] attention LSTM bias (b_ih + b_hh), logical row g*4 + u
+    float* bd;    // [256][16] decoder LSTM bias
+    float* bs;    // [256][2] fused-row biases (rows c, c + 256)
+};
+
+struct ResArgs {
+    ResWeights w;
+    int L, Lcap, nmel, nrows, max_steps, hist_cap, Lalign;
+    long long timeout_ticks;  // wall_clock64 ticks per wait
+    const float* v;
+    const float* v_b;
+    const float* Pt;   // [ADIM][Lcap] (sentence 0)
+    const float* enc;  // [Lcap][ENC]
+    // state, multi-launch layout (B = 1): step 0 reads slot 1 of h_att / h_dec and xa slot 0;
+    // the last step n-1 leaves h in slot (n-1)&1 and ctx in xa slot 1-((n-1)&1)
+    float* h_att;
+    float* c_att;
+    float* h_dec;
+    float* c_dec;
+    float* xa;
+    int64_t hps, xps;
+    float* pre1;  // relu(W1 mem): read at step 0, rewritten every step (next step's)
+    const float* alpha;
+    const int* nidx;
+    const float* u;
+    const int* flag1;
+    const int* count;
+    int* done;
+    int* n_steps;
+    float* mel_hist;
+    float* stop_hist;
+    float* align_hist;
+    unsigned long long* gran;  // [2][GR_TOTAL], zeroed before every launch
+    int* status;               // [0]: 0 ok, else the id of the wait that timed out
+};
+
+// Pack the reference-layout weights (device pointers) into ResWeights (allocated by the caller,
+// sizes from resident_weight_floats).
+struct ResSrc {
+    const float *a_wih, *a_whh, *a_bih, *a_bhh;  // attention_rnn [4096][768], [4096][1024]
+    const float *d_wih, *d_whh, *d_bih, *d_bhh;  // decoder_rnn [4096][1536], [4096][1024]
+    const float* w_pre2;                         // prenet layer 1 weight [256][256]
+    const float* w_q;                            // query_layer [128][1024]
+    const float *wf, *bf;                        // folded [nrows][1536] + [nrows]
+    int nrows;
+};
+void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc, size_t* ws);
+hipError_t resident_pack(const ResSrc& src, const ResWeights& w, hipStream_t s);
+size_t resident_smem_bytes();
+hipError_t resident_prepare();
+hipError_t launch_resident(const ResArgs& a, hipStream_t s);
+
+}  // namespace tts

@@ -1,0 +1,562 @@
+// Resident batch-1 decoder: one persistent launch for the whole decoder loop (see resident.h).
+//
+// Per step t on compute unit c (512 threads = 8 waves; thread (r = tid/32, ks = tid%32) owns
+// gate row r = g*4 + u of units 4c..4c+3 and the k-slice {i*128 + 4ks .. +4}):
+//   1. attention-LSTM partial over [ctx_{t-1} | h_att_{t-1}]            (all waves, VGPR weights)
+//   2. wave 0: wait pre1_t (+ continue flag), prenet-2 row c, publish; gather the 256 rows
+//   3. prenet part, row sums, LSTM cell of units 4c..4c+3, publish h_att_t   (tacotron2.py:195-197)
+//   4. gather h_att_t; 5. CUs < 128: query row c, publish                     (common_layers.py:179)
+//   6. decoder-LSTM partial over [h_att_t | h_dec_{t-1}]                  (LDS weights)
+//   7. CU 255: energies, sigmoid, forward attention + mask, context, publish ctx_t and the tail
+//      (common_layers.py:178-182, 199-223, 239-253)
+//   8. gather ctx_t; 9. context part, cell, publish h_dec_t               (tacotron2.py:206-208)
+//  10. gather h_dec_t; 11. waves 2/3: fused rows c, c+256 = [mel | prenet-1 of t+1 | stop]:
+//      mel -> history, prenet-1 -> publish, stop -> sigmoid + stop rule -> publish continue flag
+//      (tacotron2.py:214-224, 256-277)
+// Reductions keep fixed orders (bitwise run-to-run deterministic).
+#include "resident.h"
+
+namespace tts {
+namespace {
+
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef __attribute__((address_space(1))) int gint;
+
+constexpr int GW = 4;  // waves that sweep the 1024- and 512-granule vectors
+
+__device__ __forceinline__ void publish(u64* g, unsigned tag, float v) {
+    __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 peek(u64* g) {
+    return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fail(int* status, int code) {
+    __hip_atomic_store((gint*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals `tag`;
+// false after `tmo` wall-clock ticks (the caller flags the error, the grid drains).
+template <int N, typename F>
+__device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo) {
+    long long t_end = 0;
+    for (int spin = 0;; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int k = idx(i);
+            if (k >= 0) {
+                const u64 x = peek(g + k);
+                v[i] = __uint_as_float((unsigned)x);
+                ok = ok && (unsigned)(x >> 32) == tag;
+            }
+        }
+        if (__all(ok)) return true;
+        if (spin == 0) {
+            t_end = (long long)wall_clock64() + tmo;
+        } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
+    acc = fmaf(w.x, x.x, acc);
+    acc = fmaf(w.y, x.y, acc);
+    acc = fmaf(w.z, x.z, acc);
+    return fmaf(w.w, x.w, acc);
+}
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// sum over the 32 lanes of a half-wave (one gate row), butterfly: every lane gets the same value
+__device__ __forceinline__ float sum32(float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+constexpr int SM_WDL = 16 * 16 * 32 * 4;  // floats of the decoder-LSTM LDS weight image (128 KiB)
+constexpr int SM_ST = 64;                  // biases, cell states, stop-rule state
+constexpr int SM_RQ = 4 * 64 * 4;          // query row [4 i4][64 lanes] float4 | attention CU scratch
+constexpr int SM_RM = 2 * 6 * 64 * 4 + 2 * 256;  // fused rows [2][6][64] float4 | row 0 + energy partials
+constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 16 + SM_ST + SM_RQ + SM_RM;
+static_assert(SM_RM >= 6 * 64 * 4 + RES_WAVES * RES_LMAX, "attention CU partials");
+static_assert(SM_RQ >= 2 * RES_LMAX + 2 * RES_WAVES + ADIM, "attention CU scratch");
+
+__global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const ResArgs a) {
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = tid >> 5, ks = tid & 31;
+    extern __shared__ __align__(16) float sm[];
+    float4* wdl = reinterpret_cast<float4*>(sm);  // [16 i4][16 r][32 ks]
+    float* xh_att = sm + SM_WDL;
+    float* xh_dec = xh_att + HATT;
+    float* xctx = xh_dec + HDEC;  // [ENC] context, [ENC] = stop-rule tail
+    float* xpre = xctx + ENC + 16;
+    float* xq = xpre + PRE;
+    float* gates = xq + ADIM;  // [16]
+    int* flags = reinterpret_cast<int*>(gates + 16);  // [0] stop seen, [1] abort
+    float* st = gates + 32;    // [0,16) b_att, [16,32) b_dec (row g*4+u), [32,36) c_att, [36,40) c_dec,
+                               // [40,44) h_att, [44,48) h_dec of units 4c+u, [48,50) fused biases,
+                               // [50] flag1, [51] count (int bits, stop lane)
+    float* rq = st + SM_ST;    // query row (CUs < 128) | attention CU: aold, an, scr, v
+    float* rm = rq + SM_RQ;    // fused rows c, c+256 | attention CU: row c + energy partials
+    float* aold = rq;
+    float* an = aold + RES_LMAX;
+    float* scr = an + RES_LMAX;
+    float* xv = scr + 2 * RES_WAVES;
+    float* red = rm + 6 * 64 * 4;  // [RES_WAVES][RES_LMAX]
+
+    // ---- weights (loaded once per call) and initial state
+    float4 wa[14], wdc[4], wp;
+    // per-wave small rows (wave 0 prenet-2 in VGPRs; wave 1 query and waves 2/3 fused rows in LDS)
+    const float4* wsp = a.w.ws + ((size_t)c * RES_WAVES + wave) * 6 * 64 + lane;
+    {
+        const float4* p = a.w.wa + (size_t)c * 14 * RES_THREADS + tid;
+#pragma unroll
+        for (int i = 0; i < 14; ++i) wa[i] = p[(size_t)i * RES_THREADS];
+        const float4* q = a.w.wdc + (size_t)c * 4 * RES_THREADS + tid;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) wdc[i] = q[(size_t)i * RES_THREADS];
+        wp = wsp[0];
+        if (wave == 1 && c < ADIM)
+            for (int i = 0; i < 4; ++i) reinterpret_cast<float4*>(rq)[i * 64 + lane] = wsp[i * 64];
+        if ((wave == 2 || wave == 3) && (c + 256 * (wave - 2)) < a.nrows)
+            for (int i = 0; i < 6; ++i) reinterpret_cast<float4*>(rm)[((wave - 2) * 6 + i) * 64 + lane] = wsp[i * 64];
+        const float4* l = a.w.wdl + (size_t)c * (SM_WDL / 4);
+        for (int i = tid; i < SM_WDL / 4; i += RES_THREADS) wdl[i] = l[i];
+    }
+    if (tid < 16) {
+        st[tid] = a.w.ba[c * 16 + tid];
+        st[16 + tid] = a.w.bd[c * 16 + tid];
+    }
+    if (tid < 4) {
+        st[32 + tid] = a.c_att[4 * c + tid];
+        st[36 + tid] = a.c_dec[4 * c + tid];
+    }
+    if (tid < 2) st[48 + tid] = a.w.bs[c * 2 + tid];
+    for (int k = tid; k < HATT; k += RES_THREADS) {
+        xh_att[k] = a.h_att[a.hps + k];  // step 0 reads slot 1 (decoder_init_kernel)
+        xh_dec[k] = a.h_dec[a.hps + k];
+    }
+    for (int k = tid; k < ENC; k += RES_THREADS) xctx[k] = a.xa[PRE + k];
+    const int L = a.L;
+    const bool att_cu = c == RES_ATT_CU;
+    int n = 0;
+    float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f};
+    auto prefetch_rows = [&](int nn) {
+        // the rows the context can use after the mask: (nn-2) mod L and [nn-1, nn+2]
+        const int cx = (nn - 2 + L) % L, clo = nn >= 1 ? nn - 1 : L - 1, chi = min(nn + 2, L - 1);
+        ex = a.enc[(int64_t)cx * ENC + tid];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) erow[k] = clo + k <= chi ? a.enc[(int64_t)(clo + k) * ENC + tid] : 0.f;
+    };
+    if (att_cu) {
+        n = a.nidx[0];
+        ufa = a.u[0];
+        vb = a.v_b[0];
+        for (int j = tid; j < L; j += RES_THREADS) aold[j] = a.alpha[j];
+        if (tid < ADIM) xv[tid] = a.v[tid];
+        prefetch_rows(n);
+    }
+    const int srow = a.nmel + PRE;  // the stop row of the fused GEMM
+    const bool stop_lane = c == (srow & 255) && wave == 2 + (srow >> 8) && lane == 0;
+    if (stop_lane) {
+        reinterpret_cast<int*>(st)[50] = a.flag1[0];
+        reinterpret_cast<int*>(st)[51] = a.count[0];
+    }
+    if (tid == 0) {
+        flags[0] = 0;
+        flags[1] = 0;
+    }
+    __syncthreads();
+
+    const long long tmo = a.timeout_ticks;
+    int t = 0;
+    for (;; ++t) {
+        u64* G = a.gran + (t & 1) * GR_TOTAL;          // this step's granules
+        u64* Gp = a.gran + ((t & 1) ^ 1) * GR_TOTAL;   // the previous step's (pre1, continue flag)
+        const unsigned E = (unsigned)t * 8u;           // tags E+1 .. E+6, never 0
+        // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}]
+        float acc_a = 0.f;
+#pragma unroll
+        for (int i = 2; i < 6; ++i) acc_a = dot4(wa[i], ld4(xctx + (i - 2) * 128 + ks * 4), acc_a);
+#pragma unroll
+        for (int i = 6; i < 10; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
+        asm volatile("" ::: "memory");  // bound the hoisted LDS loads (register pressure)
+#pragma unroll
+        for (int i = 10; i < 14; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
+        // 2) prenet layer 2 (wave 0)
+        if (wave == 0) {
+            float p[5];
+            bool ok = true;
+            if (t == 0) {
+                const float4 v = ld4(a.pre1 + lane * 4);  // go frame's layer 1 (enqueue_prenet_go)
+                p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w; p[4] = 1.f;
+            } else {
+                ok = sweep<5>(Gp, E - 2, p, [&](int i) { return i < 4 ? GR_PRE1 + lane * 4 + i : GR_CTRL; }, tmo);
+            }
+            const bool go = p[4] != 0.f;
+            if (ok && go) {
+                float s = dot4(wp, float4{p[0], p[1], p[2], p[3]}, 0.f);
+                s = wave_sum(s);
+                if (lane == 0) publish(G + GR_PRE2 + c, E + 1, fmaxf(s, 0.f));
+                float q4[4];
+                ok = sweep<4>(G, E + 1, q4, [&](int i) { return GR_PRE2 + lane * 4 + i; }, tmo);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xpre[lane * 4 + i] = q4[i];
+            }
+            if (lane == 0) {
+                if (!ok) { flags[1] = 1; fail(a.status, 1); }
+                if (ok && !go) flags[0] = 1;
+            }
+        }
+        __syncthreads();  // B1
+        if (flags[0] | flags[1]) break;
+        // 3) prenet part, cell
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc_a = dot4(wa[i], ld4(xpre + i * 128 + ks * 4), acc_a);
+        acc_a = sum32(acc_a);
+        if (ks == 0) gates[r] = acc_a;
+        __syncthreads();  // B2
+        if (tid < 4) {
+            const float gi = gates[tid] + st[tid], gf = gates[4 + tid] + st[4 + tid];
+            const float gg = gates[8 + tid] + st[8 + tid], go = gates[12 + tid] + st[12 + tid];
+            const float c2 = sigmoidf_(gf) * st[32 + tid] + sigmoidf_(gi) * tanhf(gg);
+            const float h = sigmoidf_(go) * tanhf(c2);
+            st[32 + tid] = c2;
+            st[40 + tid] = h;
+            publish(G + GR_HATT + 4 * c + tid, E + 2, h);
+        }
+        // 4) gather h_att_t
+        if (wave < GW) {
+            float v4[4];
+            const bool ok = sweep<4>(G, E + 2, v4, [&](int i) { return GR_HATT + wave * 256 + i * 64 + lane; }, tmo);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xh_att[wave * 256 + i * 64 + lane] = v4[i];
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2); }
+        }
+        __syncthreads();  // B3
+        if (flags[1]) break;
+        // 5) query row
+        if (wave == 1 && c < ADIM) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                s = dot4(reinterpret_cast<const float4*>(rq)[i * 64 + lane], ld4(xh_att + i * 256 + lane * 4), s);
+            s = wave_sum(s);
+            if (lane == 0) publish(G + GR_Q + c, E + 3, s);
+        }
+        // 6) decoder LSTM over [h_att_t | h_dec_{t-1}]
+        float acc_d = 0.f;
+#pragma unroll 2
+        for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
+#pragma unroll 2
+        for (int i = 8; i < 16; ++i)
+            acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
+        // 7) attention step
+        if (att_cu) {
+            // processed inputs of this wave's 16 dims at positions lane, lane + 64 (in flight
+            // while the query arrives)
+            float pt[2][16];
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int dd = 0; dd < 16; ++dd) {
+                    const int jj = p * 64 + lane;
+                    pt[p][dd] = jj < L ? a.Pt[(int64_t)(16 * wave + dd) * a.Lcap + jj] : 0.f;
+                }
+            if (wave == 0) {
+                float q2[2];
+                const bool ok = sweep<2>(G, E + 3, q2, [&](int i) { return GR_Q + i * 64 + lane; }, tmo);
+                xq[lane] = q2[0];
+                xq[64 + lane] = q2[1];
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3); }
+            }
+            __syncthreads();  // A1
+            if (flags[1]) break;
+            // energy partials over this wave's 16 attention dims (query_energy_kernel's split);
+            // positions >= 128 read P from global memory (L2-resident across steps)
+            float xqd[16];
+#pragma unroll
+            for (int dd = 0; dd < 16; ++dd) xqd[dd] = xq[16 * wave + dd];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int jj = p * 64 + lane;
+                if (jj < L) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int dd = 0; dd < 16; ++dd) s += xv[16 * wave + dd] * tanh_fast(xqd[dd] + pt[p][dd]);
+                    red[wave * RES_LMAX + jj] = s;
+                }
+            }
+#pragma unroll 1
+            for (int jj = 128 + lane; jj < L; jj += 64) {
+                float s = 0.f;
+#pragma unroll
+                for (int dd = 0; dd < 16; ++dd) {
+                    const int d = 16 * wave + dd;
+                    s += xv[d] * tanh_fast(xqd[dd] + a.Pt[(int64_t)d * a.Lcap + jj]);
+                }
+                red[wave * RES_LMAX + jj] = s;
+            }
+            __syncthreads();  // A2
+            const int j = tid;
+            const bool in = j < L;
+            const int cx = (n - 2 + L) % L, clo = n >= 1 ? n - 1 : L - 1, chi = min(n + 2, L - 1);
+            float anj = 0.f;
+            if (in) {
+                float e = 0.f;
+#pragma unroll
+                for (int w = 0; w < RES_WAVES; ++w) e += red[w * RES_LMAX + j];
+                const float sg = sigmoidf_(e + vb);
+                const float prev = j > 0 ? aold[j - 1] : 0.f;
+                const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, aold[j]), __fmul_rn(ufa, prev)), 1e-8f);
+                anj = __fmul_rn(mix, sg);
+                an[j] = anj;
+            }
+            const bool win = in && j >= clo && j <= chi && j != cx;
+            const float wsum = wave_sum_dpp(win ? anj : 0.f);
+            const float wmax = wave_max_dpp(in ? anj : -INFINITY);
+            if (lane == 0) {
+                scr[2 * wave] = wsum;
+                scr[2 * wave + 1] = wmax;
+            }
+            __syncthreads();  // A3
+            float rs = 0.f, rm = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < RES_WAVES; ++k) {
+                rs += scr[2 * k];
+                rm = fmaxf(rm, scr[2 * k + 1]);
+            }
+            const float vx = 0.01f * rm;  // alpha[n-2] = 0.01 * val
+            const float denom = rs + vx;
+            auto weight = [&](int p) -> float {
+                if (p == cx) return vx / denom;
+                return (p >= clo && p <= chi) ? an[p] / denom : 0.f;
+            };
+            const float w = in ? weight(j) : 0.f;
+            if (t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
+            const float tail = weight(L - 2) + weight(L - 1);  // tacotron2.py:268
+            float bv = 0.f;
+            int bi = -1;
+            auto consider = [&](int p) {
+                const float wp = weight(p);
+                if (p <= L - 2 && wp > bv) { bv = wp; bi = p; }
+            };
+            if (cx < clo) consider(cx);
+            for (int p = clo; p <= chi; ++p) consider(p);
+            if (cx > chi) consider(cx);
+            float ctx = 0.f;
+            if (cx < clo) ctx += weight(cx) * ex;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (clo + k <= chi) ctx += weight(clo + k) * (clo + k == cx ? ex : erow[k]);
+            if (cx > chi) ctx += weight(cx) * ex;
+            publish(G + GR_CTX + tid, E + 4, ctx);
+            if (tid == 0) publish(G + GR_TAIL, E + 4, tail);
+            __syncthreads();  // A4: aold / an reads done
+            if (in) aold[j] = w;
+            n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step
+            prefetch_rows(n);
+        }
+        // 8) gather ctx_t and the tail
+        if (wave < GW) {
+            float v3[3];
+            const bool ok = sweep<3>(G, E + 4, v3, [&](int i) {
+                return i < 2 ? GR_CTX + wave * 128 + i * 64 + lane : (wave == 0 && lane == 0 ? GR_TAIL : -1);
+            }, tmo);
+            xctx[wave * 128 + lane] = v3[0];
+            xctx[wave * 128 + 64 + lane] = v3[1];
+            if (wave == 0 && lane == 0) xctx[ENC] = v3[2];
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4); }
+        }
+        __syncthreads();  // B4
+        if (flags[1]) break;
+        // 9) context part, cell
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc_d = dot4(wdc[i], ld4(xctx + i * 128 + ks * 4), acc_d);
+        acc_d = sum32(acc_d);
+        if (ks == 0) gates[r] = acc_d;
+        __syncthreads();  // B5
+        if (tid < 4) {
+            const float gi = gates[tid] + st[16 + tid], gf = gates[4 + tid] + st[20 + tid];
+            const float gg = gates[8 + tid] + st[24 + tid], go = gates[12 + tid] + st[28 + tid];
+            const float c2 = sigmoidf_(gf) * st[36 + tid] + sigmoidf_(gi) * tanhf(gg);
+            const float h = sigmoidf_(go) * tanhf(c2);
+            st[36 + tid] = c2;
+            st[44 + tid] = h;
+            publish(G + GR_HDEC + 4 * c + tid, E + 5, h);
+        }
+        // 10) gather h_dec_t
+        if (wave < GW) {
+            float v4[4];
+            const bool ok = sweep<4>(G, E + 5, v4, [&](int i) { return GR_HDEC + wave * 256 + i * 64 + lane; }, tmo);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xh_dec[wave * 256 + i * 64 + lane] = v4[i];
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5); }
+        }
+        __syncthreads();  // B6
+        if (flags[1]) break;
+        // 11) fused rows [mel | prenet-1 of step t+1 | stop]
+        if (wave == 2 || wave == 3) {
+            const int row = c + 256 * (wave - 2);
+            if (row < a.nrows) {
+                float s = 0.f;
+                const float4* wm = reinterpret_cast<const float4*>(rm) + (wave - 2) * 6 * 64 + lane;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s = dot4(wm[i * 64], ld4(xh_dec + i * 256 + lane * 4), s);
+#pragma unroll
+                for (int i = 4; i < 6; ++i) s = dot4(wm[i * 64], ld4(xctx + (i - 4) * 256 + lane * 4), s);
+                s = wave_sum(s);
+                const float v = s + st[48 + wave - 2];
+                if (lane == 0) {
+                    if (row < a.nmel) {
+                        if (t < a.hist_cap) a.mel_hist[(int64_t)t * a.nmel + row] = v;
+                    } else if (row < a.nmel + PRE) {
+                        const float p = fmaxf(v, 0.f);
+                        a.pre1[row - a.nmel] = p;
+                        publish(G + GR_PRE1 + row - a.nmel, E + 6, p);
+                    } else {
+                        // stopnet + stop rule (tacotron2.py:219-224, 257-277), as EPI_MEL_FUSED rule 0
+                        const float stv = sigmoidf_(v);
+                        if (t < a.hist_cap) a.stop_hist[t] = stv;
+                        const float tail = xctx[ENC];
+                        int* sst = reinterpret_cast<int*>(st);
+                        const int f1 = sst[50] | ((tail > 0.8f && t > L) ? 1 : 0);
+                        sst[50] = f1;
+                        int nd = 0;
+                        if (f1 && t > 2 * L) {
+                            sst[51] += 1;
+                            if (sst[51] > 20) nd = 1;
+                        } else if (t + 1 == a.max_steps) {
+                            nd = 1;
+                        }
+                        if (!nd && t + 1 >= a.hist_cap) {  // cannot happen: the rule stops by max_steps + 20
+                            nd = 1;
+                            fail(a.status, 100);
+                        }
+                        if (nd) {
+                            a.done[0] = 1;
+                            a.n_steps[0] = t + 1;
+                        }
+                        publish(G + GR_CTRL, E + 6, nd ? 0.f : 1.f);
+                    }
+                }
+            }
+        }
+    }
+    if (flags[1]) return;
+    // the last step t-1 leaves its state where the multi-launch path's would be
+    const int pl = (t - 1) & 1;
+    if (tid < 4) {
+        a.h_att[pl * a.hps + 4 * c + tid] = st[40 + tid];
+        a.c_att[4 * c + tid] = st[32 + tid];
+        a.h_dec[pl * a.hps + 4 * c + tid] = st[44 + tid];
+        a.c_dec[4 * c + tid] = st[36 + tid];
+    }
+    if (c == 0)
+        for (int k = tid; k < ENC; k += RES_THREADS) a.xa[(1 - pl) * a.xps + PRE + k] = xctx[k];
+}
+
+// ---- weight packing (once, at tts_decoder_create)
+__global__ void res_pack_wa(const float* wih, const float* whh, float4* out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)RES_CUS * 14 * RES_THREADS) return;
+    const int tid = idx % RES_THREADS, i4 = (idx / RES_THREADS) % 14, c = idx / (14 * RES_THREADS);
+    const int r = tid >> 5, ks = tid & 31, row = (r >> 2) * HATT + 4 * c + (r & 3);
+    float v[4];
+    for (int j = 0; j < 4; ++j) {
+        const int k = i4 * 128 + ks * 4 + j;  // over [prenet 256 | ctx 512 | h_att 1024]
+        v[j] = k < XA ? wih[(int64_t)row * XA + k] : whh[(int64_t)row * HATT + (k - XA)];
+    }
+    out[idx] = float4{v[0], v[1], v[2], v[3]};
+}
+__global__ void res_pack_wd(const float* wih, const float* whh, float4* wdl, float4* wdc) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int PER = 16 * 16 * 32 + 4 * RES_THREADS;  // float4 per CU: LDS image + ctx part
+    if (idx >= (int64_t)RES_CUS * PER) return;
+    const int c = idx / PER, e = idx % PER;
+    float v[4];
+    if (e < 16 * 16 * 32) {
+        const int i4 = e / 512, r = (e / 32) % 16, ks = e % 32;
+        const int row = (r >> 2) * HDEC + 4 * c + (r & 3);
+        for (int j = 0; j < 4; ++j) {
+            const int k = i4 * 128 + ks * 4 + j;  // over [h_att 1024 | h_dec 1024]
+            v[j] = k < HATT ? wih[(int64_t)row * (HATT + ENC) + k] : whh[(int64_t)row * HDEC + (k - HATT)];
+        }
+        wdl[(int64_t)c * 8192 + e] = float4{v[0], v[1], v[2], v[3]};
+    } else {
+        const int f = e - 16 * 16 * 32, i4 = f / RES_THREADS, tid = f % RES_THREADS;
+        const int r = tid >> 5, ks = tid & 31, row = (r >> 2) * HDEC + 4 * c + (r & 3);
+        for (int j = 0; j < 4; ++j) v[j] = wih[(int64_t)row * (HATT + ENC) + HATT + i4 * 128 + ks * 4 + j];
+        wdc[((int64_t)c * 4 + i4) * RES_THREADS + tid] = float4{v[0], v[1], v[2], v[3]};
+    }
+}
+__global__ void res_pack_ws(const float* w2, const float* wq, const float* wf, int nrows, float4* out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)RES_CUS * RES_WAVES * 6 * 64) return;
+    const int lane = idx % 64, i4 = (idx / 64) % 6, w = (idx / 384) % RES_WAVES, c = idx / (384 * RES_WAVES);
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+        if (w == 0 && i4 == 0) v[j] = w2[(int64_t)c * PRE + lane * 4 + j];
+        else if (w == 1 && c < ADIM && i4 < 4) v[j] = wq[(int64_t)c * HATT + i4 * 256 + lane * 4 + j];
+        else if (w == 2 || w == 3) {
+            const int row = c + 256 * (w - 2);
+            if (row < nrows) v[j] = wf[(int64_t)row * (HDEC + ENC) + i4 * 256 + lane * 4 + j];
+        }
+    }
+    out[idx] = float4{v[0], v[1], v[2], v[3]};
+}
+__global__ void res_pack_bias(const float* abih, const float* abhh, const float* dbih, const float* dbhh,
+                              const float* bf, int nrows, float* ba, float* bd, float* bs) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < RES_CUS * 16) {
+        const int c = idx / 16, r = idx % 16, row = (r >> 2) * HATT + 4 * c + (r & 3);
+        ba[idx] = abih[row] + abhh[row];
+        bd[idx] = dbih[row] + dbhh[row];
+    }
+    if (idx < RES_CUS * 2) {
+        const int row = idx / 2 + 256 * (idx % 2);
+        bs[idx] = row < nrows ? bf[row] : 0.f;
+    }
+}
+
+}  // namespace
+
+void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc, size_t* ws) {
+    *wa = (size_t)RES_CUS * 14 * RES_THREADS * 4;
+    *wdl = (size_t)RES_CUS * 16 * 16 * 32 * 4;
+    *wdc = (size_t)RES_CUS * 4 * RES_THREADS * 4;
+    *ws = (size_t)RES_CUS * RES_WAVES * 6 * 64 * 4;
+}
+
+hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
+    auto blocks = [](int64_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    hipLaunchKernelGGL(res_pack_wa, blocks((int64_t)RES_CUS * 14 * RES_THREADS), dim3(256), 0, st, s.a_wih, s.a_whh,
+                       w.wa);
+    hipLaunchKernelGGL(res_pack_wd, blocks((int64_t)RES_CUS * (8192 + 4 * RES_THREADS)), dim3(256), 0, st, s.d_wih,
+                       s.d_whh, w.wdl, w.wdc);
+    hipLaunchKernelGGL(res_pack_ws, blocks((int64_t)RES_CUS * RES_WAVES * 6 * 64), dim3(256), 0, st, s.w_pre2, s.w_q,
+                       s.wf, s.nrows, w.ws);
+    hipLaunchKernelGGL(res_pack_bias, blocks(RES_CUS * 16), dim3(256), 0, st, s.a_bih, s.a_bhh, s.d_bih, s.d_bhh, s.bf,
+                       s.nrows, w.ba, w.bd, w.bs);
+    return hipGetLastError();
+}
+
+size_t resident_smem_bytes() { return (size_t)SM_FLOATS * sizeof(float); }
+
+hipError_t resident_prepare() {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
+}
+
+hipError_t launch_resident(const ResArgs& a, hipStream_t s) {
+    if (a.L < 2 || a.L > RES_LMAX || a.nrows >= 2 * RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(resident_decoder_kernel, dim3(RES_CUS), dim3(RES_THREADS), resident_smem_bytes(), s, a);
+    return hipGetLastError();
+}
+
+}  // namespace tts

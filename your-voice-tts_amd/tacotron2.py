@@ -239,7 +239,9 @@ class Tacotron2:
         ms = ctypes.c_float()
         ns = ctypes.c_int()
         lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
-        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value)
+        res = ctypes.c_int()
+        lib.tts_decoder_last_path(hdec, ctypes.byref(res))
+        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value))
         self.last_lengths = frames
         return dict(mel=mel[:, :T], mel_post=mel_post[:, :T], align=align[:, :S], stop=stop[:, :S],
                     frames=frames, steps=steps, lens=lens)
