@@ -345,7 +345,8 @@ def main():
             alg = decoder_step_algorithmic(B, Lmean) * steps
             kernels["resident_decoder"] = dict(mean_ms=dec_ms, launches_per_step=1, ms_per_step=dec_ms,
                                                decoder_steps=steps, us_per_decoder_step=1000 * dec_ms / steps,
-                                               algorithmic_bytes=alg, achieved_gbs=alg / (dec_ms * 1e-3) / 1e9)
+                                               algorithmic_bytes=alg, achieved_gbs=alg / (dec_ms * 1e-3) / 1e9,
+                                               phases_us_per_step=model.profile_resident_phases())
         dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
         kdom = kernels[dom]
         traffic = load_traffic(("gst_" if gst else "") + dom)

@@ -121,6 +121,17 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
  * environment at tts_decoder_create disables it. */
 tts_status tts_decoder_last_path(tts_decoder* d, int* resident);
 
+/* Measurement only: re-runs the last resident batch-1 sentence with phase timers and returns the
+ * mean microseconds per decoder step of each phase, us[0..15] on compute unit 0 and us[16..31] on
+ * the attention compute unit (n >= 32): 0 attention-LSTM early part + wait pre1, 1 prenet-2 row
+ * (0-1 on the prenet compute units), 2 wait prenet-2, 3 attention-LSTM prenet part, 4 cell + gather
+ * h_att, 5 query row + decoder-LSTM early part, 6 wait query, 7 energies + max(alpha), 8 weights,
+ * context, publish, 9 next-step prefetch (6-9 attention CU only), 10 wait context, 11 decoder-LSTM
+ * context part, 12 cell + gather h_dec, 13 fused mel / prenet-1 / stop rows (wave 2); 14 and 15 split
+ * 7 and 8 (candidate energies up to their barrier; window weights + context before publishing). */
+#define TTS_RESIDENT_PHASES 16
+tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n);
+
 /* Measurement only (no reference counterpart): re-runs up to `reps` steps of the last
  * tts_decoder_run's batch eagerly, with a HIP event before/after every kernel on the stream it
  * is launched on, and returns the mean duration (ms) of each step kernel, in launch order:

@@ -31,6 +31,7 @@ LABELS = [
     (r"preemph_scan_kernel", "preemph"),
     (r"gl_ola_kernel", "gl_ola"),
     (r"project_inputs_kernel", "project_inputs"),
+    (r"resident_decoder_kernel", "resident_decoder"),
 ]
 
 

@@ -23,7 +23,7 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 EXPORTS = (
     "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue",
-    "tts_decoder_last_timing", "tts_decoder_last_path",
+    "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
@@ -81,6 +81,7 @@ def _declare(lib):
     lib.tts_decoder_run_continue.argtypes = lib.tts_decoder_run.argtypes
     lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_decoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_decoder_resident_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     lib.tts_postnet_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
     lib.tts_postnet_destroy.argtypes = [vp]
     lib.tts_postnet_destroy.restype = None

@@ -56,6 +56,7 @@ struct tts_decoder {
     ResWeights rw{};
     unsigned long long* gran = nullptr;  // [2][GR_TOTAL] granules, then int status[4]
     long long res_ticks = 0;
+    unsigned res_salt = 0;
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
@@ -67,6 +68,7 @@ struct tts_decoder {
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
     int last_resident = 0;    // the last run used the resident decoder
+    ResArgs last_ra{};
     InitArgs last_init{};
 };
 
@@ -379,7 +381,8 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
             float *pa = nullptr, *pdl = nullptr, *pdc = nullptr, *pws = nullptr;
             if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) || dmalloc(d, &pws, nws) ||
                 dmalloc(d, &d->rw.ba, RES_CUS * 16) || dmalloc(d, &d->rw.bd, RES_CUS * 16) ||
-                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
+                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) ||
+                dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
                 e = hipErrorOutOfMemory;
             if (e == hipSuccess) {
                 d->rw.wa = reinterpret_cast<float4*>(pa);
@@ -538,8 +541,8 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
     int run = 0;  // steps enqueued; the next step has parity run & 1
     d->last_resident = 0;
+    bool res_done = false;
     if (d->resident && B == 1 && lens[0] <= RES_LMAX) {
-        d->last_resident = 1;
         // one persistent launch runs every step (resident.h); same state / history buffers
         ResArgs ra{};
         ra.w = d->rw;
@@ -553,6 +556,9 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.mel_hist = d->mel_hist; ra.stop_hist = d->stop_hist; ra.align_hist = d->align_hist;
         ra.gran = d->gran;
         ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
+        d->res_salt = (d->res_salt + 1) & 0x3FFFF;
+        ra.salt = d->res_salt;
+        d->last_ra = ra;
         TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
         TTS_HIP(hipEventRecord(d->ev_t0, s));
         TTS_HIP(launch_resident(ra, s));
@@ -560,11 +566,22 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
         TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
         TTS_HIP(hipStreamSynchronize(s));
-        TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP,
-                  d->host_flags[0] == 100 ? "decoder did not stop within max_steps + 20 (internal error)"
-                                          : "resident decoder: a hand-off wait timed out (internal error)");
-        run = n_steps[0];
-    } else {
+        if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
+            // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
+            // stopped before touching any state; use the multi-launch path from now on
+            d->resident = false;
+            TTS_HIP(launch_decoder_init(ia, s));
+            if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+        } else {
+            TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP,
+                      d->host_flags[0] == 100 ? "decoder did not stop within max_steps + 20 (internal error)"
+                                              : "resident decoder: a hand-off wait timed out (internal error)");
+            run = n_steps[0];
+            res_done = true;
+            d->last_resident = 1;
+        }
+    }
+    if (!res_done) {
     auto key = std::make_tuple(B, Lmax, max_steps);
     auto it = d->graphs.find(key);
     if (it == d->graphs.end()) {
@@ -645,6 +662,36 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
 tts_status tts_decoder_last_path(tts_decoder* d, int* resident) {
     TTS_CHECK(d && resident, TTS_ERR_INVALID, "null argument");
     *resident = d->last_resident;
+    return TTS_OK;
+}
+
+tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n) {
+    TTS_CHECK(d && us && n >= 2 * RES_PHASES, TTS_ERR_INVALID, "bad arguments");
+    TTS_CHECK(d->last_resident && d->last_steps > 0, TTS_ERR_INVALID,
+              "tts_decoder_resident_phases needs a previous resident tts_decoder_run");
+    hipStream_t s = d->stream;
+    long long* prof = nullptr;
+    TTS_HIP(hipMalloc(&prof, sizeof(long long) * 2 * RES_PHASES));
+    TTS_HIP(hipMemsetAsync(prof, 0, sizeof(long long) * 2 * RES_PHASES, s));
+    TTS_HIP(launch_decoder_init(d->last_init, s));
+    tts_status st = enqueue_prenet_go(d, 1, s);
+    ResArgs ra = d->last_ra;
+    ra.prof = prof;
+    if (!st) {
+        TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
+        TTS_HIP(launch_resident(ra, s));
+    }
+    long long h[2 * RES_PHASES];
+    TTS_HIP(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipStreamSynchronize(s));
+    (void)hipFree(prof);
+    if (st) return st;
+    TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP, "resident decoder: a hand-off wait timed out (internal error)");
+    int dev = 0, rate_khz = 1;
+    TTS_HIP(hipGetDevice(&dev));
+    TTS_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));
+    for (int i = 0; i < 2 * RES_PHASES; ++i) us[i] = (float)(1e3 * (double)h[i] / rate_khz / d->last_steps);
     return TTS_OK;
 }
 

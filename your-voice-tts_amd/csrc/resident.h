@@ -25,23 +25,29 @@ constexpr int RES_LMAX = 256;
 constexpr int RES_ATT_CU = RES_CUS - 1;  // runs the attention step (no query row: CU >= 128)
 
 // granule slots (u64 {tag << 32 | float bits}) per step parity
-constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_PRE2 = 320, GR_HATT = 576, GR_Q = 1600, GR_CTX = 1728,
-              GR_TAIL = 2240, GR_HDEC = 2304, GR_TOTAL = 3328;
+// (GR_PRE2X: per-XCD prenet-2 vectors, [8 XCDs][256], written and read inside one XCD; GR_SETUP:
+// each CU's XCD id, parity 0 only)
+constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_HATT = 576, GR_Q = 1600, GR_CTX = 1728, GR_TAIL = 2240,
+              GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376, GR_TOTAL = 5632;
+constexpr int RES_MIN_CUS_PER_XCD = 16;  // prenet-2 rows per CU <= 16 (two per wave)
+constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
 
 struct ResWeights {
     float4* wa;   // [256 CU][14 i4][512 thr]   attention LSTM rows over [prenet | ctx | h_att]
     float4* wdl;  // [256 CU][16 i4][16 row][32 ks]  decoder LSTM rows over [h_att | h_dec] (LDS image)
     float4* wdc;  // [256 CU][4 i4][512 thr]    decoder LSTM rows over ctx
-    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  wave 0 prenet-2 row, wave 1 query row, waves 2/3 fused rows
+    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  wave 1 query row, waves 2/3 fused rows
     float* ba;    // [256][16] attention LSTM bias (b_ih + b_hh), logical row g*4 + u
     float* bd;    // [256][16] decoder LSTM bias
     float* bs;    // [256][2] fused-row biases (rows c, c + 256)
+    float* w2;    // prenet layer-2 weight, reference layout [256][256] (rows picked per XCD rank)
 };
 
 struct ResArgs {
     ResWeights w;
     int L, Lcap, nmel, nrows, max_steps, hist_cap, Lalign;
     long long timeout_ticks;  // wall_clock64 ticks per wait
+    unsigned salt;            // per-launch tag salt (18 bits): no granule of an earlier launch matches
     const float* v;
     const float* v_b;
     const float* Pt;   // [ADIM][Lcap] (sentence 0)
@@ -67,7 +73,10 @@ struct ResArgs {
     float* align_hist;
     unsigned long long* gran;  // [2][GR_TOTAL], zeroed before every launch
     int* status;               // [0]: 0 ok, else the id of the wait that timed out
+    long long* prof;           // null, or [2][RES_PHASES] wall-clock ticks summed over steps per phase
+                               // (CU 0, attention CU) — measurement only
 };
+constexpr int RES_PHASES = 16;
 
 // Pack the reference-layout weights (device pointers) into ResWeights (allocated by the caller,
 // sizes from resident_weight_floats).

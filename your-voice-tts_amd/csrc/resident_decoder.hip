@@ -23,11 +23,23 @@ typedef unsigned long long u64;
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) int gint;
 
-constexpr int GW = 4;  // waves that sweep the 1024- and 512-granule vectors
+#ifndef RES_GW
+#define RES_GW 4
+#endif
+#ifndef RES_SLEEP
+#define RES_SLEEP 1
+#endif
+constexpr int GW = RES_GW;  // waves that sweep the 1024- and 512-granule vectors
 
 __device__ __forceinline__ void publish(u64* g, unsigned tag, float v) {
     __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+}
+// Same-XCD hand-off: a workgroup-scope store (global_store ... sc0) keeps the line in the XCD's
+// L2, which every CU of that XCD reads with the agent-scope (sc1, L1-bypassing) loads of sweep().
+__device__ __forceinline__ void publish_xcd(u64* g, unsigned tag, float v) {
+    __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ u64 peek(u64* g) {
     return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -36,10 +48,10 @@ __device__ __forceinline__ void fail(int* status, int code) {
     __hip_atomic_store((gint*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals `tag`;
+// One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals tag(i);
 // false after `tmo` wall-clock ticks (the caller flags the error, the grid drains).
-template <int N, typename F>
-__device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo) {
+template <int N, typename F, typename T>
+__device__ __forceinline__ bool sweep2(u64* g, F idx, T tag, float (&v)[N], long long tmo) {
     long long t_end = 0;
     for (int spin = 0;; ++spin) {
         bool ok = true;
@@ -49,7 +61,7 @@ __device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx
             if (k >= 0) {
                 const u64 x = peek(g + k);
                 v[i] = __uint_as_float((unsigned)x);
-                ok = ok && (unsigned)(x >> 32) == tag;
+                ok = ok && (unsigned)(x >> 32) == tag(i);
             }
         }
         if (__all(ok)) return true;
@@ -58,8 +70,33 @@ __device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx
         } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
             return false;
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (RES_SLEEP) __builtin_amdgcn_s_sleep(RES_SLEEP);
     }
+}
+// One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals `tag`;
+// false after `tmo` wall-clock ticks (the caller flags the error, the grid drains).
+template <int N, typename F>
+__device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo) {
+    return sweep2<N>(g, idx, [&](int) { return tag; }, v, tmo);
+}
+
+// LSTM cell of units 4c..4c+3 from the 16 gate sums (row g*4 + u, torch order i, f, g, o): lanes
+// 0..15 evaluate one gate nonlinearity each in parallel; lanes 0..3 pull f, g, o from lanes u+4,
+// u+8, u+12 by DPP row shifts and update (c, h) exactly as the sgemm LSTM epilogue does.
+// Call with lanes 0..15 of wave 0 active; returns h in lanes 0..3 and updates c there.
+__device__ __forceinline__ float lstm_cell16(float pre, float& c) {
+    const int k = threadIdx.x;
+    const float act = (k >> 2) == 2 ? tanhf(pre) : sigmoidf_(pre);
+    const float f = dpp_move<0x104, 0xf>(act, 0.f);   // row_shl:4
+    const float g = dpp_move<0x108, 0xf>(act, 0.f);   // row_shl:8
+    const float o = dpp_move<0x10C, 0xf>(act, 0.f);   // row_shl:12
+    const float c2 = f * c + act * g;
+    c = c2;
+    return o * tanhf(c2);
+}
+// sigmoid from the hardware exp2 / reciprocal (attention energies only; ~1e-7 relative)
+__device__ __forceinline__ float sigmoid_fast(float x) {
+    return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
 }
 
 __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
@@ -69,20 +106,43 @@ __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
     return fmaf(w.w, x.w, acc);
 }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-// sum over the 32 lanes of a half-wave (one gate row), butterfly: every lane gets the same value
-__device__ __forceinline__ float sum32(float v) {
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Sums over each half-wave (lanes 0-31, 32-63) by DPP row scans: the totals land in lanes 31
+// and 63 (other lanes hold partial scans).  No LDS round trip per level.
+__device__ __forceinline__ float sum32_dpp(float v) {
+    v += dpp_move<0x111, 0xf>(v, 0.f);  // row_shr:1
+    v += dpp_move<0x112, 0xf>(v, 0.f);  // row_shr:2
+    v += dpp_move<0x114, 0xf>(v, 0.f);  // row_shr:4
+    v += dpp_move<0x118, 0xf>(v, 0.f);  // row_shr:8
+    v += dpp_move<0x142, 0xa>(v, 0.f);  // row_bcast:15 into rows 1, 3
     return v;
+}
+
+// Candidate slot s (0..15) of the attention fast path: the window W(n) = {(n-2) mod L} +
+// [n-1, min(n+2, L-1)] (slots 0-4), then p and p + 1 for every p of the previous window W(n')
+// (slots 5-14); -1 = unused.  Duplicates are allowed (same value written twice).
+__device__ __forceinline__ int res_window(int k, int nn, int L) {
+    if (k == 0) return nn >= 2 ? nn - 2 : nn - 2 + L;
+    const int clo = nn >= 1 ? nn - 1 : L - 1, chi = min(nn + 2, L - 1);
+    const int p = clo + k - 1;
+    return p <= chi ? p : -1;
+}
+__device__ __forceinline__ int res_candidate(int s, int nn, int np, int L) {
+    if (s < 5) return res_window(s, nn, L);
+    if (s >= 15) return -1;
+    const int p = res_window((s - 5) >> 1, np, L);
+    if (p < 0) return -1;
+    const int q = p + ((s - 5) & 1);
+    return q < L ? q : -1;
 }
 
 constexpr int SM_WDL = 16 * 16 * 32 * 4;  // floats of the decoder-LSTM LDS weight image (128 KiB)
 constexpr int SM_ST = 64;                  // biases, cell states, stop-rule state
 constexpr int SM_RQ = 4 * 64 * 4;          // query row [4 i4][64 lanes] float4 | attention CU scratch
 constexpr int SM_RM = 2 * 6 * 64 * 4 + 2 * 256;  // fused rows [2][6][64] float4 | row 0 + energy partials
-constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 16 + SM_ST + SM_RQ + SM_RM;
+constexpr int SM_PROF = 2 * 16;            // RES_PHASES tick accumulators (long long)
+constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 16 + SM_ST + SM_RQ + SM_RM + SM_PROF + PRE;
 static_assert(SM_RM >= 6 * 64 * 4 + RES_WAVES * RES_LMAX, "attention CU partials");
-static_assert(SM_RQ >= 2 * RES_LMAX + 2 * RES_WAVES + ADIM, "attention CU scratch");
+static_assert(SM_RQ >= 3 * RES_LMAX + 2 * RES_WAVES + 16 + ADIM, "attention CU scratch");
 
 __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const ResArgs a) {
     const int c = blockIdx.x;
@@ -103,14 +163,25 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                                // [50] flag1, [51] count (int bits, stop lane)
     float* rq = st + SM_ST;    // query row (CUs < 128) | attention CU: aold, an, scr, v
     float* rm = rq + SM_RQ;    // fused rows c, c+256 | attention CU: row c + energy partials
-    float* aold = rq;
-    float* an = aold + RES_LMAX;
-    float* scr = an + RES_LMAX;
-    float* xv = scr + 2 * RES_WAVES;
+    float* abuf = rq;                 // [2][RES_LMAX] previous alpha, ping-pong by step parity
+    float* an = abuf + 2 * RES_LMAX;  // unnormalised forward weights of this step
+    float* scr = an + RES_LMAX;       // [2 * RES_WAVES] + candidate values [16]
+    float* xv = scr + 2 * RES_WAVES + 16;
     float* red = rm + 6 * 64 * 4;  // [RES_WAVES][RES_LMAX]
+    long long* pacc = reinterpret_cast<long long*>(rm + SM_RM);
+    float* xp1 = rm + SM_RM + SM_PROF;  // pre1_t (prenet layer 1 output) gathered by wave 0
+    // optional phase timing (thread 0 of CU 0 and of the attention CU)
+    const bool prof = a.prof != nullptr && (c == 0 || c == RES_ATT_CU);
+    long long plast = 0;
+#define RES_MARK(k)                                     \
+    if (prof && tid == 0) {                             \
+        const long long now = (long long)wall_clock64(); \
+        pacc[k] += now - plast;                         \
+        plast = now;                                    \
+    }
 
     // ---- weights (loaded once per call) and initial state
-    float4 wa[14], wdc[4], wp;
+    float4 wa[14], wdc[4];
     // per-wave small rows (wave 0 prenet-2 in VGPRs; wave 1 query and waves 2/3 fused rows in LDS)
     const float4* wsp = a.w.ws + ((size_t)c * RES_WAVES + wave) * 6 * 64 + lane;
     {
@@ -120,7 +191,6 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         const float4* q = a.w.wdc + (size_t)c * 4 * RES_THREADS + tid;
 #pragma unroll
         for (int i = 0; i < 4; ++i) wdc[i] = q[(size_t)i * RES_THREADS];
-        wp = wsp[0];
         if (wave == 1 && c < ADIM)
             for (int i = 0; i < 4; ++i) reinterpret_cast<float4*>(rq)[i * 64 + lane] = wsp[i * 64];
         if ((wave == 2 || wave == 3) && (c + 256 * (wave - 2)) < a.nrows)
@@ -144,8 +214,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     for (int k = tid; k < ENC; k += RES_THREADS) xctx[k] = a.xa[PRE + k];
     const int L = a.L;
     const bool att_cu = c == RES_ATT_CU;
-    int n = 0;
-    float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f};
+    int n = 0, n_prev = 0;
+    float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f}, ptc[4] = {0.f, 0.f, 0.f, 0.f};
     auto prefetch_rows = [&](int nn) {
         // the rows the context can use after the mask: (nn-2) mod L and [nn-1, nn+2]
         const int cx = (nn - 2 + L) % L, clo = nn >= 1 ? nn - 1 : L - 1, chi = min(nn + 2, L - 1);
@@ -157,7 +227,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         n = a.nidx[0];
         ufa = a.u[0];
         vb = a.v_b[0];
-        for (int j = tid; j < L; j += RES_THREADS) aold[j] = a.alpha[j];
+        for (int j = tid; j < L; j += RES_THREADS) abuf[j] = a.alpha[j];  // step 0 reads buffer 0
         if (tid < ADIM) xv[tid] = a.v[tid];
         prefetch_rows(n);
     }
@@ -170,15 +240,63 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     if (tid == 0) {
         flags[0] = 0;
         flags[1] = 0;
+        for (int k = 0; k < RES_PHASES; ++k) pacc[k] = 0;
+        if (prof) plast = (long long)wall_clock64();
     }
     __syncthreads();
 
     const long long tmo = a.timeout_ticks;
+    // ---- XCD discovery: prenet-2 is computed and exchanged inside each XCD (same-L2 hand-off).
+    // Every CU publishes its XCC id; each reads the table, takes rank = #CUs of its XCD before it,
+    // and computes rows [rank * 256 / n, (rank + 1) * 256 / n) of its XCD's copy of prenet-2.
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const unsigned setup_tag = (a.salt << 14) | 0x3FFFu;
+    if (tid == 0) publish(a.gran + GR_SETUP + c, setup_tag, __int_as_float(xcc));
+    if (wave == 0) {
+        float v4[4];
+        const bool ok = sweep<4>(a.gran, setup_tag, v4, [&](int i) { return GR_SETUP + lane * 4 + i; }, tmo);
+        int rank = 0, nx = 0, nmin = RES_CUS;
+        for (int k = 0; k < 8; ++k) {
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int x = __float_as_int(v4[i]) & 7;
+                cnt += __popcll(__ballot(x == k));
+                if (k == xcc) rank += __popcll(__ballot(x == k && lane * 4 + i < c));
+            }
+            if (k == xcc) nx = cnt;
+            if (cnt > 0) nmin = min(nmin, cnt);
+        }
+        if (lane == 0) {
+            int* fl = reinterpret_cast<int*>(flags);
+            fl[2] = rank;
+            fl[3] = nx;
+            if (!ok) { flags[1] = 1; fail(a.status, 6); }
+            else if (nmin < RES_MIN_CUS_PER_XCD) { flags[1] = 1; fail(a.status, RES_STATUS_PLACEMENT); }
+        }
+    }
+    __syncthreads();
+    if (flags[1]) return;
+    const int p2lo = flags[2] * PRE / flags[3], p2hi = (flags[2] + 1) * PRE / flags[3];
+    const int r0 = p2lo + wave, r1 = p2lo + wave + RES_WAVES;  // this wave's prenet-2 rows (< p2hi)
+    const float4 wp0 = r0 < p2hi ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    const float4 wp1 = r1 < p2hi ? ld4(a.w.w2 + r1 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    u64* Gx = a.gran + GR_PRE2X + xcc * PRE;  // this XCD's prenet-2 slots (parity offset added below)
     int t = 0;
     for (;; ++t) {
         u64* G = a.gran + (t & 1) * GR_TOTAL;          // this step's granules
         u64* Gp = a.gran + ((t & 1) ^ 1) * GR_TOTAL;   // the previous step's (pre1, continue flag)
-        const unsigned E = (unsigned)t * 8u;           // tags E+1 .. E+6, never 0
+        const unsigned E = (a.salt << 14) | ((unsigned)t * 8u);  // tags E+1 .. E+6, never 0
+        if (att_cu && t > 0) {
+            // the next attention step's operands, in flight while pre1 is awaited: the encoder rows
+            // the mask can keep and P at the candidate positions
+            prefetch_rows(n);
+            const int pos = res_candidate(tid >> 5, n, n_prev, L);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) ptc[m] = pos >= 0 ? a.Pt[(int64_t)((tid & 31) + 32 * m) * a.Lcap + pos] : 0.f;
+        }
         // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}]
         float acc_a = 0.f;
 #pragma unroll
@@ -188,65 +306,86 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         asm volatile("" ::: "memory");  // bound the hoisted LDS loads (register pressure)
 #pragma unroll
         for (int i = 10; i < 14; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
-        // 2) prenet layer 2 (wave 0)
+        // 2) prenet layer 2: wave 0 gathers pre1_t (+ the previous step's continue flag); every
+        //    wave computes its rows of this XCD's copy, publishes them XCD-locally; wave 0 gathers
         if (wave == 0) {
+            const int gp = ((t & 1) ^ 1) * GR_TOTAL;
             float p[5];
             bool ok = true;
             if (t == 0) {
                 const float4 v = ld4(a.pre1 + lane * 4);  // go frame's layer 1 (enqueue_prenet_go)
                 p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w; p[4] = 1.f;
             } else {
-                ok = sweep<5>(Gp, E - 2, p, [&](int i) { return i < 4 ? GR_PRE1 + lane * 4 + i : GR_CTRL; }, tmo);
+                ok = sweep<5>(a.gran, E - 2, p, [&](int i) { return gp + (i < 4 ? GR_PRE1 + lane * 4 + i : GR_CTRL); }, tmo);
             }
-            const bool go = p[4] != 0.f;
-            if (ok && go) {
-                float s = dot4(wp, float4{p[0], p[1], p[2], p[3]}, 0.f);
-                s = wave_sum(s);
-                if (lane == 0) publish(G + GR_PRE2 + c, E + 1, fmaxf(s, 0.f));
-                float q4[4];
-                ok = sweep<4>(G, E + 1, q4, [&](int i) { return GR_PRE2 + lane * 4 + i; }, tmo);
+            RES_MARK(0);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) xpre[lane * 4 + i] = q4[i];
-            }
+            for (int i = 0; i < 4; ++i) xp1[lane * 4 + i] = p[i];
             if (lane == 0) {
                 if (!ok) { flags[1] = 1; fail(a.status, 1); }
-                if (ok && !go) flags[0] = 1;
+                if (ok && p[4] == 0.f) flags[0] = 1;
+            }
+        }
+        __syncthreads();  // P1
+        if (flags[0] | flags[1]) break;
+        {
+            const float4 x = ld4(xp1 + lane * 4);
+            u64* gx = Gx + (t & 1) * GR_TOTAL;
+            if (r0 < p2hi) {
+                const float s0 = wave_sum_dpp(dot4(wp0, x, 0.f));
+                if (lane == 0) publish_xcd(gx + r0, E + 1, fmaxf(s0, 0.f));
+            }
+            if (r1 < p2hi) {
+                const float s1 = wave_sum_dpp(dot4(wp1, x, 0.f));
+                if (lane == 0) publish_xcd(gx + r1, E + 1, fmaxf(s1, 0.f));
+            }
+            RES_MARK(1);
+            if (wave == 0) {
+                float q4[4];
+                const bool ok = sweep<4>(gx, E + 1, q4, [&](int i) { return lane * 4 + i; }, tmo);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xpre[lane * 4 + i] = q4[i];
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7); }
             }
         }
         __syncthreads();  // B1
-        if (flags[0] | flags[1]) break;
+        if (flags[1]) break;
+        RES_MARK(2);
         // 3) prenet part, cell
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc_a = dot4(wa[i], ld4(xpre + i * 128 + ks * 4), acc_a);
-        acc_a = sum32(acc_a);
-        if (ks == 0) gates[r] = acc_a;
+        acc_a = sum32_dpp(acc_a);
+        if (ks == 31) gates[r] = acc_a;
         __syncthreads();  // B2
-        if (tid < 4) {
-            const float gi = gates[tid] + st[tid], gf = gates[4 + tid] + st[4 + tid];
-            const float gg = gates[8 + tid] + st[8 + tid], go = gates[12 + tid] + st[12 + tid];
-            const float c2 = sigmoidf_(gf) * st[32 + tid] + sigmoidf_(gi) * tanhf(gg);
-            const float h = sigmoidf_(go) * tanhf(c2);
-            st[32 + tid] = c2;
-            st[40 + tid] = h;
-            publish(G + GR_HATT + 4 * c + tid, E + 2, h);
+        RES_MARK(3);
+        if (tid < 16) {
+            float cs = st[32 + (tid & 3)];
+            const float h = lstm_cell16(gates[tid] + st[tid], cs);
+            if (tid < 4) {
+                st[32 + tid] = cs;
+                st[40 + tid] = h;
+                publish(G + GR_HATT + 4 * c + tid, E + 2, h);
+            }
         }
         // 4) gather h_att_t
         if (wave < GW) {
-            float v4[4];
-            const bool ok = sweep<4>(G, E + 2, v4, [&](int i) { return GR_HATT + wave * 256 + i * 64 + lane; }, tmo);
+            constexpr int PER = HATT / (64 * GW);
+            float v4[PER];
+            const bool ok = sweep<PER>(G, E + 2, v4, [&](int i) { return GR_HATT + wave * 64 * PER + i * 64 + lane; }, tmo);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) xh_att[wave * 256 + i * 64 + lane] = v4[i];
+            for (int i = 0; i < PER; ++i) xh_att[wave * 64 * PER + i * 64 + lane] = v4[i];
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2); }
         }
         __syncthreads();  // B3
         if (flags[1]) break;
+        RES_MARK(4);
         // 5) query row
         if (wave == 1 && c < ADIM) {
             float s = 0.f;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 s = dot4(reinterpret_cast<const float4*>(rq)[i * 64 + lane], ld4(xh_att + i * 256 + lane * 4), s);
-            s = wave_sum(s);
+            s = wave_sum_dpp(s);
             if (lane == 0) publish(G + GR_Q + c, E + 3, s);
         }
         // 6) decoder LSTM over [h_att_t | h_dec_{t-1}]
@@ -256,18 +395,14 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
 #pragma unroll 2
         for (int i = 8; i < 16; ++i)
             acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
-        // 7) attention step
+        RES_MARK(5);
+        // 7) attention step.  After the forward mask the previous alpha is nonzero only on the
+        //    previous window S' = W(n') = {(n'-2) mod L} + [n'-1, n'+2], so every position outside
+        //    C = W(n) + S' + (S'+1) has mix = 1e-8 exactly and anj = 1e-8 * sigmoid <= 1e-8: the
+        //    outputs (window weights, max(alpha), the window sum) need the energies of C only
+        //    (<= 15 positions, duplicates harmless) whenever max over C >= 1e-8.  Step 0 (alpha
+        //    initialised nonzero everywhere) and that rare case evaluate every position.
         if (att_cu) {
-            // processed inputs of this wave's 16 dims at positions lane, lane + 64 (in flight
-            // while the query arrives)
-            float pt[2][16];
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int dd = 0; dd < 16; ++dd) {
-                    const int jj = p * 64 + lane;
-                    pt[p][dd] = jj < L ? a.Pt[(int64_t)(16 * wave + dd) * a.Lcap + jj] : 0.f;
-                }
             if (wave == 0) {
                 float q2[2];
                 const bool ok = sweep<2>(G, E + 3, q2, [&](int i) { return GR_Q + i * 64 + lane; }, tmo);
@@ -277,68 +412,101 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             }
             __syncthreads();  // A1
             if (flags[1]) break;
-            // energy partials over this wave's 16 attention dims (query_energy_kernel's split);
-            // positions >= 128 read P from global memory (L2-resident across steps)
-            float xqd[16];
+            RES_MARK(6);
+            const float* aold = abuf + (t & 1) * RES_LMAX;
+            float* anew = abuf + ((t & 1) ^ 1) * RES_LMAX;
+            float* candv = scr + 2 * RES_WAVES;
+            const int cx = n >= 2 ? n - 2 : n - 2 + L, clo = n >= 1 ? n - 1 : L - 1, chi = min(n + 2, L - 1);
+            bool full = t == 0;
+            if (!full) {
+                // candidate slot s = tid / 32: 32 lanes x 4 dims each, butterfly-summed
+                const int sl = tid >> 5, sub = tid & 31;
+                const int pos = res_candidate(sl, n, n_prev, L);
+                float part = 0.f;
 #pragma unroll
-            for (int dd = 0; dd < 16; ++dd) xqd[dd] = xq[16 * wave + dd];
+                for (int m = 0; m < 4; ++m) {
+                    const int d = sub + 32 * m;
+                    part += xv[d] * tanh_fast(xq[d] + ptc[m]);
+                }
+                const float e = sum32_dpp(part);
+                if (sub == 31) {
+                    float v = -INFINITY;
+                    if (pos >= 0) {
+                        const float sg = sigmoid_fast(e + vb);
+                        const float prev = pos > 0 ? aold[pos - 1] : 0.f;
+                        const float mix =
+                            __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, aold[pos]), __fmul_rn(ufa, prev)), 1e-8f);
+                        v = __fmul_rn(mix, sg);
+                        an[pos] = v;
+                    }
+                    candv[sl] = v;
+                }
+                __syncthreads();  // A2
+                RES_MARK(14);
+                float rm = -INFINITY;
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int jj = p * 64 + lane;
-                if (jj < L) {
+                for (int k = 0; k < 4; ++k) {
+                    const float4 v4 = reinterpret_cast<const float4*>(candv)[k];
+                    rm = fmaxf(rm, fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)));
+                }
+                full = !(rm >= 1e-8f);  // uniform
+                if (!full && tid == 0) scr[0] = rm;
+            }
+            if (full) {
+                // every position: wave w owns dims [16w, 16w + 16), lanes own positions
+                float xqd[16];
+#pragma unroll
+                for (int dd = 0; dd < 16; ++dd) xqd[dd] = xq[16 * wave + dd];
+#pragma unroll 1
+                for (int jj = lane; jj < L; jj += 64) {
                     float s = 0.f;
 #pragma unroll
-                    for (int dd = 0; dd < 16; ++dd) s += xv[16 * wave + dd] * tanh_fast(xqd[dd] + pt[p][dd]);
+                    for (int dd = 0; dd < 16; ++dd) {
+                        const int d = 16 * wave + dd;
+                        s += xv[d] * tanh_fast(xqd[dd] + a.Pt[(int64_t)d * a.Lcap + jj]);
+                    }
                     red[wave * RES_LMAX + jj] = s;
                 }
-            }
-#pragma unroll 1
-            for (int jj = 128 + lane; jj < L; jj += 64) {
-                float s = 0.f;
+                __syncthreads();
+                const int j = tid;
+                float anj = -INFINITY;
+                if (j < L) {
+                    float e = 0.f;
 #pragma unroll
-                for (int dd = 0; dd < 16; ++dd) {
-                    const int d = 16 * wave + dd;
-                    s += xv[d] * tanh_fast(xqd[dd] + a.Pt[(int64_t)d * a.Lcap + jj]);
+                    for (int w = 0; w < RES_WAVES; ++w) e += red[w * RES_LMAX + j];
+                    const float sg = sigmoid_fast(e + vb);
+                    const float prev = j > 0 ? aold[j - 1] : 0.f;
+                    const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, aold[j]), __fmul_rn(ufa, prev)), 1e-8f);
+                    anj = __fmul_rn(mix, sg);
+                    an[j] = anj;
                 }
-                red[wave * RES_LMAX + jj] = s;
+                const float wmax = wave_max_dpp(anj);
+                if (lane == 0) scr[2 * wave + 1] = wmax;
+                __syncthreads();
+                if (tid == 0) {
+                    float rm = -INFINITY;
+                    for (int k = 0; k < RES_WAVES; ++k) rm = fmaxf(rm, scr[2 * k + 1]);
+                    scr[0] = rm;
+                }
             }
-            __syncthreads();  // A2
-            const int j = tid;
-            const bool in = j < L;
-            const int cx = (n - 2 + L) % L, clo = n >= 1 ? n - 1 : L - 1, chi = min(n + 2, L - 1);
-            float anj = 0.f;
-            if (in) {
-                float e = 0.f;
-#pragma unroll
-                for (int w = 0; w < RES_WAVES; ++w) e += red[w * RES_LMAX + j];
-                const float sg = sigmoidf_(e + vb);
-                const float prev = j > 0 ? aold[j - 1] : 0.f;
-                const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, aold[j]), __fmul_rn(ufa, prev)), 1e-8f);
-                anj = __fmul_rn(mix, sg);
-                an[j] = anj;
-            }
-            const bool win = in && j >= clo && j <= chi && j != cx;
-            const float wsum = wave_sum_dpp(win ? anj : 0.f);
-            const float wmax = wave_max_dpp(in ? anj : -INFINITY);
-            if (lane == 0) {
-                scr[2 * wave] = wsum;
-                scr[2 * wave + 1] = wmax;
-            }
-            __syncthreads();  // A3
-            float rs = 0.f, rm = -INFINITY;
-#pragma unroll
-            for (int k = 0; k < RES_WAVES; ++k) {
-                rs += scr[2 * k];
-                rm = fmaxf(rm, scr[2 * k + 1]);
-            }
+            __syncthreads();  // A3: an[] of the window and max(alpha) in LDS
+            RES_MARK(7);
+            const float rm = scr[0];
+            float rs = 0.f;  // the surviving window [n-1, n+2] without (n-2) mod L, index order
+            for (int p = clo; p <= chi; ++p)
+                if (p != cx) rs += an[p];
             const float vx = 0.01f * rm;  // alpha[n-2] = 0.01 * val
             const float denom = rs + vx;
+            // the <= 5 nonzero weights, once: (n-2) mod L and the window [clo, chi]
+            const float inv = 1.f / denom;
+            const float wcx = vx * inv;
+            float ww[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ww[k] = (clo + k <= chi && clo + k != cx) ? an[clo + k] * inv : 0.f;
             auto weight = [&](int p) -> float {
-                if (p == cx) return vx / denom;
-                return (p >= clo && p <= chi) ? an[p] / denom : 0.f;
+                if (p == cx) return wcx;
+                return (p >= clo && p <= chi) ? ww[p - clo] : 0.f;
             };
-            const float w = in ? weight(j) : 0.f;
-            if (t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
             const float tail = weight(L - 2) + weight(L - 1);  // tacotron2.py:268
             float bv = 0.f;
             int bi = -1;
@@ -347,59 +515,76 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 if (p <= L - 2 && wp > bv) { bv = wp; bi = p; }
             };
             if (cx < clo) consider(cx);
-            for (int p = clo; p <= chi; ++p) consider(p);
-            if (cx > chi) consider(cx);
-            float ctx = 0.f;
-            if (cx < clo) ctx += weight(cx) * ex;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (clo + k <= chi) ctx += weight(clo + k) * (clo + k == cx ? ex : erow[k]);
-            if (cx > chi) ctx += weight(cx) * ex;
+                if (clo + k <= chi) consider(clo + k);
+            if (cx > chi) consider(cx);
+            float ctx = 0.f;
+            if (cx < clo) ctx += wcx * ex;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (clo + k <= chi) ctx += (clo + k == cx ? wcx * ex : ww[k] * erow[k]);
+            if (cx > chi) ctx += wcx * ex;
+            RES_MARK(15);
             publish(G + GR_CTX + tid, E + 4, ctx);
             if (tid == 0) publish(G + GR_TAIL, E + 4, tail);
-            __syncthreads();  // A4: aold / an reads done
-            if (in) aold[j] = w;
-            n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step
-            prefetch_rows(n);
+            xctx[tid] = ctx;  // this CU skips the gather
+            if (tid == 0) xctx[ENC] = tail;
+            RES_MARK(8);
+            // off the critical path: this step's alpha (next step's prev_alpha) and alignment row
+            const int j = tid;
+            const float w = j < L ? weight(j) : 0.f;
+            if (j < L) anew[j] = w;
+            if (t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
+            n_prev = n;
+            n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: loop top)
+            RES_MARK(9);
         }
         // 8) gather ctx_t and the tail
-        if (wave < GW) {
-            float v3[3];
-            const bool ok = sweep<3>(G, E + 4, v3, [&](int i) {
-                return i < 2 ? GR_CTX + wave * 128 + i * 64 + lane : (wave == 0 && lane == 0 ? GR_TAIL : -1);
+        if (wave < GW && !att_cu) {
+            constexpr int PER = ENC / (64 * GW);
+            float v3[PER + 1];
+            const bool ok = sweep<PER + 1>(G, E + 4, v3, [&](int i) {
+                return i < PER ? GR_CTX + wave * 64 * PER + i * 64 + lane : (wave == 0 && lane == 0 ? GR_TAIL : -1);
             }, tmo);
-            xctx[wave * 128 + lane] = v3[0];
-            xctx[wave * 128 + 64 + lane] = v3[1];
-            if (wave == 0 && lane == 0) xctx[ENC] = v3[2];
+#pragma unroll
+            for (int i = 0; i < PER; ++i) xctx[wave * 64 * PER + i * 64 + lane] = v3[i];
+            if (wave == 0 && lane == 0) xctx[ENC] = v3[PER];
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4); }
         }
         __syncthreads();  // B4
         if (flags[1]) break;
+        RES_MARK(10);
         // 9) context part, cell
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc_d = dot4(wdc[i], ld4(xctx + i * 128 + ks * 4), acc_d);
-        acc_d = sum32(acc_d);
-        if (ks == 0) gates[r] = acc_d;
+        acc_d = sum32_dpp(acc_d);
+        if (ks == 31) gates[r] = acc_d;
         __syncthreads();  // B5
-        if (tid < 4) {
-            const float gi = gates[tid] + st[16 + tid], gf = gates[4 + tid] + st[20 + tid];
-            const float gg = gates[8 + tid] + st[24 + tid], go = gates[12 + tid] + st[28 + tid];
-            const float c2 = sigmoidf_(gf) * st[36 + tid] + sigmoidf_(gi) * tanhf(gg);
-            const float h = sigmoidf_(go) * tanhf(c2);
-            st[36 + tid] = c2;
-            st[44 + tid] = h;
-            publish(G + GR_HDEC + 4 * c + tid, E + 5, h);
+        RES_MARK(11);
+        if (tid < 16) {
+            float cs = st[36 + (tid & 3)];
+            const float h = lstm_cell16(gates[tid] + st[16 + tid], cs);
+            if (tid < 4) {
+                st[36 + tid] = cs;
+                st[44 + tid] = h;
+                publish(G + GR_HDEC + 4 * c + tid, E + 5, h);
+            }
         }
         // 10) gather h_dec_t
         if (wave < GW) {
-            float v4[4];
-            const bool ok = sweep<4>(G, E + 5, v4, [&](int i) { return GR_HDEC + wave * 256 + i * 64 + lane; }, tmo);
+            constexpr int PER = HDEC / (64 * GW);
+            float v4[PER];
+            const bool ok = sweep<PER>(G, E + 5, v4, [&](int i) { return GR_HDEC + wave * 64 * PER + i * 64 + lane; }, tmo);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) xh_dec[wave * 256 + i * 64 + lane] = v4[i];
+            for (int i = 0; i < PER; ++i) xh_dec[wave * 64 * PER + i * 64 + lane] = v4[i];
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5); }
         }
         __syncthreads();  // B6
         if (flags[1]) break;
+        RES_MARK(12);
+        long long m0 = 0;  // fused-row phase timing (wave 2, lane 0)
+        if (prof && tid == 128) m0 = (long long)wall_clock64();
         // 11) fused rows [mel | prenet-1 of step t+1 | stop]
         if (wave == 2 || wave == 3) {
             const int row = c + 256 * (wave - 2);
@@ -410,7 +595,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 for (int i = 0; i < 4; ++i) s = dot4(wm[i * 64], ld4(xh_dec + i * 256 + lane * 4), s);
 #pragma unroll
                 for (int i = 4; i < 6; ++i) s = dot4(wm[i * 64], ld4(xctx + (i - 4) * 256 + lane * 4), s);
-                s = wave_sum(s);
+                s = wave_sum_dpp(s);
                 const float v = s + st[48 + wave - 2];
                 if (lane == 0) {
                     if (row < a.nmel) {
@@ -447,8 +632,11 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 }
             }
         }
+        if (prof && tid == 128) pacc[13] += (long long)wall_clock64() - m0;
     }
     if (flags[1]) return;
+    if (prof && tid == 0)
+        for (int k = 0; k < RES_PHASES; ++k) a.prof[(c == 0 ? 0 : 1) * RES_PHASES + k] = pacc[k];
     // the last step t-1 leaves its state where the multi-launch path's would be
     const int pl = (t - 1) & 1;
     if (tid < 4) {
@@ -501,8 +689,7 @@ __global__ void res_pack_ws(const float* w2, const float* wq, const float* wf, i
     const int lane = idx % 64, i4 = (idx / 64) % 6, w = (idx / 384) % RES_WAVES, c = idx / (384 * RES_WAVES);
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < 4; ++j) {
-        if (w == 0 && i4 == 0) v[j] = w2[(int64_t)c * PRE + lane * 4 + j];
-        else if (w == 1 && c < ADIM && i4 < 4) v[j] = wq[(int64_t)c * HATT + i4 * 256 + lane * 4 + j];
+        if (w == 1 && c < ADIM && i4 < 4) v[j] = wq[(int64_t)c * HATT + i4 * 256 + lane * 4 + j];
         else if (w == 2 || w == 3) {
             const int row = c + 256 * (w - 2);
             if (row < nrows) v[j] = wf[(int64_t)row * (HDEC + ENC) + i4 * 256 + lane * 4 + j];
@@ -539,6 +726,7 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
                        w.wa);
     hipLaunchKernelGGL(res_pack_wd, blocks((int64_t)RES_CUS * (8192 + 4 * RES_THREADS)), dim3(256), 0, st, s.d_wih,
                        s.d_whh, w.wdl, w.wdc);
+    (void)hipMemcpyAsync(w.w2, s.w_pre2, sizeof(float) * PRE * PRE, hipMemcpyDeviceToDevice, st);
     hipLaunchKernelGGL(res_pack_ws, blocks((int64_t)RES_CUS * RES_WAVES * 6 * 64), dim3(256), 0, st, s.w_pre2, s.w_q,
                        s.wf, s.nrows, w.ws);
     hipLaunchKernelGGL(res_pack_bias, blocks(RES_CUS * 16), dim3(256), 0, st, s.a_bih, s.a_bhh, s.d_bih, s.d_bhh, s.bf,

@@ -255,6 +255,21 @@ class Tacotron2:
         out = self.inference_batch([row for row in text.cpu().numpy()], speaker_ids=speaker_ids)
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
+    RESIDENT_PHASES = ("att_early_wait_pre1", "prenet2_row", "wait_prenet2", "att_lstm_prenet", "att_cell_gather",
+                       "query_dec_early", "wait_query", "energies_max", "weights_ctx_publish", "next_prefetch",
+                       "wait_ctx", "dec_lstm_ctx", "dec_cell_gather", "fused_rows", "cand_energies", "weights_ctx")
+
+    def profile_resident_phases(self):
+        """Mean µs per decoder step of each phase of the resident batch-1 decoder (last sentence
+        re-run with timers; measurement only): {"cu0": {...}, "attention_cu": {...}}."""
+        lib, hdec, _ = self._handles(1, 1)
+        n = 2 * len(self.RESIDENT_PHASES)
+        us = (ctypes.c_float * n)()
+        _native.check(lib.tts_decoder_resident_phases(hdec, us, n), "tts_decoder_resident_phases")
+        k = len(self.RESIDENT_PHASES)
+        return {"cu0": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[:k]])),
+                "attention_cu": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[k:]]))}
+
     def profile_step_kernels(self, reps=50):
         """Mean duration (ms) of each decoder-step kernel, HIP events on its own stream, for the
         batch of the last inference call (measurement only)."""
