@@ -381,7 +381,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
             float *pa = nullptr, *pdl = nullptr, *pdc = nullptr, *pws = nullptr;
             if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) || dmalloc(d, &pws, nws) ||
                 dmalloc(d, &d->rw.ba, RES_CUS * 16) || dmalloc(d, &d->rw.bd, RES_CUS * 16) ||
-                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) ||
+                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) || dmalloc(d, &d->rw.wq, (size_t)ADIM * HATT) ||
                 dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
                 e = hipErrorOutOfMemory;
             if (e == hipSuccess) {

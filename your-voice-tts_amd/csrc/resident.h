@@ -4,7 +4,9 @@
 // attention LSTM's in VGPRs, the decoder LSTM's recurrent/attention half in LDS, its context
 // half in VGPRs) plus a prenet-2 row, a query row and up to two fused mel/prenet-1/stop rows.
 // A step then streams no weights at all; its cost is the six dependent hand-offs
-//   pre1 -> prenet2 -> h_att -> query -> [attention on one CU] -> ctx -> h_dec -> pre1
+//   pre1 -> prenet2 -> h_att -> query -> [attention] -> ctx -> h_dec -> pre1
+// of which prenet2, query and ctx stay inside one XCD: every XCD computes its own copy of
+// prenet-2, the query and the attention step (one attention CU per XCD; identical results).
 // carried by 8-byte {tag, value} granules (agent-scope relaxed atomics, sc1: the hand-off form
 // that needs no fences, MI355X_MICROARCH.md "Valid forms").  Every wait is bounded: a wave
 // that does not see its data within the timeout flags an error and the grid drains.
@@ -22,25 +24,26 @@ constexpr int RES_CUS = 256;
 constexpr int RES_THREADS = 512;
 constexpr int RES_WAVES = RES_THREADS / 64;
 constexpr int RES_LMAX = 256;
-constexpr int RES_ATT_CU = RES_CUS - 1;  // runs the attention step (no query row: CU >= 128)
 
 // granule slots (u64 {tag << 32 | float bits}) per step parity
 // (GR_PRE2X: per-XCD prenet-2 vectors, [8 XCDs][256], written and read inside one XCD; GR_SETUP:
 // each CU's XCD id, parity 0 only)
-constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_HATT = 576, GR_Q = 1600, GR_CTX = 1728, GR_TAIL = 2240,
-              GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376, GR_TOTAL = 5632;
-constexpr int RES_MIN_CUS_PER_XCD = 16;  // prenet-2 rows per CU <= 16 (two per wave)
+// GR_QX: per-XCD query half-rows [8][128 rows][2]; GR_CTXX: per-XCD context + tail [8][528].
+constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_HATT = 576, GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376,
+              GR_QX = 5632, GR_CTXX = 7680, GR_CTXX_STRIDE = ENC + 16, GR_TOTAL = 11904;
+constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-2 rows 8 per CU
 constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
 
 struct ResWeights {
     float4* wa;   // [256 CU][14 i4][512 thr]   attention LSTM rows over [prenet | ctx | h_att]
     float4* wdl;  // [256 CU][16 i4][16 row][32 ks]  decoder LSTM rows over [h_att | h_dec] (LDS image)
     float4* wdc;  // [256 CU][4 i4][512 thr]    decoder LSTM rows over ctx
-    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  wave 1 query row, waves 2/3 fused rows
+    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  waves 2/3: fused rows c, c + 256
     float* ba;    // [256][16] attention LSTM bias (b_ih + b_hh), logical row g*4 + u
     float* bd;    // [256][16] decoder LSTM bias
     float* bs;    // [256][2] fused-row biases (rows c, c + 256)
     float* w2;    // prenet layer-2 weight, reference layout [256][256] (rows picked per XCD rank)
+    float* wq;    // query_layer weight, reference layout [128][1024] (rows picked per XCD rank)
 };
 
 struct ResArgs {

@@ -170,8 +170,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     float* red = rm + 6 * 64 * 4;  // [RES_WAVES][RES_LMAX]
     long long* pacc = reinterpret_cast<long long*>(rm + SM_RM);
     float* xp1 = rm + SM_RM + SM_PROF;  // pre1_t (prenet layer 1 output) gathered by wave 0
-    // optional phase timing (thread 0 of CU 0 and of the attention CU)
-    const bool prof = a.prof != nullptr && (c == 0 || c == RES_ATT_CU);
+    // optional phase timing (thread 0 of CU 0 and of the logging attention CU)
+    bool prof = false;
     long long plast = 0;
 #define RES_MARK(k)                                     \
     if (prof && tid == 0) {                             \
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
 
     // ---- weights (loaded once per call) and initial state
     float4 wa[14], wdc[4];
-    // per-wave small rows (wave 0 prenet-2 in VGPRs; wave 1 query and waves 2/3 fused rows in LDS)
+    // fused rows c, c + 256 (waves 2/3) in LDS
     const float4* wsp = a.w.ws + ((size_t)c * RES_WAVES + wave) * 6 * 64 + lane;
     {
         const float4* p = a.w.wa + (size_t)c * 14 * RES_THREADS + tid;
@@ -191,8 +191,6 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         const float4* q = a.w.wdc + (size_t)c * 4 * RES_THREADS + tid;
 #pragma unroll
         for (int i = 0; i < 4; ++i) wdc[i] = q[(size_t)i * RES_THREADS];
-        if (wave == 1 && c < ADIM)
-            for (int i = 0; i < 4; ++i) reinterpret_cast<float4*>(rq)[i * 64 + lane] = wsp[i * 64];
         if ((wave == 2 || wave == 3) && (c + 256 * (wave - 2)) < a.nrows)
             for (int i = 0; i < 6; ++i) reinterpret_cast<float4*>(rm)[((wave - 2) * 6 + i) * 64 + lane] = wsp[i * 64];
         const float4* l = a.w.wdl + (size_t)c * (SM_WDL / 4);
@@ -212,8 +210,62 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         xh_dec[k] = a.h_dec[a.hps + k];
     }
     for (int k = tid; k < ENC; k += RES_THREADS) xctx[k] = a.xa[PRE + k];
+    if (tid == 0) {
+        flags[0] = 0;
+        flags[1] = 0;
+        for (int k = 0; k < RES_PHASES; ++k) pacc[k] = 0;
+    }
+    __syncthreads();
+    const long long tmo = a.timeout_ticks;
+    // ---- XCD discovery: prenet-2 is computed and exchanged inside each XCD (same-L2 hand-off).
+    // Every CU publishes its XCC id; each reads the table, takes rank = #CUs of its XCD before it,
+    // and computes rows [rank * 256 / n, (rank + 1) * 256 / n) of its XCD's copy of prenet-2.
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const unsigned setup_tag = (a.salt << 14) | 0x3FFFu;
+    if (tid == 0) publish(a.gran + GR_SETUP + c, setup_tag, __int_as_float(xcc));
+    if (wave == 0) {
+        float v4[4];
+        const bool ok = sweep<4>(a.gran, setup_tag, v4, [&](int i) { return GR_SETUP + lane * 4 + i; }, tmo);
+        int rank = 0, nx = 0, nmin = RES_CUS;
+        const int xref = __builtin_amdgcn_readfirstlane(__float_as_int(v4[0]) & 7);  // XCD of CU 0
+        for (int k = 0; k < 8; ++k) {
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int x = __float_as_int(v4[i]) & 7;
+                cnt += __popcll(__ballot(x == k));
+                if (k == xcc) rank += __popcll(__ballot(x == k && lane * 4 + i < c));
+            }
+            if (k == xcc) nx = cnt;
+            if (cnt > 0) nmin = min(nmin, cnt);
+        }
+        if (lane == 0) {
+            int* fl = reinterpret_cast<int*>(flags);
+            fl[2] = rank;
+            fl[3] = nx;
+            fl[4] = xref;
+            if (!ok) { flags[1] = 1; fail(a.status, 6); }
+            else if (nmin < RES_MIN_CUS_PER_XCD) { flags[1] = 1; fail(a.status, RES_STATUS_PLACEMENT); }
+        }
+    }
+    __syncthreads();
+    if (flags[1]) return;
+    const int rank = flags[2], nx = flags[3];
+    const int p2lo = rank * PRE / nx, p2hi = (rank + 1) * PRE / nx;
+    const int r0 = p2lo + wave, r1 = p2lo + wave + RES_WAVES;  // this wave's prenet-2 rows (< p2hi)
+    const float4 wp0 = r0 < p2hi ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    const float4 wp1 = r1 < p2hi ? ld4(a.w.w2 + r1 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    // query rows 4 rank .. 4 rank + 3 of this XCD's copy: wave w holds half (w & 1) of row 4 rank + w / 2
+    const int qrow = 4 * rank + (wave >> 1), qhalf = wave & 1;
+    const float4 wq0 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + lane * 4);
+    const float4 wq1 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + 256 + lane * 4);
     const int L = a.L;
-    const bool att_cu = c == RES_ATT_CU;
+    const bool att_cu = rank == nx - 1;               // the last CU of each XCD runs its attention copy
+    const bool att_log = att_cu && xcc == flags[4];  // ... and one of them writes the alignment rows
+    prof = a.prof != nullptr && (c == 0 || att_log);
+    if (prof && tid == 0) plast = (long long)wall_clock64();
     int n = 0, n_prev = 0;
     float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f}, ptc[4] = {0.f, 0.f, 0.f, 0.f};
     auto prefetch_rows = [&](int nn) {
@@ -237,53 +289,9 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         reinterpret_cast<int*>(st)[50] = a.flag1[0];
         reinterpret_cast<int*>(st)[51] = a.count[0];
     }
-    if (tid == 0) {
-        flags[0] = 0;
-        flags[1] = 0;
-        for (int k = 0; k < RES_PHASES; ++k) pacc[k] = 0;
-        if (prof) plast = (long long)wall_clock64();
-    }
-    __syncthreads();
-
-    const long long tmo = a.timeout_ticks;
-    // ---- XCD discovery: prenet-2 is computed and exchanged inside each XCD (same-L2 hand-off).
-    // Every CU publishes its XCC id; each reads the table, takes rank = #CUs of its XCD before it,
-    // and computes rows [rank * 256 / n, (rank + 1) * 256 / n) of its XCD's copy of prenet-2.
-    int xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7;
-    const unsigned setup_tag = (a.salt << 14) | 0x3FFFu;
-    if (tid == 0) publish(a.gran + GR_SETUP + c, setup_tag, __int_as_float(xcc));
-    if (wave == 0) {
-        float v4[4];
-        const bool ok = sweep<4>(a.gran, setup_tag, v4, [&](int i) { return GR_SETUP + lane * 4 + i; }, tmo);
-        int rank = 0, nx = 0, nmin = RES_CUS;
-        for (int k = 0; k < 8; ++k) {
-            int cnt = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int x = __float_as_int(v4[i]) & 7;
-                cnt += __popcll(__ballot(x == k));
-                if (k == xcc) rank += __popcll(__ballot(x == k && lane * 4 + i < c));
-            }
-            if (k == xcc) nx = cnt;
-            if (cnt > 0) nmin = min(nmin, cnt);
-        }
-        if (lane == 0) {
-            int* fl = reinterpret_cast<int*>(flags);
-            fl[2] = rank;
-            fl[3] = nx;
-            if (!ok) { flags[1] = 1; fail(a.status, 6); }
-            else if (nmin < RES_MIN_CUS_PER_XCD) { flags[1] = 1; fail(a.status, RES_STATUS_PLACEMENT); }
-        }
-    }
-    __syncthreads();
-    if (flags[1]) return;
-    const int p2lo = flags[2] * PRE / flags[3], p2hi = (flags[2] + 1) * PRE / flags[3];
-    const int r0 = p2lo + wave, r1 = p2lo + wave + RES_WAVES;  // this wave's prenet-2 rows (< p2hi)
-    const float4 wp0 = r0 < p2hi ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
-    const float4 wp1 = r1 < p2hi ? ld4(a.w.w2 + r1 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
     u64* Gx = a.gran + GR_PRE2X + xcc * PRE;  // this XCD's prenet-2 slots (parity offset added below)
+    u64* Gq = a.gran + GR_QX + xcc * 2 * ADIM;   // this XCD's query half-rows
+    u64* Gc = a.gran + GR_CTXX + xcc * GR_CTXX_STRIDE;  // this XCD's context + tail
     int t = 0;
     for (;; ++t) {
         u64* G = a.gran + (t & 1) * GR_TOTAL;          // this step's granules
@@ -379,14 +387,12 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         __syncthreads();  // B3
         if (flags[1]) break;
         RES_MARK(4);
-        // 5) query row
-        if (wave == 1 && c < ADIM) {
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                s = dot4(reinterpret_cast<const float4*>(rq)[i * 64 + lane], ld4(xh_att + i * 256 + lane * 4), s);
+        // 5) query half-rows of this XCD's copy (common_layers.py:179), published XCD-locally
+        {
+            float s = dot4(wq0, ld4(xh_att + qhalf * 512 + lane * 4), 0.f);
+            s = dot4(wq1, ld4(xh_att + qhalf * 512 + 256 + lane * 4), s);
             s = wave_sum_dpp(s);
-            if (lane == 0) publish(G + GR_Q + c, E + 3, s);
+            if (lane == 0) publish_xcd(Gq + (t & 1) * GR_TOTAL + 2 * qrow + qhalf, E + 3, s);
         }
         // 6) decoder LSTM over [h_att_t | h_dec_{t-1}]
         float acc_d = 0.f;
@@ -404,10 +410,10 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         //    initialised nonzero everywhere) and that rare case evaluate every position.
         if (att_cu) {
             if (wave == 0) {
-                float q2[2];
-                const bool ok = sweep<2>(G, E + 3, q2, [&](int i) { return GR_Q + i * 64 + lane; }, tmo);
-                xq[lane] = q2[0];
-                xq[64 + lane] = q2[1];
+                float q4[4];
+                const bool ok = sweep<4>(Gq + (t & 1) * GR_TOTAL, E + 3, q4, [&](int i) { return lane * 4 + i; }, tmo);
+                xq[2 * lane] = q4[0] + q4[1];
+                xq[2 * lane + 1] = q4[2] + q4[3];
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3); }
             }
             __syncthreads();  // A1
@@ -526,8 +532,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 if (clo + k <= chi) ctx += (clo + k == cx ? wcx * ex : ww[k] * erow[k]);
             if (cx > chi) ctx += wcx * ex;
             RES_MARK(15);
-            publish(G + GR_CTX + tid, E + 4, ctx);
-            if (tid == 0) publish(G + GR_TAIL, E + 4, tail);
+            publish_xcd(Gc + (t & 1) * GR_TOTAL + tid, E + 4, ctx);
+            if (tid == 0) publish_xcd(Gc + (t & 1) * GR_TOTAL + ENC, E + 4, tail);
             xctx[tid] = ctx;  // this CU skips the gather
             if (tid == 0) xctx[ENC] = tail;
             RES_MARK(8);
@@ -535,7 +541,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             const int j = tid;
             const float w = j < L ? weight(j) : 0.f;
             if (j < L) anew[j] = w;
-            if (t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
+            if (att_log && t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
             n_prev = n;
             n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: loop top)
             RES_MARK(9);
@@ -544,8 +550,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         if (wave < GW && !att_cu) {
             constexpr int PER = ENC / (64 * GW);
             float v3[PER + 1];
-            const bool ok = sweep<PER + 1>(G, E + 4, v3, [&](int i) {
-                return i < PER ? GR_CTX + wave * 64 * PER + i * 64 + lane : (wave == 0 && lane == 0 ? GR_TAIL : -1);
+            const bool ok = sweep<PER + 1>(Gc + (t & 1) * GR_TOTAL, E + 4, v3, [&](int i) {
+                return i < PER ? wave * 64 * PER + i * 64 + lane : (wave == 0 && lane == 0 ? ENC : -1);
             }, tmo);
 #pragma unroll
             for (int i = 0; i < PER; ++i) xctx[wave * 64 * PER + i * 64 + lane] = v3[i];
@@ -689,8 +695,7 @@ __global__ void res_pack_ws(const float* w2, const float* wq, const float* wf, i
     const int lane = idx % 64, i4 = (idx / 64) % 6, w = (idx / 384) % RES_WAVES, c = idx / (384 * RES_WAVES);
     float v[4] = {0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < 4; ++j) {
-        if (w == 1 && c < ADIM && i4 < 4) v[j] = wq[(int64_t)c * HATT + i4 * 256 + lane * 4 + j];
-        else if (w == 2 || w == 3) {
+        if (w == 2 || w == 3) {
             const int row = c + 256 * (w - 2);
             if (row < nrows) v[j] = wf[(int64_t)row * (HDEC + ENC) + i4 * 256 + lane * 4 + j];
         }
@@ -727,6 +732,7 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
     hipLaunchKernelGGL(res_pack_wd, blocks((int64_t)RES_CUS * (8192 + 4 * RES_THREADS)), dim3(256), 0, st, s.d_wih,
                        s.d_whh, w.wdl, w.wdc);
     (void)hipMemcpyAsync(w.w2, s.w_pre2, sizeof(float) * PRE * PRE, hipMemcpyDeviceToDevice, st);
+    (void)hipMemcpyAsync(w.wq, s.w_q, sizeof(float) * ADIM * HATT, hipMemcpyDeviceToDevice, st);
     hipLaunchKernelGGL(res_pack_ws, blocks((int64_t)RES_CUS * RES_WAVES * 6 * 64), dim3(256), 0, st, s.w_pre2, s.w_q,
                        s.wf, s.nrows, w.ws);
     hipLaunchKernelGGL(res_pack_bias, blocks(RES_CUS * 16), dim3(256), 0, st, s.a_bih, s.a_bhh, s.d_bih, s.d_bhh, s.bf,
