@@ -314,6 +314,11 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         asm volatile("" ::: "memory");  // bound the hoisted LDS loads (register pressure)
 #pragma unroll
         for (int i = 10; i < 14; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
+        // decoder LSTM over h_dec_{t-1}, also while pre1 is in flight
+        float acc_d = 0.f;
+#pragma unroll 2
+        for (int i = 8; i < 16; ++i)
+            acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
         // 2) prenet layer 2: wave 0 gathers pre1_t (+ the previous step's continue flag); every
         //    wave computes its rows of this XCD's copy, publishes them XCD-locally; wave 0 gathers
         if (wave == 0) {
@@ -394,13 +399,12 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             s = wave_sum_dpp(s);
             if (lane == 0) publish_xcd(Gq + (t & 1) * GR_TOTAL + 2 * qrow + qhalf, E + 3, s);
         }
-        // 6) decoder LSTM over [h_att_t | h_dec_{t-1}]
-        float acc_d = 0.f;
+        // 6) decoder LSTM over h_att_t (its h_dec_{t-1} half ran at the loop top); the attention
+        //    CU does this after its attention step, which is on the critical path
+        if (!att_cu) {
 #pragma unroll 2
-        for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
-#pragma unroll 2
-        for (int i = 8; i < 16; ++i)
-            acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
+            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
+        }
         RES_MARK(5);
         // 7) attention step.  After the forward mask the previous alpha is nonzero only on the
         //    previous window S' = W(n') = {(n'-2) mod L} + [n'-1, n'+2], so every position outside
@@ -544,6 +548,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (att_log && t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
             n_prev = n;
             n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: loop top)
+#pragma unroll 2
+            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
             RES_MARK(9);
         }
         // 8) gather ctx_t and the tail
