@@ -413,6 +413,18 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         //    (<= 15 positions, duplicates harmless) whenever max over C >= 1e-8.  Step 0 (alpha
         //    initialised nonzero everywhere) and that rare case evaluate every position.
         if (att_cu) {
+            const float* aold = abuf + (t & 1) * RES_LMAX;
+            float* anew = abuf + ((t & 1) ^ 1) * RES_LMAX;
+            float* candv = scr + 2 * RES_WAVES;
+            const int cx = n >= 2 ? n - 2 : n - 2 + L, clo = n >= 1 ? n - 1 : L - 1, chi = min(n + 2, L - 1);
+            // candidate slot s = tid / 32 (32 lanes x 4 dims): its operands that do not depend on
+            // the query are read before the query arrives
+            const int sl = tid >> 5, sub = tid & 31;
+            const int pos = t > 0 ? res_candidate(sl, n, n_prev, L) : -1;
+            float xvd[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) xvd[m] = xv[sub + 32 * m];
+            const float a_pos = pos >= 0 ? aold[pos] : 0.f, a_prev = pos > 0 ? aold[pos - 1] : 0.f;
             if (wave == 0) {
                 float q4[4];
                 const bool ok = sweep<4>(Gq + (t & 1) * GR_TOTAL, E + 3, q4, [&](int i) { return lane * 4 + i; }, tmo);
@@ -423,29 +435,18 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             __syncthreads();  // A1
             if (flags[1]) break;
             RES_MARK(6);
-            const float* aold = abuf + (t & 1) * RES_LMAX;
-            float* anew = abuf + ((t & 1) ^ 1) * RES_LMAX;
-            float* candv = scr + 2 * RES_WAVES;
-            const int cx = n >= 2 ? n - 2 : n - 2 + L, clo = n >= 1 ? n - 1 : L - 1, chi = min(n + 2, L - 1);
             bool full = t == 0;
+            float rm = -INFINITY;
             if (!full) {
-                // candidate slot s = tid / 32: 32 lanes x 4 dims each, butterfly-summed
-                const int sl = tid >> 5, sub = tid & 31;
-                const int pos = res_candidate(sl, n, n_prev, L);
                 float part = 0.f;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int d = sub + 32 * m;
-                    part += xv[d] * tanh_fast(xq[d] + ptc[m]);
-                }
+                for (int m = 0; m < 4; ++m) part += xvd[m] * tanh_fast(xq[sub + 32 * m] + ptc[m]);
                 const float e = sum32_dpp(part);
                 if (sub == 31) {
                     float v = -INFINITY;
                     if (pos >= 0) {
                         const float sg = sigmoid_fast(e + vb);
-                        const float prev = pos > 0 ? aold[pos - 1] : 0.f;
-                        const float mix =
-                            __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, aold[pos]), __fmul_rn(ufa, prev)), 1e-8f);
+                        const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - ufa, a_pos), __fmul_rn(ufa, a_prev)), 1e-8f);
                         v = __fmul_rn(mix, sg);
                         an[pos] = v;
                     }
@@ -453,14 +454,12 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 }
                 __syncthreads();  // A2
                 RES_MARK(14);
-                float rm = -INFINITY;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const float4 v4 = reinterpret_cast<const float4*>(candv)[k];
                     rm = fmaxf(rm, fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)));
                 }
                 full = !(rm >= 1e-8f);  // uniform
-                if (!full && tid == 0) scr[0] = rm;
             }
             if (full) {
                 // every position: wave w owns dims [16w, 16w + 16), lanes own positions
@@ -493,26 +492,23 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 const float wmax = wave_max_dpp(anj);
                 if (lane == 0) scr[2 * wave + 1] = wmax;
                 __syncthreads();
-                if (tid == 0) {
-                    float rm = -INFINITY;
-                    for (int k = 0; k < RES_WAVES; ++k) rm = fmaxf(rm, scr[2 * k + 1]);
-                    scr[0] = rm;
-                }
+                rm = -INFINITY;
+#pragma unroll
+                for (int k = 0; k < RES_WAVES; ++k) rm = fmaxf(rm, scr[2 * k + 1]);
             }
-            __syncthreads();  // A3: an[] of the window and max(alpha) in LDS
             RES_MARK(7);
-            const float rm = scr[0];
-            float rs = 0.f;  // the surviving window [n-1, n+2] without (n-2) mod L, index order
-            for (int p = clo; p <= chi; ++p)
-                if (p != cx) rs += an[p];
+            // the surviving window [n-1, n+2] without (n-2) mod L: its unnormalised weights once
+            float aw[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) aw[k] = (clo + k <= chi && clo + k != cx) ? an[clo + k] : 0.f;
+            const float rs = ((aw[0] + aw[1]) + aw[2]) + aw[3];  // index order
             const float vx = 0.01f * rm;  // alpha[n-2] = 0.01 * val
             const float denom = rs + vx;
-            // the <= 5 nonzero weights, once: (n-2) mod L and the window [clo, chi]
             const float inv = 1.f / denom;
             const float wcx = vx * inv;
             float ww[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) ww[k] = (clo + k <= chi && clo + k != cx) ? an[clo + k] * inv : 0.f;
+            for (int k = 0; k < 4; ++k) ww[k] = aw[k] * inv;
             auto weight = [&](int p) -> float {
                 if (p == cx) return wcx;
                 return (p >= clo && p <= chi) ? ww[p - clo] : 0.f;
