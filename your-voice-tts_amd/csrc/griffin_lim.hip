@@ -141,6 +141,34 @@ __device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q
     return wss > 1.17549435e-38f ? y / wss : y;
 }
 
+// ola_sample with the <= OLA_MAX contributing frames' loads issued together (the sum still runs
+// frame by frame in index order; absent contributors add exact zeros): bitwise equal to it.
+constexpr int OLA_MAX = 5;  // ceil(win / hop) for the reference geometry (1102 / 275)
+__device__ __forceinline__ float ola_sample_unrolled(const double* __restrict__ fr, int q, int F, const Geo& g,
+                                                     const double* __restrict__ win2) {
+    if (q < g.woff) return 0.f;
+    int ilo = q - g.woff - g.win + 1;
+    ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
+    int ihi = (q - g.woff) / g.hop;
+    if (ihi > F - 1) ihi = F - 1;
+    double fv[OLA_MAX], wv[OLA_MAX];
+#pragma unroll
+    for (int k = 0; k < OLA_MAX; ++k) {
+        const int i = ilo + k;
+        const int o = q - i * g.hop;
+        const bool ok = i <= ihi;
+        fv[k] = ok ? fr[(int64_t)i * g.winp + (o - g.woff)] : 0.0;
+        wv[k] = ok ? win2[o] : 0.0;
+    }
+    float y = 0.f, wss = 0.f;
+#pragma unroll
+    for (int k = 0; k < OLA_MAX; ++k) {
+        y = (float)((double)y + fv[k]);
+        wss = (float)((double)wss + wv[k]);
+    }
+    return wss > 1.17549435e-38f ? y / wss : y;
+}
+
 // ---------------------------------------------------------------- |S|^power
 struct MagArgs {
     int mode;  // TTS_GL_FROM_MEL / TTS_GL_FROM_LINEAR
@@ -207,6 +235,7 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
 struct IterArgs {
     const double* S;      // [B][Fmax][1025]
     const float* y;       // [B][Nmax] the previous iteration's float32 signal (gl_ola_kernel)
+    const double* prev;   // FUSED: the previous iteration's frames (overlap-added here instead)
     int64_t Nmax;
     double* next;         // frames written by this iteration
     const int* F;
@@ -226,7 +255,10 @@ __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
 
-template <bool INIT>
+// FUSED (small batches): the frame's own 2048 STFT input samples are overlap-added from the
+// previous iteration's frames inside this launch (bitwise the values gl_ola_kernel would store),
+// so an iteration is one launch instead of two.
+template <bool INIT, bool FUSED = false>
 __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     const int b = blockIdx.y;
     const int f = xcd_remap(blockIdx.x, gridDim.x);
@@ -270,7 +302,13 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
             const int n = tid + i * GL_THREADS;
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
             wi[i] = sup ? a.c.win[n] : 0.0;
-            yi[i] = sup ? yb[reflect_idx(f * g.hop + n - NFFT / 2, N)] : 0.f;
+            if (FUSED) {
+                const double* fb = a.prev + (int64_t)b * a.Fmax * g.winp;
+                yi[i] = sup ? ola_sample_unrolled(fb, reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2, Fb, g, a.c.win2)
+                            : 0.f;
+            } else {
+                yi[i] = sup ? yb[reflect_idx(f * g.hop + n - NFFT / 2, N)] : 0.f;
+            }
         }
         double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
 #pragma unroll
@@ -523,6 +561,7 @@ struct tts_gl {
     std::map<GraphKey, hipGraphExec_t> graphs;
     float last_ms = 0.f;
     int last_launches = 0;
+    bool last_fused = false;
     bool have_last = false;
     IterArgs last_iter{};
     FinArgs last_fin{};
@@ -677,6 +716,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.y = g->y;
     fa.Nmax = Nmax;
     const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
+    // small batches: overlap-add fused into the iteration launch (one launch per iteration)
+    const bool fused = (int64_t)B * Fmax <= 1024 && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
     if (iters > 0) {
         // one iteration = overlap-add of the previous frames into the float32 signal (every
         // sample once) + one workgroup per frame for STFT -> phase -> iSTFT of that signal
@@ -686,13 +727,18 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             hipGraph_t graph = nullptr;
             TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
             for (int i = 0; i < iters; ++i) {
-                FinArgs o = fa;
-                o.frames = g->frames + (i & 1) * fstride;
-                hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, o);
                 IterArgs a = ia;
                 a.phase_u = nullptr;
                 a.next = g->frames + ((i + 1) & 1) * fstride;
-                hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+                if (fused) {
+                    a.prev = g->frames + (i & 1) * fstride;
+                    hipLaunchKernelGGL((gl_iter_kernel<false, true>), grid, block, 0, s, a);
+                } else {
+                    FinArgs o = fa;
+                    o.frames = g->frames + (i & 1) * fstride;
+                    hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, o);
+                    hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+                }
             }
             hipError_t ce = hipGetLastError();
             hipError_t ee = hipStreamEndCapture(s, &graph);
@@ -716,7 +762,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
     TTS_HIP(hipEventSynchronize(g->ev_t1));
     TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
-    g->last_launches = 2 * iters;
+    g->last_launches = (fused ? 1 : 2) * iters;
+    g->last_fused = fused;
     g->have_last = true;
     g->last_iter = ia;
     g->last_fin = fa;
@@ -740,11 +787,15 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
         IterArgs a = ia;
         a.phase_u = nullptr;
         a.next = g->frames + ((r + 1) & 1) * g->last_fstride;
+        a.prev = f.frames;
         TTS_HIP(hipEventRecord(ev[0], s));
-        hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
+        if (!g->last_fused) hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[1], s));
-        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+        if (g->last_fused)
+            hipLaunchKernelGGL((gl_iter_kernel<false, true>), grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[2], s));
         TTS_HIP(hipEventSynchronize(ev[2]));
