@@ -29,7 +29,14 @@ struct ConvArgs {
     int pool2;           // stage max(in[t], in[t+1]) with in[T_b] = 0: CBHG's ConstantPad1d([0, 1]) +
                          // MaxPool1d(2, stride 1) (layers/tacotron.py:137-139, 188) fused into the next conv
     int out_ld;          // row stride of out / resid in floats (0 = Cout)
+    // optional split-K workspace (>= CONV_SPLITK_FLOATS floats): small launches (batch-1 postnet /
+    // encoder: ~100 output tiles) split the input channels over up to 16 workgroups per tile and
+    // reduce the partial sums in a second launch, in split order (deterministic)
+    float* part;
+    int Ttile;  // frames covered by output tiles (>= max T_b; 0 = Tmax): a caller whose buffers are
+                // sized for a cap (postnet: max_decoder_steps + 20) passes the batch's longest sentence
 };
+constexpr size_t CONV_SPLITK_FLOATS = (size_t)1 << 20;  // split x tiles <= 1024 -> <= 1M partials
 
 constexpr int CONV_BN = 64;  // output channels per tile
 inline int conv_co_pad(int Cout) { return (Cout + CONV_BN - 1) / CONV_BN * CONV_BN; }

@@ -16,8 +16,8 @@ namespace tts {
 
 namespace {
 
-template <int KW, int BM, int WM, int WN>
-__global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
+template <int KW, int BM, int WM, int WN, bool SPLIT = false>
+__global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit = 1, int nb = 1) {
     constexpr int PAD = (KW - 1) / 2;
     constexpr int BK = KW <= 5 ? 16 : (KW <= 8 ? 8 : 4);
     constexpr int NACC = KW <= 5 ? KW : 1;  // accumulator sets (per tap for short kernels)
@@ -28,9 +28,14 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
     // so every XCD works on a fixed set of channel tiles and its L2 keeps their weight slabs
     // (655 KB each at Cin = 512) across all the frame tiles it is given (speed only).
     const int ntl = a.co_pad / BN;
-    const int ntile = blockIdx.x % ntl;
-    const int rest = blockIdx.x / ntl;
-    const int mtiles = (a.Tmax + BM - 1) / BM;
+    const int Tt = a.Ttile ? a.Ttile : a.Tmax;
+    const int mtiles = (Tt + BM - 1) / BM;
+    // split-K: z-th slice of the K steps; the split index is the slowest grid coordinate
+    const int ntiles_all = SPLIT ? (int)(gridDim.x / nsplit) : (int)gridDim.x;
+    const int z = SPLIT ? (int)blockIdx.x / ntiles_all : 0;
+    const int bx = SPLIT ? (int)blockIdx.x % ntiles_all : (int)blockIdx.x;
+    const int ntile = bx % ntl;
+    const int rest = bx / ntl;
     const int b = rest / mtiles;
     const int t0 = (rest % mtiles) * BM;
     const int c0 = ntile * BN;
@@ -107,14 +112,16 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
             }                                                                                                    \
         }                                                                                                        \
     }
-    const int nsteps = a.Cin / BK;
-    CONV_GLOAD(0);
+    const int nsteps_all = a.Cin / BK;
+    const int sbeg = SPLIT ? z * nsteps_all / nsplit : 0;
+    const int send = SPLIT ? (z + 1) * nsteps_all / nsplit : nsteps_all;
+    CONV_GLOAD(sbeg * BK);
     CONV_LSTORE(0);
     __syncthreads();
     const int row = lane & 15, kq = lane >> 4;
-    for (int st = 0; st < nsteps; ++st) {
-        const int cur = st & 1;
-        CONV_GLOAD(min(st + 1, nsteps - 1) * BK);  // the last step reloads itself (unused)
+    for (int st = sbeg; st < send; ++st) {
+        const int cur = (st - sbeg) & 1;
+        CONV_GLOAD(min(st + 1, send - 1) * BK);  // the last step reloads itself (unused)
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
 #pragma unroll
@@ -139,6 +146,25 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a) {
 #undef CONV_GLOAD
 #undef CONV_LSTORE
     // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)
+    if (SPLIT) {
+        // raw partial sums -> part[z][b][t][co_pad]; conv_reduce_kernel applies the epilogue
+        const int64_t pb = ((int64_t)z * nb + b) * Tt;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int t = t0 + wt + i * 16 + (lane >> 4) * 4 + r;
+                    const int co = c0 + wc + j * 16 + (lane & 15);
+                    if (t >= Tb) continue;
+                    float sum = acc[0][i][j][r];
+#pragma unroll
+                    for (int k = 1; k < NACC; ++k) sum += acc[k][i][j][r];
+                    a.part[(pb + t) * a.co_pad + co] = sum;
+                }
+        return;
+    }
     const int ld = a.out_ld ? a.out_ld : a.Cout;
     float* outb = a.out + (int64_t)b * a.Tmax * ld;
     const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * ld : nullptr;
@@ -220,14 +246,52 @@ __global__ void fold_bn_kernel(const float* bias, const float* gamma, const floa
     shift[c] = beta[c] + ((bias ? bias[c] : 0.f) - mean[c]) * sc;
 }
 
+// Split-K epilogue: out[b][t][co] = act(scale * sum_z part[z][b][t][co] + shift) (+ resid), the
+// partials summed in split order.  Rows t >= T_b are left untouched (as the one-pass epilogue).
+__global__ void conv_reduce_kernel(const ConvArgs a, int B, int nsplit) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int Tt = a.Ttile ? a.Ttile : a.Tmax;
+    const int64_t total = (int64_t)B * Tt * a.Cout;
+    if (i >= total) return;
+    const int co = i % a.Cout;
+    const int t = (i / a.Cout) % Tt;
+    const int b = i / ((int64_t)a.Cout * Tt);
+    if (t >= a.T[b]) return;
+    float sum = 0.f;
+    for (int z = 0; z < nsplit; ++z) sum += a.part[(((int64_t)z * B + b) * Tt + t) * a.co_pad + co];
+    float y = a.scale ? sum * a.scale[co] : sum;
+    if (a.shift) y += a.shift[co];
+    if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+    else if (a.act == CONV_TANH) y = tanhf(y);
+    else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
+    const int ld = a.out_ld ? a.out_ld : a.Cout;
+    if (a.resid) y = a.resid[((int64_t)b * a.Tmax + t) * ld + co] + y;
+    a.out[((int64_t)b * a.Tmax + t) * ld + co] = y;
+}
+
 template <int KW>
 hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
     const dim3 block(256);
+    constexpr int BK = KW <= 5 ? 16 : (KW <= 8 ? 8 : 4);
+    const int Tt = a.Ttile ? a.Ttile : a.Tmax;
+    const int tiles = ((Tt + 15) / 16) * (a.co_pad / CONV_BN) * B;
+    if (a.part && a.act != CONV_HIGHWAY && tiles < 256) {
+        // split the K steps so that the launch fills the chip: nsplit x tiles <= 1024
+        const int nsteps = a.Cin / BK;
+        int ns = 1;
+        while (ns * 2 <= 16 && tiles * ns * 2 <= 1024 && nsteps % (ns * 2) == 0 && nsteps / (ns * 2) >= 2) ns *= 2;
+        if (ns > 1 && (size_t)ns * B * Tt * a.co_pad <= CONV_SPLITK_FLOATS) {
+            hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4, true>), dim3(tiles * ns), block, 0, s, a, ns, B);
+            const int64_t total = (int64_t)B * Tt * a.Cout;
+            hipLaunchKernelGGL(conv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, B, ns);
+            return hipGetLastError();
+        }
+    }
     if (frames_hint <= 4096) {
-        const dim3 grid(((a.Tmax + 15) / 16) * (a.co_pad / CONV_BN) * B);
+        const dim3 grid(((Tt + 15) / 16) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4>), grid, block, 0, s, a);
     } else {
-        const dim3 grid(((a.Tmax + 63) / 64) * (a.co_pad / CONV_BN) * B);
+        const dim3 grid(((Tt + 63) / 64) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 64, 2, 2>), grid, block, 0, s, a);
     }
     return hipGetLastError();

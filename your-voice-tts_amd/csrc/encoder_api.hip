@@ -34,6 +34,7 @@ struct tts_encoder {
     float* Whh = nullptr;                // packed [2 directions][64 tiles][16 chunks][64][4]
     int *ids = nullptr, *T = nullptr;
     float *act0 = nullptr, *act1 = nullptr, *xi = nullptr, *h = nullptr, *c = nullptr, *out = nullptr;
+    float* part = nullptr;  // split-K workspace of the convolutions (CONV_SPLITK_FLOATS)
     std::map<std::pair<int, int>, hipGraphExec_t> graphs;
 };
 
@@ -68,6 +69,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.Cout = EDIM;
         a.co_pad = EDIM;
         a.act = CONV_RELU;
+        a.part = e->part;
         TTS_HIP(conv_launch(a, 5, B, frames, s));
     }
     {
@@ -82,6 +84,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.Cout = 2 * EG;
         a.co_pad = 2 * EG;
         a.act = CONV_NONE;
+        a.part = e->part;
         TTS_HIP(conv_launch(a, 1, B, frames, s));
     }
     const int64_t hs = (int64_t)e->Bcap * EH;  // per-direction stride; h slots [2][2][Bcap][H]
@@ -205,6 +208,7 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
     CK(emalloc(e, &e->h, (size_t)4 * max_batch * EH));
     CK(emalloc(e, &e->c, (size_t)2 * max_batch * EH));
     CK(emalloc(e, &e->out, BL * EDIM));
+    CK(emalloc(e, &e->part, CONV_SPLITK_FLOATS));
     HK(hipStreamSynchronize(s));
 #undef CK
 #undef HK

@@ -4,6 +4,8 @@
 // Roofline: MFMA-fp32 bound, 8.68 MFLOP per frame.
 #include <string>
 
+#include <algorithm>
+
 #include "conv1d.h"
 
 using namespace tts;
@@ -18,6 +20,7 @@ struct tts_postnet {
     size_t buf_floats = 0;
     int* T = nullptr;
     int Tcap_B = 0;
+    float* part = nullptr;  // split-K workspace (CONV_SPLITK_FLOATS)
 };
 
 extern "C" {
@@ -31,6 +34,7 @@ void tts_postnet_destroy(tts_postnet* p) {
     }
     for (int i = 0; i < 2; ++i)
         if (p->buf[i]) (void)hipFree(p->buf[i]);
+    if (p->part) (void)hipFree(p->part);
     if (p->T) (void)hipFree(p->T);
     delete p;
 }
@@ -74,7 +78,8 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
         if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, 1e-5f, p->scale[l], p->shift[l], s);
         if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     }
-    hipError_t e = hipStreamSynchronize(s);
+    hipError_t e = hipMalloc(&p->part, CONV_SPLITK_FLOATS * sizeof(float));
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     *out = p;
     return TTS_OK;
@@ -83,10 +88,11 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
 tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, int B, int Tmax, float* out,
                            void* stream) {
     TTS_CHECK(p && mel && T && out && B >= 1 && Tmax >= 1, TTS_ERR_INVALID, "bad postnet_run arguments");
-    int frames = 0;
+    int frames = 0, Tlong = 1;
     for (int b = 0; b < B; ++b) {
         TTS_CHECK(T[b] >= 0 && T[b] <= Tmax, TTS_ERR_INVALID, "T[b] out of range");
         frames += T[b];
+        Tlong = std::max(Tlong, (int)T[b]);
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t need = (size_t)B * Tmax * 512;
@@ -120,6 +126,8 @@ tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, i
         a.Cout = p->cout[l];
         a.co_pad = p->co_pad[l];
         a.act = l < 4 ? CONV_TANH : CONV_NONE;
+        a.part = p->part;
+        a.Ttile = Tlong;
         TTS_HIP(conv_launch(a, 5, B, frames, s));
         in = a.out;
     }
