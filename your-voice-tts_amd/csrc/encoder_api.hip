@@ -12,7 +12,10 @@
 #include <unordered_map>
 #include <vector>
 
+#include <cstdlib>
+
 #include "conv1d.h"
+#include "encoder_resident.h"
 #include "sgemm.h"
 
 using namespace tts;
@@ -36,6 +39,14 @@ struct tts_encoder {
     float *act0 = nullptr, *act1 = nullptr, *xi = nullptr, *h = nullptr, *c = nullptr, *out = nullptr;
     float* part = nullptr;  // split-K workspace of the convolutions (CONV_SPLITK_FLOATS)
     std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+    // resident batch-1 BiLSTM (encoder_resident.h): one launch for the whole recurrence
+    bool resident = false;
+    float4* rw = nullptr;
+    unsigned long long* rgran = nullptr;
+    long long rtmo = 0;
+    unsigned rsalt = 0;
+    int* host_status = nullptr;  // pinned
+    std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
 };
 
 namespace {
@@ -49,7 +60,7 @@ tts_status emalloc(tts_encoder* e, T** p, size_t n) {
     return TTS_OK;
 }
 
-tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s) {
+tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s, bool resident = false) {
     // outputs past L_b and the initial LSTM state are zero
     // outputs past L_b are zero; the initial LSTM state is set outside the graph (tts_encoder_run_state)
     TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
@@ -88,6 +99,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         TTS_HIP(conv_launch(a, 1, B, frames, s));
     }
     const int64_t hs = (int64_t)e->Bcap * EH;  // per-direction stride; h slots [2][2][Bcap][H]
+    if (resident) return TTS_OK;  // the recurrence: enqueue_encoder_resident, launched outside the graph
     for (int st = 0; st < Lmax; ++st) {
         float* h_prev = e->h + (int64_t)((st + 1) & 1) * 2 * hs;
         float* h_next = e->h + (int64_t)(st & 1) * 2 * hs;
@@ -116,6 +128,30 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
     return TTS_OK;
 }
 
+// B = 1: the whole recurrence in one direct launch (per-launch salt); h_0 / c_0 come from slot 1 / c,
+// h_n goes to slot (L-1) & 1 (where tts_encoder_run_state reads it) and c_n to c
+tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, hipStream_t s) {
+    const int64_t hs = (int64_t)e->Bcap * EH;
+    TTS_HIP(hipMemsetAsync(e->rgran, 0, sizeof(unsigned long long) * encoder_resident_granules(), s));
+    EncResArgs a{};
+    a.w = e->rw;
+    a.xi = e->xi;
+    a.L = Lmax;
+    a.hdir = hs;
+    a.h0 = e->h + 2 * hs;
+    a.c0 = e->c;
+    a.h_fin = e->h + (int64_t)((Lmax - 1) & 1) * 2 * hs;
+    a.c_fin = e->c;
+    a.out = e->out;
+    a.gran = e->rgran;
+    a.status = reinterpret_cast<int*>(e->rgran + encoder_resident_granules() - 2);
+    a.tmo = e->rtmo;
+    e->rsalt = (e->rsalt + 1) & 0x3FFFF;
+    a.salt = e->rsalt;
+    TTS_HIP(launch_encoder_resident(a, s));
+    return TTS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -124,6 +160,8 @@ void tts_encoder_destroy(tts_encoder* e) {
     if (!e) return;
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : e->rgraphs) (void)hipGraphExecDestroy(kv.second);
+    if (e->host_status) (void)hipHostFree(e->host_status);
     for (void* p : e->allocs) (void)hipFree(p);
     for (hipEvent_t ev : {e->ev_in, e->ev_out})
         if (ev) (void)hipEventDestroy(ev);
@@ -209,6 +247,23 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
     CK(emalloc(e, &e->c, (size_t)2 * max_batch * EH));
     CK(emalloc(e, &e->out, BL * EDIM));
     CK(emalloc(e, &e->part, CONV_SPLITK_FLOATS));
+    {
+        const char* env = getenv("TTS_RESIDENT");
+        int dev = 0, ncu = 0, rate_khz = 0;
+        if (!(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 128 &&
+            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0) {
+            float* w4 = nullptr;
+            CK(emalloc(e, &w4, encoder_resident_weight_float4() * 4));
+            e->rw = reinterpret_cast<float4*>(w4);
+            CK(emalloc(e, &e->rgran, encoder_resident_granules()));
+            HK(encoder_resident_pack(get("encoder.lstm.weight_hh_l0", (int64_t)EG * EH),
+                                     get("encoder.lstm.weight_hh_l0_reverse", (int64_t)EG * EH), e->rw, s));
+            HK(hipHostMalloc(reinterpret_cast<void**>(&e->host_status), sizeof(int)));
+            e->rtmo = (long long)rate_khz * 50;  // 50 ms per hand-off wait
+            e->resident = true;
+        }
+    }
     HK(hipStreamSynchronize(s));
 #undef CK
 #undef HK
@@ -241,6 +296,36 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * hs, s));
         TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * hs, s));
     }
+    if (e->resident && B == 1 && lens[0] == Lmax) {
+        auto rit = e->rgraphs.find(Lmax);
+        if (rit == e->rgraphs.end()) {
+            hipGraph_t g = nullptr;
+            TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            tts_status st = enqueue_encoder(e, 1, Lmax, Lmax, s, true);
+            hipError_t ee = hipStreamEndCapture(s, &g);
+            if (st) return st;
+            TTS_HIP(ee);
+            hipGraphExec_t exec = nullptr;
+            TTS_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+            TTS_HIP(hipGraphDestroy(g));
+            rit = e->rgraphs.emplace(Lmax, exec).first;
+        }
+        TTS_HIP(hipGraphLaunch(rit->second, s));
+        {
+            tts_status st = enqueue_encoder_resident(e, Lmax, s);
+            if (st) return st;
+        }
+        TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
+                               hipMemcpyDeviceToHost, s));
+        TTS_HIP(hipStreamSynchronize(s));
+        if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
+            e->resident = false;  // rerun below with the per-step launches (same state, untouched)
+        } else {
+            TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP, "resident encoder: a hand-off wait timed out (internal error)");
+            goto done;
+        }
+    }
+    {
     auto key = std::make_pair(B, Lmax);
     auto git = e->graphs.find(key);
     if (git == e->graphs.end()) {
@@ -257,6 +342,8 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         git = e->graphs.emplace(key, exec).first;
     }
     TTS_HIP(hipGraphLaunch(git->second, s));
+    }
+done:
     TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
     if (state_out) {
         // h_n of each direction: sentence b wrote its last state at step L_b - 1 (slot (L_b-1) & 1)

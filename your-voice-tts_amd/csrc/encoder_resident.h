@@ -1,0 +1,31 @@
+// Resident batch-1 encoder BiLSTM (see encoder_resident.hip).
+#pragma once
+#include "common.h"
+
+namespace tts {
+
+constexpr int ENC_RES_STATUS_PLACEMENT = 50;  // fewer than 16 workgroups on CU 0's XCD
+
+struct EncResArgs {
+    const float4* w;     // packed W_hh of both directions (encoder_resident_pack)
+    const float* xi;     // [Tmax][2][1024] input projection + both biases (sentence 0)
+    int L;               // encoder length of the sentence
+    int64_t hdir;        // per-direction stride of h0 / c0 / h_fin / c_fin (floats)
+    const float* h0;     // [2][hdir] initial h (forward, backward) or null (zeros)
+    const float* c0;     // [2][hdir] initial c or null
+    float* h_fin;        // [2][hdir] h_n
+    float* c_fin;        // [2][hdir] c_n
+    float* out;          // [Tmax][512] outputs (rows >= L untouched)
+    unsigned long long* gran;  // encoder_resident_granules() u64, zeroed before every launch
+    int* status;         // 0 ok; ENC_RES_STATUS_PLACEMENT; else a wait timed out
+    long long tmo;       // wall_clock64 ticks per wait
+    unsigned salt;       // per-launch tag salt (18 bits): launched directly, never from a graph,
+                         // so no granule (or stale cache line) of an earlier launch can match
+};
+
+size_t encoder_resident_weight_float4();
+size_t encoder_resident_granules();  // includes the trailing status word
+hipError_t encoder_resident_pack(const float* whh_fwd, const float* whh_bwd, float4* out, hipStream_t s);
+hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s);
+
+}  // namespace tts

@@ -1,0 +1,189 @@
+// Resident batch-1 encoder BiLSTM (Encoder.inference's nn.LSTM, layers/tacotron2.py:56-61, 82):
+// the whole recurrence of both directions as ONE launch instead of L dependent step launches.
+//
+// 256 workgroups are launched; each reads its XCC id and the 256-entry table of all of them, and
+// the first 16 workgroups (by index) of CU 0's XCD take the roles direction = rank / 8, slot =
+// rank % 8; the rest exit.  A role holds W_hh rows of 32 hidden units (x 4 gates, 128 rows x 256,
+// 128 KiB) in VGPRs; thread (row r = tid / 4, k quarter q = tid % 4) owns W_hh[row][64q .. 64q+64).
+// Rows are unit-major (r = 4 u + gate) so the 16 lanes of a unit hold its 4 gate sums after the
+// quad reduction, and one lane per unit updates (c, h) like the sgemm ENC_LSTM epilogue.  Per
+// step every role publishes its 32 h values as 8-byte {tag, value} granules with a
+// workgroup-scope store (the line stays in the XCD's L2) and gathers its direction's 256 values
+// with agent-scope loads: XCD-local hand-offs, no fences.  Waits are bounded (status on timeout).
+#include "encoder_resident.h"
+
+namespace tts {
+namespace {
+
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef __attribute__((address_space(1))) int gint;
+
+constexpr int ER_THREADS = 512;
+constexpr int ER_SLOTS = 8;    // workgroups per direction
+constexpr int ER_UNITS = 32;   // hidden units per workgroup
+constexpr int H = 256, G4 = 4 * H;
+constexpr int GR_TABLE = 0, GR_H = 256;  // granules: table [256], h [2 parity][2 dir][256]
+
+__device__ __forceinline__ void pub_dev(u64* g, unsigned tag, float v) {
+    __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pub_xcd(u64* g, unsigned tag, float v) {
+    __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ u64 peek(u64* g) {
+    return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave: lane l polls granules base + 4l .. 4l+3 until every tag matches
+__device__ __forceinline__ bool sweep4(u64* g, unsigned tag, float (&v)[4], long long tmo) {
+    const int lane = threadIdx.x & 63;
+    long long t_end = 0;
+    for (int spin = 0;; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u64 x = peek(g + lane * 4 + i);
+            v[i] = __uint_as_float((unsigned)x);
+            ok = ok && (unsigned)(x >> 32) == tag;
+        }
+        if (__all(ok)) return true;
+        if (spin == 0) t_end = (long long)wall_clock64() + tmo;
+        else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
+    acc = fmaf(w.x, x.x, acc);
+    acc = fmaf(w.y, x.y, acc);
+    acc = fmaf(w.z, x.z, acc);
+    return fmaf(w.w, x.w, acc);
+}
+
+__global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const EncResArgs a) {
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    __shared__ __align__(16) float hsb[2][H];  // h_{s-1} by step parity (the gather fills the other)
+    __shared__ int info[4];
+    // ---- roles from the XCD table
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const unsigned setup_tag = (a.salt << 14) | 0x3FFFu;
+    if (tid == 0) pub_dev(a.gran + GR_TABLE + c, setup_tag, __int_as_float(xcc));
+    if (wave == 0) {
+        float v[4];
+        const bool ok = sweep4(a.gran + GR_TABLE, setup_tag, v, a.tmo);
+        const int xref = __builtin_amdgcn_readfirstlane(__float_as_int(v[0]) & 7);
+        int rank = 0, nref = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int x = __float_as_int(v[i]) & 7;
+            nref += __popcll(__ballot(x == xref));
+            rank += __popcll(__ballot(x == xref && lane * 4 + i < c));
+        }
+        if (lane == 0) {
+            info[0] = ok ? 1 : 0;
+            info[1] = xcc == xref ? rank : -1;
+            info[2] = nref;
+            info[3] = 0;
+            if (!ok) __hip_atomic_store((gint*)a.status, 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (nref < 2 * ER_SLOTS && c == 0)
+                __hip_atomic_store((gint*)a.status, ENC_RES_STATUS_PLACEMENT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const int role = info[1];
+    if (!info[0] || info[2] < 2 * ER_SLOTS || role < 0 || role >= 2 * ER_SLOTS) return;
+    const int dir = role / ER_SLOTS, slot = role % ER_SLOTS;
+    const int row = tid >> 2, kq = tid & 3;  // row = 4 * unit_local + gate
+    const int ul = row >> 2, gate = row & 3;
+    const int unit = slot * ER_UNITS + ul;
+    float4 w[16];
+    const float4* wp = a.w + ((size_t)(dir * ER_SLOTS + slot) * 16) * ER_THREADS + tid;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = wp[(size_t)i * ER_THREADS];
+    // initial state
+    for (int k = tid; k < H; k += ER_THREADS) hsb[0][k] = a.h0 ? a.h0[dir * a.hdir + k] : 0.f;
+    float cs = 0.f;  // cell of `unit` (lanes with row & 3 == 0 && kq == 0)
+    if (a.c0) cs = a.c0[dir * a.hdir + unit];
+    float hlast = 0.f;
+    const int L = a.L;
+    auto xi_at = [&](int s) -> float {
+        const int pos = dir == 0 ? s : L - 1 - s;
+        return a.xi[(int64_t)pos * (2 * G4) + dir * G4 + gate * H + unit];
+    };
+    float xcur = L > 0 ? xi_at(0) : 0.f;
+    __syncthreads();
+    for (int s = 0; s < L; ++s) {
+        const float xnext = s + 1 < L ? xi_at(s + 1) : 0.f;  // in flight during this step
+        const float* hs = hsb[s & 1];
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc = dot4(w[i], *reinterpret_cast<const float4*>(hs + kq * 64 + 4 * i), acc);
+        // quad sum (k quarters), then gate pre-activation
+        acc += dpp_move<0xB1, 0xf>(acc, 0.f);  // quad_perm [1,0,3,2]
+        acc += dpp_move<0x4E, 0xf>(acc, 0.f);  // quad_perm [2,3,0,1]
+        const float pre = acc + xcur;
+        const float act = gate == 2 ? tanhf(pre) : sigmoidf_(pre);
+        const float f = dpp_move<0x104, 0xf>(act, 0.f);  // row_shl:4  -> gate 1 of this unit
+        const float g = dpp_move<0x108, 0xf>(act, 0.f);  // row_shl:8  -> gate 2
+        const float o = dpp_move<0x10C, 0xf>(act, 0.f);  // row_shl:12 -> gate 3
+        const int par = s & 1;
+        u64* gh = a.gran + GR_H + (par * 2 + dir) * H;
+        if ((tid & 15) == 0) {
+            cs = f * cs + act * g;  // c' = s(f) c + s(i) tanh(g)
+            const float h = o * tanhf(cs);
+            hlast = h;
+            pub_xcd(gh + unit, (a.salt << 14) | (unsigned)(s + 1), h);
+            const int pos = dir == 0 ? s : L - 1 - s;
+            a.out[(int64_t)pos * (2 * H) + dir * H + unit] = h;
+        }
+        xcur = xnext;
+        if (wave == 0) {
+            float v[4];
+            const bool ok = sweep4(gh, (a.salt << 14) | (unsigned)(s + 1), v, a.tmo);
+            if (!ok) {
+                if (lane == 0) __hip_atomic_store((gint*)a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                info[3] = 1;
+            }
+            *reinterpret_cast<float4*>(hsb[(s + 1) & 1] + lane * 4) = float4{v[0], v[1], v[2], v[3]};
+        }
+        __syncthreads();
+        if (info[3] == 1) return;
+    }
+    if ((tid & 15) == 0 && L > 0) {
+        a.h_fin[dir * a.hdir + unit] = hlast;
+        a.c_fin[dir * a.hdir + unit] = cs;
+    }
+}
+
+__global__ void enc_res_pack_kernel(const float* whh_f, const float* whh_b, float4* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)2 * ER_SLOTS * 16 * ER_THREADS) return;
+    const int tid = i % ER_THREADS, i4 = (i / ER_THREADS) % 16, slot = (i / (16 * ER_THREADS)) % ER_SLOTS;
+    const int dir = i / (16 * ER_THREADS * ER_SLOTS);
+    const int row = tid >> 2, kq = tid & 3, ul = row >> 2, gate = row & 3;
+    const int ref = gate * H + slot * ER_UNITS + ul;
+    const float* W = dir ? whh_b : whh_f;
+    const float* p = W + (int64_t)ref * H + kq * 64 + 4 * i4;
+    out[i] = float4{p[0], p[1], p[2], p[3]};
+}
+
+}  // namespace
+
+size_t encoder_resident_weight_float4() { return (size_t)2 * ER_SLOTS * 16 * ER_THREADS; }
+size_t encoder_resident_granules() { return GR_H + 4 * H + 2; }
+
+hipError_t encoder_resident_pack(const float* whh_f, const float* whh_b, float4* out, hipStream_t s) {
+    const int64_t n = (int64_t)encoder_resident_weight_float4();
+    hipLaunchKernelGGL(enc_res_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, whh_f, whh_b, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(encoder_resident_kernel, dim3(256), dim3(ER_THREADS), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace tts
