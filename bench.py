@@ -331,12 +331,17 @@ def main():
         # resident batch-1 decoder: ONE launch runs every step (csrc/resident_decoder.hip), timed
         # with HIP events on the library stream around that launch; otherwise the per-step kernels
         kd = {} if resident else model.profile_step_kernels(reps=50 if not gst else 20)
-        kg = ap.profile_gl_kernels(reps=20)
+        # small batches run every GL iteration after the first in ONE persistent launch
+        # (griffin_lim.hip: gl_persistent_kernel), timed with HIP events around it
+        gl_persistent = ap.last_gl_timing()["gl_iterations"] == 1 and args.iters > 1
+        kg = {} if gl_persistent else ap.profile_gl_kernels(reps=20)
         launches = {k: steps for k in kd}
-        # one GL iteration = overlap-add launch (frames -> float32 signal) + per-frame
-        # STFT/iSTFT launch; priced together against SURVEY 8(d)'s bytes per frame-iteration
-        launches["gl_iter"] = args.iters
-        allk = {**kd, "gl_iter": kg["gl_iter"] + kg["gl_ola"]}
+        allk = dict(kd)
+        if not gl_persistent:
+            # one GL iteration = overlap-add launch (frames -> float32 signal) + per-frame
+            # STFT/iSTFT launch; priced together against SURVEY 8(d)'s bytes per frame-iteration
+            launches["gl_iter"] = args.iters
+            allk["gl_iter"] = kg["gl_iter"] + kg["gl_ola"]
         for k, ms in allk.items():
             kind, alg = (kernel_algorithmic_gst if gst else kernel_algorithmic)(k, B, Lmean, frames_total)
             kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],
@@ -347,6 +352,11 @@ def main():
                                                decoder_steps=steps, us_per_decoder_step=1000 * dec_ms / steps,
                                                algorithmic_bytes=alg, achieved_gbs=alg / (dec_ms * 1e-3) / 1e9,
                                                phases_us_per_step=model.profile_resident_phases())
+        if gl_persistent:
+            alg = GL_BYTES_PER_FRAME_ITER * frames_total * args.iters
+            kernels["gl_persistent"] = dict(mean_ms=gl_ms, launches_per_step=1, ms_per_step=gl_ms,
+                                            gl_iterations=args.iters, us_per_iteration=1000 * gl_ms / args.iters,
+                                            algorithmic_bytes=alg, achieved_gbs=alg / (gl_ms * 1e-3) / 1e9)
         dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
         kdom = kernels[dom]
         traffic = load_traffic(("gst_" if gst else "") + dom)

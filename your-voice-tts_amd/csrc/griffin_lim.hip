@@ -18,6 +18,7 @@
 //   -> store the frame.  Iterations ping-pong the frames buffer (a frame's neighbours still read
 //   the previous iteration), one launch per iteration, replayed from a hipGraph.
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -374,6 +375,212 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- persistent GL loop (small batches)
+// Every GL iteration after the initial one, for all frames, in ONE launch: workgroup (sentence,
+// frame) keeps its iteration-invariant operands (|S| row, window, twiddles, and the overlap-add
+// geometry of its 2048 STFT input samples: contributor offsets and the window sum-square) in
+// registers, and per iteration
+//   waits until every frame it overlap-adds from has published the previous iteration (one
+//   tag word per frame, polled by one wave), overlap-adds its input samples from their frames
+//   (agent-scope loads: the data was written by other CUs in this launch), runs the same
+//   STFT -> S X/|X| -> iSTFT as gl_iter_kernel, stores its frame write-through (sc1) and, after
+//   every storing wave drained, publishes its tag.
+// Every iteration writes a frame slot of its own (never rewritten in the launch): with parity
+// ping-pong, a consumer on another XCD read its L2's copy of the line from two iterations before
+// (sc1 loads bypass L1 but are L2-served; an acquire only drops L1) -- measured nondeterministic
+// 1e-4..1e-2 rel RMS errors.  Every wait is bounded.
+struct PersArgs {
+    IterArgs it;        // S, F, Fmax, B, geometry, constants (y / next / prev unused)
+    double* frames;     // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
+    int64_t fstride;
+    int iters;          // iterations after the initial one
+    int it0;            // first iteration index of this launch (parity of the frames it reads)
+    unsigned* flags;    // [B][Fmax] tag of the last iteration each frame published
+    unsigned salt;      // per launch (18 bits)
+    long long tmo;      // wall_clock64 ticks per wait
+    int* status;
+};
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+typedef __attribute__((address_space(1))) unsigned gu32_t;
+typedef __attribute__((address_space(1))) int gi32_t;
+
+__global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArgs p) {
+    const IterArgs& a = p.it;
+    const int b = blockIdx.y;
+    const int f = xcd_remap(blockIdx.x, gridDim.x);
+    const int Fb = a.F[b];
+    if (f >= Fb) return;
+    const Geo g = a.g;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ __align__(16) double2 buf0[NH];
+    __shared__ __align__(16) double2 buf1[NH];
+    __shared__ __align__(16) double2 X[NB + 1];
+    __shared__ int rng[3];  // contributor frame range lo, hi; abort flag
+    constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;
+    constexpr int PN = NFFT / GL_THREADS;
+    constexpr int PW = (NFFT + GL_THREADS - 1) / GL_THREADS;
+    // ---- iteration-invariant operands
+    const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    const FftTw ftw = load_fft_tw(a.c.tw);
+    double2 tk[PK];
+    double sk[PK];
+#pragma unroll
+    for (int i = 0; i < PK; ++i) {
+        const int k = tid + i * GL_THREADS;
+        tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
+        sk[i] = k < NB ? Sf[k] : 0.0;
+    }
+    double wo[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        const int n = tid + i * GL_THREADS;
+        wo[i] = n < g.win ? a.c.win[g.woff + n] : 0.0;
+    }
+    // STFT input sample i of this thread: n = tid + 256 i; its overlap-add contributors (frame
+    // offsets into one parity's sentence block, -1 = none) and window sum-square, as ola_sample
+    const int N = g.hop * (Fb - 1);
+    double wi[PN];
+    int off[PN][OLA_MAX];
+    float wssv[PN];
+    int flo = Fb, fhi = -1;
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+        const int n = tid + i * GL_THREADS;
+        const bool sup = n >= g.woff && n < g.woff + g.win;
+        wi[i] = sup ? a.c.win[n] : 0.0;
+        const int q = reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2;
+        int ilo = q - g.woff - g.win + 1;
+        ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
+        int ihi = (q - g.woff) / g.hop;
+        if (ihi > Fb - 1) ihi = Fb - 1;
+        const bool any = sup && q >= g.woff;
+        float wss = 0.f;
+#pragma unroll
+        for (int k = 0; k < OLA_MAX; ++k) {
+            const int fi = ilo + k;
+            const int o = q - fi * g.hop;
+            const bool ok = any && fi <= ihi;
+            off[i][k] = ok ? fi * g.winp + (o - g.woff) : -1;
+            wss = (float)((double)wss + (ok ? a.c.win2[o] : 0.0));
+            if (ok) { flo = min(flo, fi); fhi = max(fhi, fi); }
+        }
+        wssv[i] = wss;
+    }
+    if (tid == 0) { rng[0] = Fb; rng[1] = -1; rng[2] = 0; }
+    __syncthreads();
+    if (fhi >= 0) { atomicMin(&rng[0], flo); atomicMax(&rng[1], fhi); }
+    __syncthreads();
+    const int clo = rng[0], chi = rng[1];
+    unsigned* flb = p.flags + (int64_t)b * a.Fmax;
+    if (tid == 0 && chi - clo >= 64) {  // wider than one polling wave (cannot happen for hop >= 64)
+        __hip_atomic_store((gi32_t*)p.status, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        rng[2] = 1;
+    }
+    __syncthreads();
+    if (rng[2]) return;
+    for (int it = p.it0; it < p.it0 + p.iters; ++it) {
+        const double* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
+        double* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
+        if (it > p.it0 && wave == 0) {
+            // the previous iteration of every contributor frame, one lane per frame: its tag is it
+            // or, when that frame already finished this iteration too, it + 1 (never further: the
+            // contributor relation is symmetric, so it waits for this frame before iteration it + 1)
+            const int fr = clo + lane;
+            long long t_end = 0;
+            for (int spin = 0;; ++spin) {
+                bool ok = fr > chi;
+                if (!ok) {
+                    const unsigned v =
+                        __hip_atomic_load((gu32_t*)(flb + fr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = (v >> 14) == p.salt && (int)(v & 0x3FFFu) >= it;
+                }
+                if (__all(ok)) break;
+                if (spin == 0) {
+                    t_end = (long long)wall_clock64() + p.tmo;
+                } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
+                    if (lane == 0) {
+                        __hip_atomic_store((gi32_t*)p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        rng[2] = 1;
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+#if GL_ACQUIRE
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        }
+        __syncthreads();
+        if (rng[2]) return;
+        // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads)
+        double* xr = reinterpret_cast<double*>(buf0);
+#pragma unroll
+        for (int i = 0; i < PN; ++i) {
+            double fv[OLA_MAX];
+#pragma unroll
+            for (int k = 0; k < OLA_MAX; ++k)
+                fv[k] = off[i][k] >= 0 ? __longlong_as_double((long long)__hip_atomic_load(
+                                             (gu64_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                                       : 0.0;
+            float y = 0.f;
+#pragma unroll
+            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + fv[k]);
+            const float yv = wssv[i] > 1.17549435e-38f ? y / wssv[i] : y;
+            xr[tid + i * GL_THREADS] = wi[i] * (double)yv;
+        }
+        __syncthreads();
+        const double2* Z = fft1024<false>(buf0, buf1, ftw);
+#pragma unroll
+        for (int i = 0; i < PK; ++i) {
+            const int k = tid + i * GL_THREADS;
+            if (k >= NB) break;
+            const double2 zk = Z[k & (NH - 1)];
+            const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
+            const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
+            const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};
+            const double2 t = tk[i];
+            const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
+            const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
+            const double r = sqrt(xre * xre + xim * xim);
+            const double s = sk[i];
+            X[k] = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+        }
+        __syncthreads();
+        if (tid == 0) {
+            X[0].y = 0.0;
+            X[NB - 1].y = 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NH / GL_THREADS; ++i) {
+            const int k = tid + i * GL_THREADS;
+            const double2 xk = X[k];
+            const double2 xc = cconj(X[NH - k]);
+            const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
+            const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
+            const double2 O = cmul(D, cconj(tk[i]));
+            buf0[k] = double2{E.x - O.y, E.y + O.x};
+        }
+        __syncthreads();
+        const double2* z = fft1024<true>(buf0, buf1, ftw);
+        const double* zr = reinterpret_cast<const double*>(z);
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            const int n = tid + i * GL_THREADS;
+            if (n < g.win)
+                __hip_atomic_store((gu64_t*)(dst + n),
+                                   (unsigned long long)__double_as_longlong(wo[i] * (zr[g.woff + n] * (1.0 / NH))),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+        __syncthreads();  // ... before one lane signals; the LDS buffers are reused next iteration
+        if (tid == 0)
+            __hip_atomic_store((gu32_t*)(flb + f), (p.salt << 14) | (unsigned)(it + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
 struct FinArgs {
     const double* frames;
@@ -536,6 +743,11 @@ __global__ __launch_bounds__(GL_THREADS) void mel_analysis_kernel(const MelArgs 
     }
 }
 
+bool getenv_off(const char* name) {
+    const char* v = getenv(name);
+    return v && v[0] == '0';
+}
+
 struct GraphKey {
     int B, Fmax, iters;
     bool operator<(const GraphKey& o) const { return std::tie(B, Fmax, iters) < std::tie(o.B, o.Fmax, o.iters); }
@@ -562,6 +774,15 @@ struct tts_gl {
     float last_ms = 0.f;
     int last_launches = 0;
     bool last_fused = false;
+    bool last_persistent = false;
+    unsigned* flags = nullptr;  // persistent loop: [flags_n] tags
+    size_t flags_n = 0;
+    double* pfr = nullptr;      // persistent loop: one frame slot per iteration
+    size_t pfr_n = 0;
+    int* pstatus = nullptr;     // [dev] status of the persistent loop
+    int* host_status = nullptr; // pinned
+    unsigned salt = 0;
+    long long tmo = 0;
     bool have_last = false;
     IterArgs last_iter{};
     FinArgs last_fin{};
@@ -575,8 +796,9 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS})
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr})
         if (p) (void)hipFree(p);
+    if (g->host_status) (void)hipHostFree(g->host_status);
     for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1})
         if (e) (void)hipEventDestroy(e);
     if (g->stream) (void)hipStreamDestroy(g->stream);
@@ -627,6 +849,17 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
         const size_t n = (size_t)NB * cfg->num_mels;
         if ((e = hipMalloc(&g->pinv, n * 8)) != hipSuccess) return fail(e, "hipMalloc");
         if ((e = hipMemcpy(g->pinv, inv_mel_basis, n * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
+    }
+    // persistent GL loop: status word, timeout (50 ms per wait); needs >= 256 compute units
+    {
+        int dev = 0, ncu = 0, rate_khz = 0;
+        if ((e = hipMalloc(&g->pstatus, 16)) != hipSuccess) return fail(e, "hipMalloc");
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&g->host_status), sizeof(int))) != hipSuccess)
+            return fail(e, "hipHostMalloc");
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256 &&
+            hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0)
+            g->tmo = (long long)rate_khz * 50;
     }
     *out = g;
     return TTS_OK;
@@ -691,6 +924,24 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     hipLaunchKernelGGL(gl_magnitude_kernel, dim3((Fmax + MAG_FRAMES - 1) / MAG_FRAMES, B), dim3(256), 0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
+    // small batches: overlap-add fused into the iteration launch (one launch per iteration); at most
+    // 256 frames in all: the whole loop as one persistent launch (one workgroup per frame), whose
+    // iterations write slots of their own: a frame slot is never rewritten inside the launch, so no
+    // XCD's L2 can hold an earlier copy of the bytes an iteration reads
+    const bool fused = (int64_t)B * Fmax <= 1024 && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
+    int frames_total = 0;
+    for (int b = 0; b < B; ++b) frames_total += F[b];
+    const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+    if (persistent) {
+        const size_t need = fstride * (size_t)(iters + 1);
+        if (need > g->pfr_n) {
+            if (g->pfr) TTS_HIP(hipFree(g->pfr));
+            g->pfr = nullptr;
+            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(double)));
+            g->pfr_n = need;
+        }
+    }
+    double* const fr0 = persistent ? g->pfr : g->frames;
     IterArgs ia{};
     ia.S = g->S;
     ia.F = g->F;
@@ -702,7 +953,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.seed = seed;
     ia.y = g->y;
     ia.Nmax = Nmax;
-    ia.next = g->frames;
+    ia.next = fr0;
     const dim3 grid(Fmax, B), block(GL_THREADS);
     hipLaunchKernelGGL(gl_iter_kernel<true>, grid, block, 0, s, ia);
     TTS_HIP(hipGetLastError());
@@ -716,9 +967,41 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.y = g->y;
     fa.Nmax = Nmax;
     const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
-    // small batches: overlap-add fused into the iteration launch (one launch per iteration)
-    const bool fused = (int64_t)B * Fmax <= 1024 && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
-    if (iters > 0) {
+    g->last_persistent = persistent;
+    if (persistent) {
+        if ((size_t)B * Fmax > g->flags_n) {
+            if (g->flags) TTS_HIP(hipFree(g->flags));
+            g->flags = nullptr;
+            TTS_HIP(hipMalloc(&g->flags, sizeof(unsigned) * (size_t)B * Fmax));
+            g->flags_n = (size_t)B * Fmax;
+        }
+        TTS_HIP(hipMemsetAsync(g->pstatus, 0, sizeof(int), s));
+        PersArgs pa{};
+        pa.it = ia;
+        pa.frames = g->pfr;
+        pa.fstride = (int64_t)fstride;
+        pa.iters = iters;
+        pa.flags = g->flags;
+        g->salt = (g->salt + 1) & 0x3FFFF;
+        pa.salt = g->salt;
+        pa.tmo = g->tmo;
+        pa.status = g->pstatus;
+        const char* one = getenv("TTS_GL_PERSIST_ONE");
+        if (!(one && one[0] == '1')) {
+            hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, pa);
+            TTS_HIP(hipGetLastError());
+        } else {  // debug: one iteration per launch (no in-launch hand-offs)
+            for (int i = 0; i < iters; ++i) {
+                PersArgs q = pa;
+                q.it0 = i;
+                q.iters = 1;
+                g->salt = (g->salt + 1) & 0x3FFFF;
+                q.salt = g->salt;
+                hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, q);
+                TTS_HIP(hipGetLastError());
+            }
+        }
+    } else if (iters > 0) {
         // one iteration = overlap-add of the previous frames into the float32 signal (every
         // sample once) + one workgroup per frame for STFT -> phase -> iSTFT of that signal
         GraphKey key{B, Fmax, iters};
@@ -752,7 +1035,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
     TTS_HIP(hipEventRecord(g->ev_t1, s));
-    fa.frames = g->frames + (iters & 1) * fstride;
+    fa.frames = persistent ? g->pfr + (size_t)iters * fstride : g->frames + (iters & 1) * fstride;
     hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, fa);
     TTS_HIP(hipGetLastError());
     hipLaunchKernelGGL(preemph_scan_kernel, dim3(B), dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop,
@@ -762,7 +1045,12 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
     TTS_HIP(hipEventSynchronize(g->ev_t1));
     TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
-    g->last_launches = (fused ? 1 : 2) * iters;
+    g->last_launches = persistent ? 1 : (fused ? 1 : 2) * iters;
+    if (persistent) {
+        TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
+        TTS_HIP(hipStreamSynchronize(s));
+        TTS_CHECK(g->host_status[0] == 0, TTS_ERR_HIP, "persistent Griffin-Lim: a hand-off wait timed out (internal error)");
+    }
     g->last_fused = fused;
     g->have_last = true;
     g->last_iter = ia;
