@@ -150,8 +150,10 @@ def run_step(model, ap, ids, mine, world, seed):
                                     style_mel=style.index_select(0, sel))
         wav = ap.griffin_lim_batch(out["linear"], out["frames"], mode=audiomod._native.TTS_GL_FROM_LINEAR, seed=seed)
     else:
-        out = model.inference_batch([ids[i] for i in mine])
-        wav = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=seed)
+        # ids -> wav in one native call (tts_synth_run): the same stage entry points as
+        # inference_batch + griffin_lim_batch, without the host round trips between them
+        wav, frames = model.synthesize_native([ids[i] for i in mine], ap, seed=seed)
+        out = dict(frames=frames)
     if world > 1:
         # finished waveforms only, gather-v to rank 0 over RCCL (point-to-point, one link per peer)
         rows = [wav[k, :ap.hop_length * (T - 1)] for k, T in enumerate(out["frames"])]

@@ -201,6 +201,23 @@ tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
 #define TTS_GL_KERNELS 2
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels);
 
+/* ---------------------------------------------------------------- whole-sentence synthesis
+ * Replaces utils/synthesis.py:synthesis for Tacotron2 without speakers (model.inference, :50-57,
+ * then ap.inv_mel_spectrogram of the postnet output, :69-77) in ONE call over the handles above:
+ * tts_encoder_run -> tts_decoder_run -> tts_postnet_run -> tts_gl_run (mel mode, device phases
+ * from `seed`), bitwise the same as calling them one by one, without the host round trips in
+ * between.  The handles stay owned by the caller and must outlive the tts_synth. */
+typedef struct tts_synth tts_synth;
+tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_gl* g, int r, int n_mel, int hop,
+                            tts_synth** out);
+void tts_synth_destroy(tts_synth* s);
+/*   ids    [host] int32 [B][Lmax]; lens [host] int32 [B], 2 <= lens[b] <= Lmax
+ *   wav    [dev]  fp64 [B][hop*(Fmax-1)] out, Fmax = max frames[b] (wav_cap = elements available)
+ *   frames [host] int32 [B] out: mel frames of each sentence (decoder steps * r); sentence b's
+ *          waveform is the first hop*(frames[b]-1) samples of its row, the rest zero. */
+tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, int B, int Lmax, int max_steps,
+                         int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames, void* stream);
+
 /* ---------------------------------------------------------------- Tacotron / TacotronGST
  * SURVEY config 5 (config_tacotron_gst.json) and config_tacotron.json: the r-frames-per-step
  * Tacotron family, models/tacotron.py / models/tacotrongst.py. */

@@ -253,3 +253,45 @@ def test_inference_truncated_vs_reference():
     z0 = golden("t2_fwdmask_L12")
     mel, mel_post, _, _ = m.inference(torch.from_numpy(z0["ids"])[None])
     assert rel_rms(mel_post[0].cpu().numpy(), z0["mel_post"]) < MEL_RTOL
+
+
+@pytest.mark.parametrize("coef", [0.97, 0.98, 0.995])
+@pytest.mark.parametrize("F", [17, 100, 300])
+def test_deemphasis_scan_chunks(audio_cfg, coef, F):
+    """The chunk-parallel de-emphasis (griffin_lim.hip: preemph_scan_kernel) vs scipy's sequential
+    lfilter on the same float32 signal: the signal comes from a run with pre-emphasis off (same
+    phases), so the only difference is the recurrence.  0.995 needs more look-back than a tile and
+    takes the one-chunk-per-sentence scan; 17 frames fit one chunk, 100 and 300 span several."""
+    from scipy.signal import lfilter
+    audio = load_pkg("audio")
+    rng = np.random.Generator(np.random.PCG64(F))
+    mel = torch.from_numpy(rng.uniform(0, 1, size=(1, F, 80)).astype(np.float32)).cuda()
+    pu = rng.uniform(0, 1, size=(1, 1025, F))
+    base = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 2, "preemphasis": 0.0})
+    emph = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 2, "preemphasis": coef})
+    y = base.griffin_lim_batch(mel, [F], phase_u=pu).cpu().numpy()[0]
+    wav = emph.griffin_lim_batch(mel, [F], phase_u=pu).cpu().numpy()[0]
+    n = base.hop_length * (F - 1)
+    ref = lfilter([1.0], [1.0, -coef], y[:n])
+    err = np.abs(wav[:n] - ref)
+    bad = np.nonzero(err > 1e-12 * np.max(np.abs(ref)))[0]
+    assert bad.size == 0, (bad.size, bad[:4], bad[-4:], err.max())
+    assert np.all(wav[n:] == 0)
+
+
+@pytest.mark.parametrize("cases", [["t2_fwdmask_L100"], ["t2_fwdmask_L40", "t2_fwdmask_L12", "t2_fwdmask_L100"]])
+def test_synthesize_native_matches_staged(audio_cfg, cases):
+    """tts_synth_run (ids -> wav in one call) is bitwise the staged path: inference_batch, then
+    griffin_lim_batch with the same device-phase seed (batch 1 = resident decoder + persistent GL;
+    a ragged batch 3 = multi-launch decoder + compacted GL input)."""
+    zs = [golden(c) for c in cases]
+    m = _model(golden_flags(zs[0]))
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 10})
+    ids = [z["ids"] for z in zs]
+    wav, frames = m.synthesize_native(ids, ap, seed=5)
+    out = m.inference_batch(ids)
+    ref = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=5)
+    assert frames == out["frames"] == [z["mel"].shape[0] for z in zs]
+    assert wav.shape == ref.shape
+    assert torch.equal(wav, ref)

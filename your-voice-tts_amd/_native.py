@@ -28,6 +28,7 @@ EXPORTS = (
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
     "tts_gl_set_mel_basis", "tts_gl_melspectrogram",
+    "tts_synth_create", "tts_synth_destroy", "tts_synth_run",
     "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
     "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_profile",
     "tts_last_error", "tts_version",
@@ -94,6 +95,11 @@ def _declare(lib):
     lib.tts_gl_set_mel_basis.argtypes = [vp, vp]
     lib.tts_gl_melspectrogram.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int64, vp, ctypes.c_int, vp]
     lib.tts_gl_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    lib.tts_synth_create.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+    lib.tts_synth_destroy.argtypes = [vp]
+    lib.tts_synth_destroy.restype = None
+    lib.tts_synth_run.argtypes = [vp, I32P, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_uint64, vp, ctypes.c_int64, I32P, vp]
     FP = ctypes.POINTER(ctypes.c_float)
     lib.tts_decoder_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_gl_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]

@@ -67,13 +67,17 @@ hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int wid
 // ------------------------------------------------------------------ processed inputs
 // Pt[b][d][j] = sum_k W[d][k] enc[b][j][k]  (inputs_layer, common_layers.py:115-116, tacotron2.py:176)
 // Stored d-major so the per-step energy loop reads it coalesced along j.
+// PJ_POS positions per workgroup (PJ_POS / 2 per thread): enough workgroups to overlap the W row
+// reads (each thread streams its row of W, 8 float4 loads in flight), not one per 16 positions.
+constexpr int PJ_POS = 4;
 template <int ENC_>
 __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, const float* W, int Lmax, int Lcap,
                                                              float* Pt) {
+    constexpr int PT = PJ_POS / 2;
     const int b = blockIdx.y;
-    const int j0 = blockIdx.x * 16;
-    __shared__ __align__(16) float xs[16][ENC_];
-    for (int i = threadIdx.x; i < 16 * ENC_ / 4; i += blockDim.x) {
+    const int j0 = blockIdx.x * PJ_POS;
+    __shared__ __align__(16) float xs[PJ_POS][ENC_];
+    for (int i = threadIdx.x; i < PJ_POS * ENC_ / 4; i += blockDim.x) {
         const int r = i / (ENC_ / 4), c = i % (ENC_ / 4);
         const int j = j0 + r;
         float4 v = float4{0.f, 0.f, 0.f, 0.f};
@@ -83,28 +87,29 @@ __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, c
     __syncthreads();
     const int d = threadIdx.x & 127;
     const int jh = threadIdx.x >> 7;
-    float acc[8];
+    float acc[PT];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int i = 0; i < PT; ++i) acc[i] = 0.f;
     const float4* w4 = reinterpret_cast<const float4*>(W + (int64_t)d * ENC_);
+#pragma unroll 8
     for (int k4 = 0; k4 < ENC_ / 4; ++k4) {
         const float4 w = w4[k4];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 x = reinterpret_cast<const float4*>(&xs[jh * 8 + i][0])[k4];
+        for (int i = 0; i < PT; ++i) {
+            const float4 x = reinterpret_cast<const float4*>(&xs[jh * PT + i][0])[k4];
             acc[i] += w.x * x.x + w.y * x.y + w.z * x.z + w.w * x.w;
         }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int j = j0 + jh * 8 + i;
+    for (int i = 0; i < PT; ++i) {
+        const int j = j0 + jh * PT + i;
         if (j < Lmax) Pt[((int64_t)b * ADIM + d) * Lcap + j] = acc[i];
     }
 }
 
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt,
                                  hipStream_t s, int enc_dim) {
-    const dim3 grid((Lmax + 15) / 16, B);
+    const dim3 grid((Lmax + PJ_POS - 1) / PJ_POS, B);
     if (enc_dim == 512)
         hipLaunchKernelGGL(project_inputs_kernel<512>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
     else if (enc_dim == 256)

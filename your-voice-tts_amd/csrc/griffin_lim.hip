@@ -33,9 +33,11 @@ constexpr int NFFT = 2048;
 constexpr int NB = 1025;  // bins
 constexpr int NH = 1024;  // complex FFT size
 constexpr int GL_THREADS = 256;
-constexpr int MAG_FRAMES = 4;  // frames per workgroup in the magnitude kernel
+constexpr int MAG_KT = 64;  // magnitude kernel tile: bins (one per lane) ...
+constexpr int MAG_FT = 32;  // ... x frames (MAG_FT / 4 per wave)
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_PER = 8;  // samples per thread per scan tile
+constexpr int SCAN_CHUNK = 4096;  // de-emphasis output samples per workgroup
 
 struct Geo {
     int hop, win, woff, winp;  // woff = (NFFT - win) / 2, winp = win rounded up to 4
@@ -176,7 +178,7 @@ struct MagArgs {
     const float* spec;
     int n_in, Fmax;
     const int* F;
-    const double* pinv;  // [1025][n_mels]
+    const double* pinv;  // [n_mels][1025]: pinv(mel basis) transposed (lanes read consecutive bins)
     double* S;
     float min_db, ref_db, power, max_norm;
     int signal_norm, symmetric, clip;
@@ -198,37 +200,55 @@ __device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) {
     return powf(10.f, (d + a.ref_db) * 0.05f);
 }
 
+// Tile = MAG_KT bins x MAG_FT frames per workgroup: the pinv columns of the tile's bins staged in
+// LDS once, the frames' amplitudes (float, as numpy has them) computed into LDS, then lane = bin,
+// each wave MAG_FT / 4 frames, every (bin, frame) dot product summed over mels in order.
 __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
-    const int b = blockIdx.y;
-    const int f0 = blockIdx.x * MAG_FRAMES;
+    const int b = blockIdx.z;
     const int Fb = a.F[b];
+    const int f0 = blockIdx.y * MAG_FT;
     if (f0 >= Fb) return;
-    const int nf = min(MAG_FRAMES, Fb - f0);
+    const int nf = min(MAG_FT, Fb - f0);
     const float* sp = a.spec + ((int64_t)b * a.Fmax + f0) * a.n_in;
     double* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
+    const int tid = threadIdx.x;
+    const int k0 = blockIdx.x * MAG_KT;
     if (a.mode == TTS_GL_FROM_LINEAR) {
         // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160)
-        for (int i = threadIdx.x; i < nf * NB; i += blockDim.x) S[i] = (double)powf(denorm_to_amp(sp[i], a), a.power);
+        for (int i = tid; i < nf * MAG_KT; i += blockDim.x) {
+            const int f = i / MAG_KT, k = k0 + i % MAG_KT;
+            if (k < NB) S[(int64_t)f * NB + k] = (double)powf(denorm_to_amp(sp[(int64_t)f * NB + k], a), a.power);
+        }
         return;
     }
-    __shared__ double amp[MAG_FRAMES][80];
-    for (int i = threadIdx.x; i < MAG_FRAMES * a.n_in; i += blockDim.x) {
+    __shared__ double pw[80][MAG_KT];
+    __shared__ float amp[MAG_FT][80];
+    for (int i = tid; i < a.n_in * MAG_KT; i += blockDim.x) {
+        const int m = i / MAG_KT, kk = i % MAG_KT;
+        pw[m][kk] = k0 + kk < NB ? a.pinv[(int64_t)m * NB + k0 + kk] : 0.0;
+    }
+    for (int i = tid; i < MAG_FT * a.n_in; i += blockDim.x) {
         const int f = i / a.n_in, m = i % a.n_in;
-        amp[f][m] = f < nf ? (double)denorm_to_amp(sp[f * a.n_in + m], a) : 0.0;
+        amp[f][m] = f < nf ? denorm_to_amp(sp[f * a.n_in + m], a) : 0.f;
     }
     __syncthreads();
     // _mel_to_linear: max(1e-10, pinv(M) . S) in float64 (utils/audio.py:64-66), then ** power
-    for (int k = threadIdx.x; k < NB; k += blockDim.x) {
-        const double* pr = a.pinv + (int64_t)k * a.n_in;
-        double acc[MAG_FRAMES];
+    const int lane = tid & 63, wave = tid >> 6, k = k0 + lane;
+    constexpr int FW = MAG_FT / 4;
+    double acc[FW];
 #pragma unroll
-        for (int f = 0; f < MAG_FRAMES; ++f) acc[f] = 0.0;
-        for (int m = 0; m < a.n_in; ++m) {
-            const double w = pr[m];
+    for (int i = 0; i < FW; ++i) acc[i] = 0.0;
+    for (int m = 0; m < a.n_in; ++m) {
+        const double w = pw[m][lane];
 #pragma unroll
-            for (int f = 0; f < MAG_FRAMES; ++f) acc[f] += w * amp[f][m];
+        for (int i = 0; i < FW; ++i) acc[i] += w * (double)amp[wave * FW + i][m];
+    }
+    if (k < NB) {
+#pragma unroll
+        for (int i = 0; i < FW; ++i) {
+            const int f = wave * FW + i;
+            if (f < nf) S[(int64_t)f * NB + k] = pow(fmax(acc[i], 1e-10), (double)a.power);
         }
-        for (int f = 0; f < nf; ++f) S[(int64_t)f * NB + k] = pow(fmax(acc[f], 1e-10), (double)a.power);
     }
 }
 
@@ -602,66 +622,77 @@ __global__ void gl_ola_kernel(const FinArgs a) {
 }
 
 // y[n] = x[n] + c*y[n-1] in float64 (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136).
-// One workgroup per sentence, tiles of SCAN_THREADS*SCAN_PER samples: coalesced tile load into
-// LDS, per-thread serial scan, Hillis-Steele scan of the (c^len, value) carries, coalesced store.
+// Chunk-parallel: workgroup (chunk i, sentence b) writes y[i*chunk, (i+1)*chunk) and starts its scan
+// `look` samples earlier from y = 0: the state it misses is c^look * y, below 1e-22 of |y| (the host
+// picks look from |c|; with look = 0 the one workgroup per sentence scans from sample 0, exactly the
+// recurrence up to rounding order).  A tile of SCAN_THREADS*SCAN_PER samples: per-thread serial scan,
+// then the (c^len, value) carries composed across lanes by shuffles and across waves through LDS.
+__device__ __forceinline__ void scan_combine(double& A, double& Bv, double pa, double pb) {
+    // (pa, pb) precedes (A, Bv): y_out = A (pa y_in + pb) + Bv
+    Bv = fma(pb, A, Bv);
+    A = pa * A;
+}
 __global__ __launch_bounds__(SCAN_THREADS) void preemph_scan_kernel(const float* y, int64_t Nmax, const int* F, int hop,
-                                                                    double coef, int apply, double* wav) {
-    const int b = blockIdx.x;
+                                                                    double coef, int apply, int64_t chunk, int64_t look,
+                                                                    double* wav) {
+    const int b = blockIdx.y;
     const int64_t N = (int64_t)hop * (F[b] - 1);
+    const int64_t o0 = (int64_t)blockIdx.x * chunk;
+    if (o0 >= N) return;
+    const int64_t o1 = o0 + chunk < N ? o0 + chunk : N;
     const float* x = y + (int64_t)b * Nmax;
     double* o = wav + (int64_t)b * Nmax;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (!apply) {
-        for (int64_t i = tid; i < N; i += blockDim.x) o[i] = (double)x[i];
+        for (int64_t i = o0 + tid; i < o1; i += SCAN_THREADS) o[i] = (double)x[i];
         return;
     }
-    constexpr int TILE = SCAN_THREADS * SCAN_PER;
-    __shared__ double tile[TILE];
-    __shared__ double sa[SCAN_THREADS], sb[SCAN_THREADS];
+    constexpr int TILE = SCAN_THREADS * SCAN_PER, NW = SCAN_THREADS / 64;
+    __shared__ double wa[NW], wb[NW];
     double cpow[SCAN_PER + 1];
     cpow[0] = 1.0;
+#pragma unroll
     for (int k = 1; k <= SCAN_PER; ++k) cpow[k] = cpow[k - 1] * coef;
+    const int64_t s0 = o0 - look > 0 ? ((o0 - look) & ~(int64_t)7) : 0;
     double carry = 0.0;  // y at the end of the previous tile
-    for (int64_t t0 = 0; t0 < N; t0 += TILE) {
-        for (int i = tid; i < TILE; i += SCAN_THREADS) tile[i] = t0 + i < N ? (double)x[t0 + i] : 0.0;
-        __syncthreads();
-        // local serial scan of this thread's SCAN_PER samples with zero carry-in
-        double v = 0.0;
-        double loc[SCAN_PER];
+    for (int64_t t0 = s0; t0 < o1; t0 += TILE) {
+        const int64_t base = t0 + (int64_t)tid * SCAN_PER;
+        double v = 0.0, loc[SCAN_PER];
 #pragma unroll
         for (int k = 0; k < SCAN_PER; ++k) {
-            v = tile[tid * SCAN_PER + k] + coef * v;
+            v = (base + k < o1 ? (double)x[base + k] : 0.0) + coef * v;
             loc[k] = v;
         }
-        // inclusive scan of (A, B) pairs, y_end = A * y_in + B; combine (A1,B1) then (A2,B2) = (A1 A2, B1 A2 + B2)
+        // inclusive composition over the lanes of this wave
         double A = cpow[SCAN_PER], Bv = v;
-        for (int off = 1; off < SCAN_THREADS; off <<= 1) {
-            sa[tid] = A;
-            sb[tid] = Bv;
-            __syncthreads();
-            if (tid >= off) {
-                const double pa = sa[tid - off], pb = sb[tid - off];
-                Bv = pb * A + Bv;
-                A = pa * A;
-            }
-            __syncthreads();
-        }
-        // exclusive carry into this thread = inclusive of the previous thread, applied to the tile carry-in
-        sa[tid] = A;
-        sb[tid] = Bv;
-        __syncthreads();
-        const double cin = tid == 0 ? carry : sa[tid - 1] * carry + sb[tid - 1];
-        const double tile_end = sa[SCAN_THREADS - 1] * carry + sb[SCAN_THREADS - 1];
 #pragma unroll
-        for (int k = 0; k < SCAN_PER; ++k) tile[tid * SCAN_PER + k] = loc[k] + cpow[k + 1] * cin;
+        for (int off = 1; off < 64; off <<= 1) {
+            const double pa = __shfl_up(A, off, 64), pb = __shfl_up(Bv, off, 64);
+            if (lane >= off) scan_combine(A, Bv, pa, pb);
+        }
+        if (lane == 63) { wa[wave] = A; wb[wave] = Bv; }
         __syncthreads();
-        for (int i = tid; i < TILE; i += SCAN_THREADS)
-            if (t0 + i < N) o[t0 + i] = tile[i];
+        // every wave composes the waves' totals itself (NW lanes), then takes its carry-in
+        double WA = lane < NW ? wa[lane] : 1.0, WB = lane < NW ? wb[lane] : 0.0;
+#pragma unroll
+        for (int off = 1; off < NW; off <<= 1) {
+            const double qa = __shfl_up(WA, off, 64), qb = __shfl_up(WB, off, 64);
+            if (lane >= off) scan_combine(WA, WB, qa, qb);
+        }
+        const double win_in = wave == 0 ? carry : __shfl(WA, wave - 1, 64) * carry + __shfl(WB, wave - 1, 64);
+        const double tile_end = __shfl(WA, NW - 1, 64) * carry + __shfl(WB, NW - 1, 64);
+        // y entering this thread: compose the lanes before it (exclusive) with the wave's carry-in
+        const double pa = __shfl_up(A, 1, 64), pb = __shfl_up(Bv, 1, 64);
+        const double cin = lane == 0 ? win_in : pa * win_in + pb;
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; ++k) {
+            const int64_t i = base + k;
+            if (i >= o0 && i < o1) o[i] = loc[k] + cpow[k + 1] * cin;
+        }
         carry = tile_end;
-        __syncthreads();
+        __syncthreads();  // wa / wb are rewritten by the next tile
     }
 }
-
 
 // ---------------------------------------------------------------- mel analysis
 // AudioProcessor.melspectrogram (utils/audio.py:146-152) for the GST style wav
@@ -848,7 +879,10 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if (inv_mel_basis) {
         const size_t n = (size_t)NB * cfg->num_mels;
         if ((e = hipMalloc(&g->pinv, n * 8)) != hipSuccess) return fail(e, "hipMalloc");
-        if ((e = hipMemcpy(g->pinv, inv_mel_basis, n * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
+        std::vector<double> pt(n);
+        for (int k = 0; k < NB; ++k)
+            for (int m = 0; m < cfg->num_mels; ++m) pt[(size_t)m * NB + k] = inv_mel_basis[(size_t)k * cfg->num_mels + m];
+        if ((e = hipMemcpy(g->pinv, pt.data(), n * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
     }
     // persistent GL loop: status word, timeout (50 ms per wait); needs >= 256 compute units
     {
@@ -921,7 +955,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ma.signal_norm = g->cfg.signal_norm;
     ma.symmetric = g->cfg.symmetric_norm;
     ma.clip = g->cfg.clip_norm;
-    hipLaunchKernelGGL(gl_magnitude_kernel, dim3((Fmax + MAG_FRAMES - 1) / MAG_FRAMES, B), dim3(256), 0, s, ma);
+    hipLaunchKernelGGL(gl_magnitude_kernel, dim3((NB + MAG_KT - 1) / MAG_KT, (Fmax + MAG_FT - 1) / MAG_FT, B), dim3(256),
+                       0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
     // small batches: overlap-add fused into the iteration launch (one launch per iteration); at most
@@ -976,6 +1011,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             g->flags_n = (size_t)B * Fmax;
         }
         TTS_HIP(hipMemsetAsync(g->pstatus, 0, sizeof(int), s));
+        // tags are salted per handle, and a new handle can get a freed one's flag words: zero them
+        TTS_HIP(hipMemsetAsync(g->flags, 0, sizeof(unsigned) * (size_t)B * Fmax, s));
         PersArgs pa{};
         pa.it = ia;
         pa.frames = g->pfr;
@@ -1038,8 +1075,20 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.frames = persistent ? g->pfr + (size_t)iters * fstride : g->frames + (iters & 1) * fstride;
     hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, fa);
     TTS_HIP(hipGetLastError());
-    hipLaunchKernelGGL(preemph_scan_kernel, dim3(B), dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop,
-                       g->cfg.preemphasis, g->cfg.preemphasis != 0.0 ? 1 : 0, wav);
+    {
+        // de-emphasis chunks: each starts `look` samples early, |c|^look <= 1e-22; one chunk per
+        // sentence (look 0) when that does not fit one scan tile
+        const double c = g->cfg.preemphasis, ac = std::fabs(c);
+        int64_t chunk = SCAN_CHUNK, look = 0;
+        if (ac > 0.0) {
+            const double need = ac < 1.0 ? std::ceil(std::log(1e-22) / std::log(ac)) : 1e30;
+            if (need <= (double)(SCAN_THREADS * SCAN_PER - SCAN_CHUNK - 8)) look = (int64_t)need;
+            else chunk = Nmax;
+        }
+        const dim3 sgrid((unsigned)((Nmax + chunk - 1) / chunk), B);
+        hipLaunchKernelGGL(preemph_scan_kernel, sgrid, dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop, c,
+                           c != 0.0 ? 1 : 0, chunk, look, wav);
+    }
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_out, s));
     TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));

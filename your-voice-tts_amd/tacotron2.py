@@ -63,6 +63,8 @@ class Tacotron2:
         self._params = OrderedDict(
             (k, torch.from_numpy(v)) for k, v in weights.generate(self._spec, seed).items())
         self._native = None  # (decoder handle, postnet handle, key)
+        self._synth = None  # (tts_synth handle, key, AudioProcessor)
+        self._wav_buf = None
         self._enc_state = None  # inference_truncated: encoder BiLSTM state [4, 1, 256] (h_f, h_b, c_f, c_b)
         self._trunc_started = False  # inference_truncated: decoder states carried on the native handle
         self.last_lengths = None
@@ -119,6 +121,9 @@ class Tacotron2:
         self._lstm = None
         self._enc_state = None
         self._trunc_started = False
+        if self._synth is not None:
+            _native.load_library().tts_synth_destroy(self._synth[0])
+            self._synth = None
         if self._native is not None:
             lib = _native.load_library()
             lib.tts_decoder_destroy(self._native[0])
@@ -254,6 +259,53 @@ class Tacotron2:
             text = text.unsqueeze(0)
         out = self.inference_batch([row for row in text.cpu().numpy()], speaker_ids=speaker_ids)
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
+
+    @torch.no_grad()
+    def synthesize_native(self, ids_list, ap, seed=0, iters=None):
+        """utils/synthesis.py:synthesis (model.inference, :50-57 -> ap.inv_mel_spectrogram, :69-77)
+        for a ragged batch in ONE native call (tts_synth_run): encoder -> decoder -> postnet ->
+        Griffin-Lim with device phases from ``seed``, bitwise what inference_batch followed by
+        ap.griffin_lim_batch(mel_post, frames, seed=seed) returns, without the host round trips
+        between the stages.  Returns (wav: CUDA fp64 [B, hop*(Fmax-1)], frames)."""
+        if "speaker_embedding.weight" in self._params:
+            raise ValueError("synthesize_native: speaker embeddings go through inference_batch")
+        lens = [len(x) for x in ids_list]
+        if min(lens) < 2:
+            raise ValueError("encoder length must be >= 2 (common_layers.py:213)")
+        B, Lmax = len(lens), max(lens)
+        lib, hdec, hpost = self._handles(Lmax, B)
+        _, hgl = ap._handle()
+        key = (self._native[2], id(ap), hgl.value if hasattr(hgl, "value") else int(hgl))
+        if self._synth is not None and self._synth[1] != key:
+            lib.tts_synth_destroy(self._synth[0])
+            self._synth = None
+        if self._synth is None:
+            hs = ctypes.c_void_p()
+            _native.check(lib.tts_synth_create(self._native[3], hdec, hpost, hgl, self.n_frames_per_step, 80,
+                                               ap.hop_length, ctypes.byref(hs)), "tts_synth_create")
+            # hold ap: its GL handle must outlive the synth handle
+            self._synth = (hs, key, ap)
+        hs = self._synth[0]
+        max_steps = int(self.decoder.max_decoder_steps)
+        ids = np.zeros((B, Lmax), np.int32)
+        for b, x in enumerate(ids_list):
+            ids[b, :lens[b]] = np.asarray(x, dtype=np.int32)
+        cap = B * ap.hop_length * max_steps * self.n_frames_per_step
+        if self._wav_buf is None or self._wav_buf.numel() < cap:
+            self._wav_buf = torch.empty(cap, dtype=torch.float64, device=self.device)
+        frames = (ctypes.c_int32 * B)()
+        iters = ap.griffin_lim_iters if iters is None else iters
+        _native.check(lib.tts_synth_run(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens), B, Lmax,
+                                        max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
+                                        cap, frames, _native.stream_handle()), "tts_synth_run")
+        frames = [int(f) for f in frames]
+        ms, ns, res = ctypes.c_float(), ctypes.c_int(), ctypes.c_int()
+        lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
+        lib.tts_decoder_last_path(hdec, ctypes.byref(res))
+        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value))
+        self.last_lengths = frames
+        n = ap.hop_length * (max(frames) - 1)
+        return self._wav_buf[:B * n].view(B, n), frames
 
     RESIDENT_PHASES = ("att_early_wait_pre1", "prenet2_row", "wait_prenet2", "att_lstm_prenet", "att_cell_gather",
                        "query_dec_early", "wait_query", "energies_max", "weights_ctx_publish", "next_prefetch",
