@@ -295,3 +295,27 @@ def test_synthesize_native_matches_staged(audio_cfg, cases):
     assert frames == out["frames"] == [z["mel"].shape[0] for z in zs]
     assert wav.shape == ref.shape
     assert torch.equal(wav, ref)
+
+
+def test_synthesize_native_back_to_back(audio_cfg):
+    """tts_synth_run returns once Griffin-Lim is enqueued (the next call's host work and encoder
+    overlap it; its stages run on the synth handle's stream): back-to-back calls with alternating
+    batch shapes, each output taken on the caller's stream right after its call, each bitwise the
+    staged path; then a staged call on the same handles right after a pipelined one."""
+    zs = {c: golden(c) for c in ("t2_fwdmask_L100", "t2_fwdmask_L40", "t2_fwdmask_L12")}
+    m = _model(golden_flags(zs["t2_fwdmask_L100"]))
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
+    seq = [["t2_fwdmask_L100"], ["t2_fwdmask_L40", "t2_fwdmask_L12"], ["t2_fwdmask_L100"], ["t2_fwdmask_L12"]]
+    outs = []
+    for k, cases in enumerate(seq):
+        wav, frames = m.synthesize_native([zs[c]["ids"] for c in cases], ap, seed=20 + k)
+        outs.append((wav.clone(), frames))  # ordered after the call on the caller's stream
+    m.synthesize_native([zs["t2_fwdmask_L40"]["ids"]], ap, seed=99)
+    for k, cases in enumerate(seq):
+        ids = [zs[c]["ids"] for c in cases]
+        out = m.inference_batch(ids)
+        ref = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=20 + k)
+        wav, frames = outs[k]
+        assert frames == out["frames"]
+        assert torch.equal(wav, ref), k

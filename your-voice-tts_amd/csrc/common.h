@@ -25,6 +25,17 @@ tts_status hip_fail(hipError_t e, const char* what, const char* file, int line);
         }                                            \
     } while (0)
 
+// Pipeline mode (tts_synth_run, synth_api.hip; internal, not exported): while set, a stage runs its
+// work on the caller's stream instead of its own (no event hand-off in or out), and leaves the
+// completion checks that would block the host (encoder placement status, Griffin-Lim timing and
+// status) pending for the pipeline to collect at its next synchronisation point.
+void encoder_set_pipeline(tts_encoder* e, bool on);
+// *placement_failed = 1: the resident encoder could not be placed (rerun with per-step launches)
+tts_status encoder_pending_status(tts_encoder* e, int* placement_failed);
+void decoder_set_pipeline(tts_decoder* d, bool on);
+void gl_set_pipeline(tts_gl* g, bool on);
+tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int WAVE = 64;

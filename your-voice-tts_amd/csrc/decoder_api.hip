@@ -64,6 +64,7 @@ struct tts_decoder {
     int* host_flags = nullptr;  // pinned
     std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
+    bool pipeline = false;  // tts_synth_run: work on the caller's stream
     int last_steps = 0;
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
@@ -505,9 +506,11 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         first = std::max(first, std::min(2 * lens[b] + 22, max_steps));
     }
     hipStream_t cs = static_cast<hipStream_t>(stream);
-    hipStream_t s = d->stream;
-    TTS_HIP(hipEventRecord(d->ev_in, cs));
-    TTS_HIP(hipStreamWaitEvent(s, d->ev_in, 0));
+    hipStream_t s = d->pipeline ? cs : d->stream;
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(d->ev_in, cs));
+        TTS_HIP(hipStreamWaitEvent(s, d->ev_in, 0));
+    }
     TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4, B,
                              hipMemcpyDeviceToDevice, s));
     TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
@@ -635,8 +638,10 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                                  (size_t)nmax * Lmax * 4, B, hipMemcpyDeviceToDevice, s));
     // the mel history is written unguarded by done[] (see EPI_MEL_FUSED): zero rows past n_steps
     TTS_HIP(launch_zero_tail(mel, (int64_t)steps_cap * nm, d->n_steps, (int)nm, nmax, B, s));
-    TTS_HIP(hipEventRecord(d->ev_out, s));
-    TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(d->ev_out, s));
+        TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
+    }
     TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
     d->last_steps = run;
     d->last_B = B;
@@ -669,6 +674,7 @@ tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n) {
     TTS_CHECK(d && us && n >= 2 * RES_PHASES, TTS_ERR_INVALID, "bad arguments");
     TTS_CHECK(d->last_resident && d->last_steps > 0, TTS_ERR_INVALID,
               "tts_decoder_resident_phases needs a previous resident tts_decoder_run");
+    TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
     hipStream_t s = d->stream;
     long long* prof = nullptr;
     TTS_HIP(hipMalloc(&prof, sizeof(long long) * 2 * RES_PHASES));
@@ -703,6 +709,7 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
     const int K = TTS_DECODER_STEP_KERNELS;
     hipEvent_t ev[K + 1];
     for (int i = 0; i <= K; ++i) TTS_HIP(hipEventCreate(&ev[i]));
+    TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
     hipStream_t s = d->stream;
     TTS_HIP(launch_decoder_init(d->last_init, s));
     tts_status st = enqueue_prenet_go(d, d->last_B, s);
@@ -724,3 +731,7 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
 }
 
 }  // extern "C"
+
+namespace tts {
+void decoder_set_pipeline(tts_decoder* d, bool on) { d->pipeline = on; }
+}  // namespace tts

@@ -46,6 +46,8 @@ struct tts_encoder {
     long long rtmo = 0;
     unsigned rsalt = 0;
     int* host_status = nullptr;  // pinned
+    bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
+    bool status_pending = false;
     std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
 };
 
@@ -279,9 +281,11 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
     for (int b = 0; b < B; ++b)
         TTS_CHECK(lens[b] >= 1 && lens[b] <= Lmax, TTS_ERR_INVALID, "length out of range [1, Lmax]");
     hipStream_t cs = static_cast<hipStream_t>(stream);
-    hipStream_t s = e->stream;
-    TTS_HIP(hipEventRecord(e->ev_in, cs));
-    TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
+    hipStream_t s = e->pipeline ? cs : e->stream;
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(e->ev_in, cs));
+        TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
+    }
     TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
     TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
     // initial state (h_0, c_0) of both directions: step 0 reads the parity-1 h slots
@@ -317,6 +321,10 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         }
         TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
                                hipMemcpyDeviceToHost, s));
+        if (e->pipeline) {  // the pipeline reads the status at its next synchronisation point
+            e->status_pending = true;
+            goto done;
+        }
         TTS_HIP(hipStreamSynchronize(s));
         if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
             e->resident = false;  // rerun below with the per-step launches (same state, untouched)
@@ -357,10 +365,33 @@ done:
             }
         }
     }
-    TTS_HIP(hipEventRecord(e->ev_out, s));
-    TTS_HIP(hipStreamWaitEvent(cs, e->ev_out, 0));
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(e->ev_out, s));
+        TTS_HIP(hipStreamWaitEvent(cs, e->ev_out, 0));
+    }
     return TTS_OK;
 }
+
+}  // extern "C"
+
+namespace tts {
+void encoder_set_pipeline(tts_encoder* e, bool on) { e->pipeline = on; }
+
+tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
+    *placement_failed = 0;
+    if (!e->status_pending) return TTS_OK;
+    e->status_pending = false;  // the caller synchronised the stream the status copy ran on
+    if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
+        e->resident = false;
+        *placement_failed = 1;
+        return TTS_OK;
+    }
+    TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP, "resident encoder: a hand-off wait timed out (internal error)");
+    return TTS_OK;
+}
+}  // namespace tts
+
+extern "C" {
 
 tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax, float* out,
                            void* stream) {

@@ -791,6 +791,7 @@ struct tts_gl {
     Geo g{};
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+    hipEvent_t ev_done = nullptr;  // end of the last tts_gl_run (its status copy included)
     double *win = nullptr, *win2 = nullptr, *pinv = nullptr, *basis = nullptr;
     int* NS = nullptr;  // mel analysis: samples per sentence
     int NS_cap = 0;
@@ -816,6 +817,8 @@ struct tts_gl {
     long long tmo = 0;
     bool have_last = false;
     IterArgs last_iter{};
+    bool pipeline = false;        // tts_synth_run: caller's stream, completion collected later
+    bool pending = false;         // a pipeline run whose timing / status is not collected yet
     FinArgs last_fin{};
     size_t last_fstride = 0;
 };
@@ -825,12 +828,13 @@ extern "C" {
 void tts_gl_destroy(tts_gl* g) {
     if (!g) return;
     if (g->stream) (void)hipStreamSynchronize(g->stream);
+    if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
                     (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
-    for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1})
+    for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done})
         if (e) (void)hipEventDestroy(e);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -867,6 +871,7 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if ((e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
     if ((e = hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_out, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    if ((e = hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreate(&g->ev_t0)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreate(&g->ev_t1)) != hipSuccess) return fail(e, "event");
     if ((e = hipMalloc(&g->win, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
@@ -899,6 +904,24 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     return TTS_OK;
 }
 
+}  // extern "C"
+
+namespace tts {
+void gl_set_pipeline(tts_gl* g, bool on) { g->pipeline = on; }
+
+tts_status gl_collect(tts_gl* g) {
+    if (!g->pending) return TTS_OK;
+    g->pending = false;
+    TTS_HIP(hipEventSynchronize(g->ev_done));
+    TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
+    if (g->last_persistent)
+        TTS_CHECK(g->host_status[0] == 0, TTS_ERR_HIP, "persistent Griffin-Lim: a hand-off wait timed out (internal error)");
+    return TTS_OK;
+}
+}  // namespace tts
+
+extern "C" {
+
 tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
                       const double* phase_u, uint64_t seed, int iters, double* wav, void* stream) {
     TTS_CHECK(g && spec && F && wav && B >= 1 && Fmax >= 2 && iters >= 0, TTS_ERR_INVALID, "bad gl_run arguments");
@@ -906,9 +929,13 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_CHECK(mode == TTS_GL_FROM_LINEAR || g->pinv, TTS_ERR_INVALID, "mel mode needs inv_mel_basis at create");
     for (int b = 0; b < B; ++b) TTS_CHECK(F[b] >= 2 && F[b] <= Fmax, TTS_ERR_INVALID, "F[b] out of range [2, Fmax]");
     hipStream_t cs = static_cast<hipStream_t>(stream);
-    hipStream_t s = g->stream;
+    hipStream_t s = g->pipeline ? cs : g->stream;
     const Geo geo = g->g;
     const int64_t Nmax = (int64_t)geo.hop * (Fmax - 1);
+    {
+        tts_status pst = gl_collect(g);  // the previous pipeline run, if any (its status, timing)
+        if (pst) return pst;
+    }
     // workspace (grow only; graphs bake the buffer addresses and are dropped when they move)
     const size_t needS = (size_t)B * Fmax * NB, needF = (size_t)2 * B * Fmax * geo.winp, needY = (size_t)B * Nmax;
     bool moved = false;
@@ -921,7 +948,9 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         moved = true;
         return TTS_OK;
     };
-    TTS_HIP(hipStreamSynchronize(s));
+    // the workspace may move below: nothing of this handle may still be in flight (a pipeline
+    // run's stream has been synchronised by its caller before the next run)
+    if (!g->pipeline) TTS_HIP(hipStreamSynchronize(s));
     tts_status st;
     if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, 8))) return st;
     if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, 8))) return st;
@@ -937,8 +966,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
         g->graphs.clear();
     }
-    TTS_HIP(hipEventRecord(g->ev_in, cs));
-    TTS_HIP(hipStreamWaitEvent(s, g->ev_in, 0));
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(g->ev_in, cs));
+        TTS_HIP(hipStreamWaitEvent(s, g->ev_in, 0));
+    }
     TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
     MagArgs ma{};
     ma.mode = mode;
@@ -1090,15 +1121,14 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                            c != 0.0 ? 1 : 0, chunk, look, wav);
     }
     TTS_HIP(hipGetLastError());
-    TTS_HIP(hipEventRecord(g->ev_out, s));
-    TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
-    TTS_HIP(hipEventSynchronize(g->ev_t1));
-    TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
     g->last_launches = persistent ? 1 : (fused ? 1 : 2) * iters;
-    if (persistent) {
-        TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
-        TTS_HIP(hipStreamSynchronize(s));
-        TTS_CHECK(g->host_status[0] == 0, TTS_ERR_HIP, "persistent Griffin-Lim: a hand-off wait timed out (internal error)");
+    if (persistent) TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipEventRecord(g->ev_done, s));
+    if (s != cs) TTS_HIP(hipStreamWaitEvent(cs, g->ev_done, 0));
+    g->pending = true;
+    if (!g->pipeline) {
+        tts_status cst = gl_collect(g);
+        if (cst) return cst;
     }
     g->last_fused = fused;
     g->have_last = true;
@@ -1111,6 +1141,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) {
     TTS_CHECK(g && kernel_ms && n_kernels >= TTS_GL_KERNELS && reps >= 1, TTS_ERR_INVALID, "bad profile arguments");
     TTS_CHECK(g->have_last, TTS_ERR_INVALID, "tts_gl_profile needs a previous tts_gl_run");
+    {
+        tts_status pst = gl_collect(g);
+        if (pst) return pst;
+    }
     hipStream_t s = g->stream;
     hipEvent_t ev[3];
     for (auto& e : ev) TTS_HIP(hipEventCreate(&e));
@@ -1205,6 +1239,10 @@ tts_status tts_gl_melspectrogram(tts_gl* g, const double* wav, const int32_t* N,
 
 tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches) {
     TTS_CHECK(g && loop_ms && launches, TTS_ERR_INVALID, "null argument");
+    {
+        tts_status pst = gl_collect(g);
+        if (pst) return pst;
+    }
     *loop_ms = g->last_ms;
     *launches = g->last_launches;
     return TTS_OK;

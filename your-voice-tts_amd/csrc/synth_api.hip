@@ -3,7 +3,9 @@
 // postnet output, :69-77) for Tacotron2 without speaker embedding.  Every stage is the same entry
 // point the host package binds one by one (same numerics, bitwise); this call only removes the
 // host round trips between them: one H2D of the ids, the decoder's stop-step readback (the
-// sentence length is decided on the device) and the stages' own completion waits.
+// sentence length is decided on the device) and the stages' own completion waits.  The stages
+// run in pipeline mode (common.h) on one stream of this handle, and the call returns once
+// Griffin-Lim is enqueued: the waveform is ready when the caller's stream reaches it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,6 +23,15 @@ struct tts_synth {
     float *enc = nullptr, *mel = nullptr, *stop = nullptr, *post = nullptr, *spec = nullptr;
     size_t ids_n = 0, enc_n = 0, mel_n = 0, stop_n = 0, spec_n = 0;
     std::vector<int32_t> steps;
+    // the whole pipeline runs on this stream (one hand-off in from the caller's, one out); the
+    // call returns once Griffin-Lim is enqueued, so the next call's host work overlaps it
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    // pinned host staging of ids / lens / frames, alternated per call: call k reuses call k-2's
+    // buffer, whose copies completed before call k-1's decoder synchronisation
+    int32_t* pin[2] = {nullptr, nullptr};
+    size_t pin_n[2] = {0, 0};
+    unsigned calls = 0;
 };
 
 namespace {
@@ -33,6 +44,18 @@ tts_status grow(T** p, size_t& have, size_t need) {
     have = need;
     return TTS_OK;
 }
+
+// stages run in pipeline mode (common.h) for the duration of one tts_synth_run
+struct PipelineScope {
+    tts_synth* s;
+    explicit PipelineScope(tts_synth* x) : s(x) { set(true); }
+    ~PipelineScope() { set(false); }
+    void set(bool on) {
+        tts::encoder_set_pipeline(s->e, on);
+        tts::decoder_set_pipeline(s->d, on);
+        tts::gl_set_pipeline(s->g, on);
+    }
+};
 }  // namespace
 
 extern "C" {
@@ -49,14 +72,28 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
     s->r = r;
     s->nmel = n_mel;
     s->hop = hop;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming) != hipSuccess) {
+        tts_synth_destroy(s);
+        tts::set_error("tts_synth_create: stream / event creation failed");
+        return TTS_ERR_HIP;
+    }
     *out = s;
     return TTS_OK;
 }
 
 void tts_synth_destroy(tts_synth* s) {
     if (!s) return;
+    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    (void)tts::gl_collect(s->g);
     for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post, (void*)s->spec})
         if (q) (void)hipFree(q);
+    for (int32_t* q : s->pin)
+        if (q) (void)hipHostFree(q);
+    for (hipEvent_t ev : {s->ev_in, s->ev_out})
+        if (ev) (void)hipEventDestroy(ev);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
 
@@ -65,9 +102,16 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
     TTS_CHECK(s && ids && lens && wav && frames && B >= 1 && Lmax >= 2 && max_steps >= 1 && gl_iters >= 0,
               TTS_ERR_INVALID, "bad synth arguments");
     hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t ss = s->stream;
     const int cap = max_steps + 21;  // decoder steps_cap (>= max_steps + 20)
     const size_t T = (size_t)cap * s->r;
     tts_status st;
+    // buffers are only (re)allocated with nothing of this pipeline in flight
+    const bool regrow = (size_t)B * Lmax > s->ids_n || (size_t)B * Lmax * 512 > s->enc_n ||
+                        (size_t)B * T * s->nmel > s->mel_n || (size_t)B * cap > s->stop_n;
+    const int par = s->calls & 1;
+    const size_t pin_need = (size_t)B * Lmax + 2 * (size_t)B;
+    if (regrow || pin_need > s->pin_n[par]) TTS_HIP(hipStreamSynchronize(ss));
     if ((st = grow(&s->ids, s->ids_n, (size_t)B * Lmax))) return st;
     if ((st = grow(&s->enc, s->enc_n, (size_t)B * Lmax * 512))) return st;
     if ((st = grow(&s->mel, s->mel_n, (size_t)B * T * s->nmel))) return st;
@@ -81,29 +125,56 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
         TTS_HIP(hipMalloc(&s->spec, s->mel_n * sizeof(float)));
         s->spec_n = s->mel_n;
     }
-    TTS_HIP(hipMemcpyAsync(s->ids, ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, cs));
-    if ((st = tts_encoder_run(s->e, s->ids, lens, B, Lmax, s->enc, cs))) return st;
+    if (pin_need > s->pin_n[par]) {
+        if (s->pin[par]) TTS_HIP(hipHostFree(s->pin[par]));
+        s->pin[par] = nullptr;
+        TTS_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->pin[par]), pin_need * sizeof(int32_t)));
+        s->pin_n[par] = pin_need;
+    }
+    ++s->calls;
+    int32_t* h_ids = s->pin[par];
+    int32_t* h_lens = h_ids + (size_t)B * Lmax;
+    int32_t* h_frames = h_lens + B;
+    std::copy(ids, ids + (size_t)B * Lmax, h_ids);
+    std::copy(lens, lens + B, h_lens);
+
+    PipelineScope scope(s);
+    TTS_HIP(hipEventRecord(s->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(ss, s->ev_in, 0));
+    TTS_HIP(hipMemcpyAsync(s->ids, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
     s->steps.assign(B, 0);
-    if ((st = tts_decoder_run(s->d, s->enc, lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr, s->steps.data(),
-                              cs)))
-        return st;
+    for (int attempt = 0;; ++attempt) {
+        if ((st = tts_encoder_run(s->e, s->ids, h_lens, B, Lmax, s->enc, ss))) return st;
+        // synchronises ss: the encoder's placement status is then readable
+        if ((st = tts_decoder_run(s->d, s->enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr,
+                                  s->steps.data(), ss)))
+            return st;
+        int rerun = 0;
+        if ((st = tts::encoder_pending_status(s->e, &rerun))) return st;
+        if (!rerun) break;
+        TTS_CHECK(attempt == 0, TTS_ERR_HIP, "encoder rerun failed (internal error)");
+    }
     int Fmax = 0;
     for (int b = 0; b < B; ++b) {
-        frames[b] = s->steps[b] * s->r;
-        Fmax = std::max(Fmax, (int)frames[b]);
+        h_frames[b] = s->steps[b] * s->r;
+        Fmax = std::max(Fmax, (int)h_frames[b]);
     }
     TTS_CHECK(Fmax >= 2, TTS_ERR_INVALID, "a sentence decoded to fewer than 2 frames");
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
-    if ((st = tts_postnet_run(s->p, s->mel, frames, B, (int)T, s->post, cs))) return st;
+    std::copy(h_frames, h_frames + B, frames);
+    if ((st = tts_postnet_run(s->p, s->mel, h_frames, B, (int)T, s->post, ss))) return st;
     const float* spec = s->post;
     if (B > 1) {  // GL input is [B][Fmax][nmel]: compact the rows of each sentence; shorter
                   // sentences leave their waveform tail unwritten: zero it
         const size_t row = (size_t)s->nmel * sizeof(float);
-        TTS_HIP(hipMemcpy2DAsync(s->spec, Fmax * row, s->post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, cs));
+        TTS_HIP(hipMemcpy2DAsync(s->spec, Fmax * row, s->post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, ss));
         spec = s->spec;
-        TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), cs));
+        TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), ss));
     }
-    return tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, frames, B, Fmax, nullptr, seed, gl_iters, wav, cs);
+    if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, ss))) return st;
+    TTS_HIP(hipEventRecord(s->ev_out, ss));
+    TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+    return TTS_OK;
 }
 
 }  // extern "C"
