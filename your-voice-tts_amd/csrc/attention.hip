@@ -67,17 +67,30 @@ hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int wid
 // ------------------------------------------------------------------ processed inputs
 // Pt[b][d][j] = sum_k W[d][k] enc[b][j][k]  (inputs_layer, common_layers.py:115-116, tacotron2.py:176)
 // Stored d-major so the per-step energy loop reads it coalesced along j.
-// PJ_POS positions per workgroup (PJ_POS / 2 per thread): enough workgroups to overlap the W row
-// reads (each thread streams its row of W, 8 float4 loads in flight), not one per 16 positions.
-constexpr int PJ_POS = 4;
+// Workgroup = 32 attention dims x PJ_POS positions; each dim's 512-long dot products are split over
+// 8 adjacent lanes (K slices of ENC_ / 8, every W load of a lane issued at once) and reduced with
+// xor shuffles in a fixed order: a short dependency chain per thread instead of one W row streamed
+// serially.  Grid (ADIM / 32 dim groups x position tiles, B).
+constexpr int PJ_POS = 8;
+constexpr int PJ_KS = 8;   // K slices per dim
+constexpr int PJ_DG = 32;  // dims per workgroup
 template <int ENC_>
 __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, const float* W, int Lmax, int Lcap,
                                                              float* Pt) {
-    constexpr int PT = PJ_POS / 2;
+    constexpr int KQ = ENC_ / 4 / PJ_KS;  // float4 per lane
     const int b = blockIdx.y;
-    const int j0 = blockIdx.x * PJ_POS;
+    const int dg = blockIdx.x % (ADIM / PJ_DG);
+    const int j0 = (blockIdx.x / (ADIM / PJ_DG)) * PJ_POS;
+    const int tid = threadIdx.x, ks = tid & (PJ_KS - 1), d = dg * PJ_DG + (tid >> 3);
     __shared__ __align__(16) float xs[PJ_POS][ENC_];
-    for (int i = threadIdx.x; i < PJ_POS * ENC_ / 4; i += blockDim.x) {
+    const float4* w4 = reinterpret_cast<const float4*>(W + (int64_t)d * ENC_) + ks * KQ;
+    float4 w[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) w[q] = w4[q];
+    constexpr int XL = PJ_POS * ENC_ / 4 / 256;
+#pragma unroll
+    for (int t = 0; t < XL; ++t) {
+        const int i = tid + t * 256;
         const int r = i / (ENC_ / 4), c = i % (ENC_ / 4);
         const int j = j0 + r;
         float4 v = float4{0.f, 0.f, 0.f, 0.f};
@@ -85,31 +98,32 @@ __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, c
         reinterpret_cast<float4*>(&xs[r][0])[c] = v;
     }
     __syncthreads();
-    const int d = threadIdx.x & 127;
-    const int jh = threadIdx.x >> 7;
-    float acc[PT];
+    float acc[PJ_POS];
 #pragma unroll
-    for (int i = 0; i < PT; ++i) acc[i] = 0.f;
-    const float4* w4 = reinterpret_cast<const float4*>(W + (int64_t)d * ENC_);
-#pragma unroll 8
-    for (int k4 = 0; k4 < ENC_ / 4; ++k4) {
-        const float4 w = w4[k4];
+    for (int i = 0; i < PJ_POS; ++i) {
+        acc[i] = 0.f;
 #pragma unroll
-        for (int i = 0; i < PT; ++i) {
-            const float4 x = reinterpret_cast<const float4*>(&xs[jh * PT + i][0])[k4];
-            acc[i] += w.x * x.x + w.y * x.y + w.z * x.z + w.w * x.w;
+        for (int q = 0; q < KQ; ++q) {
+            const float4 x = reinterpret_cast<const float4*>(&xs[i][0])[ks * KQ + q];
+            acc[i] += w[q].x * x.x + w[q].y * x.y + w[q].z * x.z + w[q].w * x.w;
         }
     }
 #pragma unroll
-    for (int i = 0; i < PT; ++i) {
-        const int j = j0 + jh * PT + i;
-        if (j < Lmax) Pt[((int64_t)b * ADIM + d) * Lcap + j] = acc[i];
-    }
+    for (int o = 1; o < PJ_KS; o <<= 1)
+#pragma unroll
+        for (int i = 0; i < PJ_POS; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
+    // every lane of the 8 holds the same sums (the xor butterfly adds commutative pairs); lane ks
+    // stores position ks
+    float v = acc[0];
+#pragma unroll
+    for (int i = 1; i < PJ_POS; ++i) v = ks == i ? acc[i] : v;
+    if (j0 + ks < Lmax) Pt[((int64_t)b * ADIM + d) * Lcap + j0 + ks] = v;
 }
+static_assert(PJ_POS == PJ_KS, "one stored position per K-slice lane");
 
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt,
                                  hipStream_t s, int enc_dim) {
-    const dim3 grid((Lmax + PJ_POS - 1) / PJ_POS, B);
+    const dim3 grid((ADIM / PJ_DG) * ((Lmax + PJ_POS - 1) / PJ_POS), B);
     if (enc_dim == 512)
         hipLaunchKernelGGL(project_inputs_kernel<512>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
     else if (enc_dim == 256)

@@ -109,6 +109,52 @@ __device__ double2* fft1024(double2* src, double2* dst, const FftTw& tw) {
     return src;
 }
 
+// fft1024 with register edges: thread j enters with z[j + 256 r] (r = 0..3) in v -- the operands of
+// its first radix-4 butterfly (Ns = 1, untwiddled) -- so the first pass reads no LDS; with TO_REGS
+// the last pass (Ns = 256, whose outputs of thread j are z[j + 256 r] again) leaves its results in v
+// instead of LDS (returns null).  Same operations in the same order as fft1024: bitwise equal.
+// Pass 0 writes `dst`; the caller's previous readers of both buffers must have passed a barrier.
+template <bool INV, bool TO_REGS>
+__device__ double2* fft1024_regs(double2 (&v)[4], double2* src, double2* dst, const FftTw& tw) {
+    const int j = threadIdx.x;
+#pragma unroll
+    for (int Ns = 1, p = -1; Ns < NH; Ns *= 4, ++p) {
+        const int k = j & (Ns - 1);
+        if (Ns > 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = src[j + r * 256];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) {
+                double2 w = tw.w[p][r - 1];
+                if (INV) w = cconj(w);
+                v[r] = cmul(v[r], w);
+            }
+        }
+        const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
+        const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
+        const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
+        const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
+        const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
+        v[0] = double2{a0.x + a2.x, a0.y + a2.y};
+        v[1] = double2{a1.x + m3.x, a1.y + m3.y};
+        v[2] = double2{a0.x - a2.x, a0.y - a2.y};
+        v[3] = double2{a1.x - m3.x, a1.y - m3.y};
+        if (TO_REGS && Ns == NH / 4) return nullptr;  // idxD = j: v[r] is z[j + 256 r]
+        const int idxD = (j / Ns) * Ns * 4 + k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[idxD + r * Ns] = v[r];
+        __syncthreads();
+        double2* t = src;
+        src = dst;
+        dst = t;
+    }
+    return src;
+}
+
+// Real sample i (0..7) of thread j at the register edges of fft1024_regs: complex point j + 256 (i/2),
+// real part (i even) or imaginary part (i odd) = real sample 2 j + 512 (i/2) + (i & 1).
+__device__ __forceinline__ int edge_sample(int j, int i) { return 2 * j + 512 * (i >> 1) + (i & 1); }
+
 // Bijective XCD-aware remap: consecutive logical frames share an XCD (their OLA gathers
 // re-read each other's frames through that XCD's L2).  Speed only, never correctness.
 __device__ __forceinline__ int xcd_remap(int bid, int n) {
@@ -223,13 +269,29 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     }
     __shared__ double pw[80][MAG_KT];
     __shared__ float amp[MAG_FT][80];
-    for (int i = tid; i < a.n_in * MAG_KT; i += blockDim.x) {
-        const int m = i / MAG_KT, kk = i % MAG_KT;
-        pw[m][kk] = k0 + kk < NB ? a.pinv[(int64_t)m * NB + k0 + kk] : 0.0;
+    // fixed trip counts (n_in <= 80): every staging load of the tile is in flight at once
+    constexpr int PWL = 80 * MAG_KT / 256, AML = MAG_FT * 80 / 256;
+    double pv[PWL];
+    float sv[AML];
+#pragma unroll
+    for (int j = 0; j < PWL; ++j) {
+        const int i = tid + j * 256, m = i / MAG_KT, kk = i % MAG_KT;
+        pv[j] = m < a.n_in && k0 + kk < NB ? a.pinv[(int64_t)m * NB + k0 + kk] : 0.0;
     }
-    for (int i = tid; i < MAG_FT * a.n_in; i += blockDim.x) {
-        const int f = i / a.n_in, m = i % a.n_in;
-        amp[f][m] = f < nf ? denorm_to_amp(sp[f * a.n_in + m], a) : 0.f;
+#pragma unroll
+    for (int j = 0; j < AML; ++j) {
+        const int i = tid + j * 256, f = i / 80, m = i % 80;
+        sv[j] = f < nf && m < a.n_in ? sp[f * a.n_in + m] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < PWL; ++j) {
+        const int i = tid + j * 256;
+        pw[i / MAG_KT][i % MAG_KT] = pv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < AML; ++j) {
+        const int i = tid + j * 256, f = i / 80, m = i % 80;
+        amp[f][m] = f < nf && m < a.n_in ? denorm_to_amp(sv[j], a) : 0.f;
     }
     __syncthreads();
     // _mel_to_linear: max(1e-10, pinv(M) . S) in float64 (utils/audio.py:64-66), then ** power
@@ -304,12 +366,12 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
         sk[i] = k < NB ? Sf[k] : 0.0;
     }
-    constexpr int PW = (NFFT + GL_THREADS - 1) / GL_THREADS;  // output samples per thread (<= 8)
-    double wo[PW];
+    // synthesis window at this thread's output samples (the register edge of the inverse FFT)
+    double wo[PN];
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-        const int n = tid + i * GL_THREADS;
-        wo[i] = n < g.win ? a.c.win[g.woff + n] : 0.0;
+    for (int i = 0; i < PN; ++i) {
+        const int m = edge_sample(tid, i), n = m - g.woff;
+        wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
     }
 
     if (!INIT) {
@@ -320,7 +382,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         float yi[PN];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
-            const int n = tid + i * GL_THREADS;
+            const int n = edge_sample(tid, i);  // the first butterfly's operands stay in registers
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
             wi[i] = sup ? a.c.win[n] : 0.0;
             if (FUSED) {
@@ -331,11 +393,10 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
                 yi[i] = sup ? yb[reflect_idx(f * g.hop + n - NFFT / 2, N)] : 0.f;
             }
         }
-        double* xr = reinterpret_cast<double*>(buf0);  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
+        double2 v[4];  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
 #pragma unroll
-        for (int i = 0; i < PN; ++i) xr[tid + i * GL_THREADS] = wi[i] * (double)yi[i];
-        __syncthreads();
-        const double2* Z = fft1024<false>(buf0, buf1, ftw);
+        for (int r = 0; r < 4; ++r) v[r] = double2{wi[2 * r] * (double)yi[2 * r], wi[2 * r + 1] * (double)yi[2 * r + 1]};
+        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
         // real-FFT split; the STFT value is stored complex64 (librosa stft dtype) and its phase
         // exp(i angle(X)) (angle(0) = 0) is applied to |S| in float64 (utils/audio.py:187-188)
 #pragma unroll
@@ -351,7 +412,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
             const double r = sqrt(xre * xre + xim * xim);
             const double s = sk[i];
-            X[k] = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+            double2 xv = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+            if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
+            X[k] = xv;
         }
     } else {
         // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183)
@@ -363,16 +426,13 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
             sincos(2.0 * M_PI * u, &sn, &cs);
-            X[k] = double2{sk[i] * cs, sk[i] * sn};
+            X[k] = double2{sk[i] * cs, (k == 0 || k == NB - 1) ? 0.0 : sk[i] * sn};
         }
     }
     __syncthreads();
-    // ---- inverse real FFT (istft: ifft of the Hermitian-extended spectrum, .real => Im X_0 = Im X_N/2 = 0)
-    if (tid == 0) {
-        X[0].y = 0.0;
-        X[NB - 1].y = 0.0;
-    }
-    __syncthreads();
+    // ---- inverse real FFT (istft: ifft of the Hermitian-extended spectrum, .real => Im X_0 = Im X_N/2 = 0,
+    // set where X is written); the first butterfly's operands z[tid + 256 i] stay in registers
+    double2 v[4];
 #pragma unroll
     for (int i = 0; i < NH / GL_THREADS; ++i) {
         const int k = tid + i * GL_THREADS;
@@ -381,17 +441,17 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
         const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
         const double2 O = cmul(D, cconj(tk[i]));
-        buf0[k] = double2{E.x - O.y, E.y + O.x};  // E + i O
+        v[i] = double2{E.x - O.y, E.y + O.x};  // E + i O
     }
-    __syncthreads();
-    const double2* z = fft1024<true>(buf0, buf1, ftw);
-    // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft)
+    fft1024_regs<true, true>(v, buf0, buf1, ftw);
+    // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft), from
+    // the last butterfly's registers
     double* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
-    const double* zr = reinterpret_cast<const double*>(z);
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-        const int n = tid + i * GL_THREADS;
-        if (n < g.win) out[n] = wo[i] * (zr[g.woff + n] * (1.0 / NH));
+    for (int i = 0; i < PN; ++i) {
+        const int n = edge_sample(tid, i) - g.woff;
+        const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
+        if (n >= 0 && n < g.win) out[n] = wo[i] * (zv * (1.0 / NH));
     }
 }
 
@@ -438,7 +498,6 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     __shared__ int rng[3];  // contributor frame range lo, hi; abort flag
     constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;
     constexpr int PN = NFFT / GL_THREADS;
-    constexpr int PW = (NFFT + GL_THREADS - 1) / GL_THREADS;
     // ---- iteration-invariant operands
     const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     const FftTw ftw = load_fft_tw(a.c.tw);
@@ -450,13 +509,13 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
         sk[i] = k < NB ? Sf[k] : 0.0;
     }
-    double wo[PW];
+    double wo[PN];  // synthesis window at this thread's output samples (edge_sample)
 #pragma unroll
-    for (int i = 0; i < PW; ++i) {
-        const int n = tid + i * GL_THREADS;
-        wo[i] = n < g.win ? a.c.win[g.woff + n] : 0.0;
+    for (int i = 0; i < PN; ++i) {
+        const int m = edge_sample(tid, i), n = m - g.woff;
+        wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
     }
-    // STFT input sample i of this thread: n = tid + 256 i; its overlap-add contributors (frame
+    // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors (frame
     // offsets into one parity's sentence block, -1 = none) and window sum-square, as ola_sample
     const int N = g.hop * (Fb - 1);
     double wi[PN];
@@ -465,7 +524,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     int flo = Fb, fhi = -1;
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
-        const int n = tid + i * GL_THREADS;
+        const int n = edge_sample(tid, i);
         const bool sup = n >= g.woff && n < g.woff + g.win;
         wi[i] = sup ? a.c.win[n] : 0.0;
         const int q = reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2;
@@ -533,8 +592,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         }
         __syncthreads();
         if (rng[2]) return;
-        // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads)
-        double* xr = reinterpret_cast<double*>(buf0);
+        // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads),
+        // straight into the first butterfly's registers
+        double2 v[4];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             double fv[OLA_MAX];
@@ -547,10 +607,10 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
 #pragma unroll
             for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + fv[k]);
             const float yv = wssv[i] > 1.17549435e-38f ? y / wssv[i] : y;
-            xr[tid + i * GL_THREADS] = wi[i] * (double)yv;
+            if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
+            else v[i >> 1].x = wi[i] * (double)yv;
         }
-        __syncthreads();
-        const double2* Z = fft1024<false>(buf0, buf1, ftw);
+        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
             const int k = tid + i * GL_THREADS;
@@ -564,12 +624,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
             const double r = sqrt(xre * xre + xim * xim);
             const double s = sk[i];
-            X[k] = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
-        }
-        __syncthreads();
-        if (tid == 0) {
-            X[0].y = 0.0;
-            X[NB - 1].y = 0.0;
+            double2 xv = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+            if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
+            X[k] = xv;
         }
         __syncthreads();
 #pragma unroll
@@ -580,17 +637,16 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
             const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
             const double2 O = cmul(D, cconj(tk[i]));
-            buf0[k] = double2{E.x - O.y, E.y + O.x};
+            v[i] = double2{E.x - O.y, E.y + O.x};
         }
-        __syncthreads();
-        const double2* z = fft1024<true>(buf0, buf1, ftw);
-        const double* zr = reinterpret_cast<const double*>(z);
+        fft1024_regs<true, true>(v, buf0, buf1, ftw);
 #pragma unroll
-        for (int i = 0; i < PW; ++i) {
-            const int n = tid + i * GL_THREADS;
-            if (n < g.win)
+        for (int i = 0; i < PN; ++i) {
+            const int n = edge_sample(tid, i) - g.woff;
+            const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
+            if (n >= 0 && n < g.win)
                 __hip_atomic_store((gu64_t*)(dst + n),
-                                   (unsigned long long)__double_as_longlong(wo[i] * (zr[g.woff + n] * (1.0 / NH))),
+                                   (unsigned long long)__double_as_longlong(wo[i] * (zv * (1.0 / NH))),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
