@@ -328,6 +328,8 @@ struct IterArgs {
     GLConst c;
     const double* phase_u;  // initial iSTFT only: [B][1025][Fmax] or null (device RNG)
     unsigned long long seed;
+    unsigned* zero_flags;   // initial iSTFT only: the persistent loop's tag words to clear, or null
+    int* zero_status;       // ... and its status word
 };
 
 __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned long long idx) {
@@ -349,6 +351,10 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     if (f >= Fb) return;
     const Geo g = a.g;
     const int tid = threadIdx.x;
+    if (INIT && tid == 0) {  // the persistent loop that follows reads tags of frames < F[b] only
+        if (a.zero_flags) a.zero_flags[(int64_t)b * a.Fmax + f] = 0u;
+        if (a.zero_status && (b | f) == 0) *a.zero_status = 0;
+    }
     __shared__ __align__(16) double2 buf0[NH];
     __shared__ __align__(16) double2 buf1[NH];
     __shared__ __align__(16) double2 X[NB + 1];
@@ -410,9 +416,12 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
             const double2 t = tk[i];
             const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
-            const double r = sqrt(xre * xre + xim * xim);
+            // unit phase X / |X| by one reciprocal square root (the float-rounded components
+            // square exactly in double): no divisions on the iteration's critical path
+            const double m2 = xre * xre + xim * xim;
+            const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
             const double s = sk[i];
-            double2 xv = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+            double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
             if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
             X[k] = xv;
         }
@@ -622,9 +631,12 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double2 t = tk[i];
             const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
-            const double r = sqrt(xre * xre + xim * xim);
+            // unit phase X / |X| by one reciprocal square root (the float-rounded components
+            // square exactly in double): no divisions on the iteration's critical path
+            const double m2 = xre * xre + xim * xim;
+            const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
             const double s = sk[i];
-            double2 xv = r > 0.0 ? double2{s * (xre / r), s * (xim / r)} : double2{s, 0.0};
+            double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
             if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
             X[k] = xv;
         }
@@ -1076,8 +1088,22 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.y = g->y;
     ia.Nmax = Nmax;
     ia.next = fr0;
+    if (persistent) {
+        if ((size_t)B * Fmax > g->flags_n) {
+            if (g->flags) TTS_HIP(hipFree(g->flags));
+            g->flags = nullptr;
+            TTS_HIP(hipMalloc(&g->flags, sizeof(unsigned) * (size_t)B * Fmax));
+            g->flags_n = (size_t)B * Fmax;
+        }
+        // tags are salted per handle, and a new handle can get a freed one's flag words: the
+        // initial iSTFT launch zeroes them and the status word
+        ia.zero_flags = g->flags;
+        ia.zero_status = g->pstatus;
+    }
     const dim3 grid(Fmax, B), block(GL_THREADS);
     hipLaunchKernelGGL(gl_iter_kernel<true>, grid, block, 0, s, ia);
+    ia.zero_flags = nullptr;
+    ia.zero_status = nullptr;
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_t0, s));
     FinArgs fa{};
@@ -1091,15 +1117,6 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
     g->last_persistent = persistent;
     if (persistent) {
-        if ((size_t)B * Fmax > g->flags_n) {
-            if (g->flags) TTS_HIP(hipFree(g->flags));
-            g->flags = nullptr;
-            TTS_HIP(hipMalloc(&g->flags, sizeof(unsigned) * (size_t)B * Fmax));
-            g->flags_n = (size_t)B * Fmax;
-        }
-        TTS_HIP(hipMemsetAsync(g->pstatus, 0, sizeof(int), s));
-        // tags are salted per handle, and a new handle can get a freed one's flag words: zero them
-        TTS_HIP(hipMemsetAsync(g->flags, 0, sizeof(unsigned) * (size_t)B * Fmax, s));
         PersArgs pa{};
         pa.it = ia;
         pa.frames = g->pfr;
