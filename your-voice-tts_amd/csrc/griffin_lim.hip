@@ -18,6 +18,7 @@
 //   -> store the frame.  Iterations ping-pong the frames buffer (a frame's neighbours still read
 //   the previous iteration), one launch per iteration, replayed from a hipGraph.
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <tuple>
@@ -488,6 +489,8 @@ struct PersArgs {
     unsigned salt;      // per launch (18 bits)
     long long tmo;      // wall_clock64 ticks per wait
     int* status;
+    long long* prof;    // diagnostic (TTS_GL_PHASES): per-phase wall_clock64 ticks of frame prof_f, or null
+    int prof_f;
 };
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned gu32_t;
@@ -566,6 +569,15 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     }
     __syncthreads();
     if (rng[2]) return;
+    const bool timed = p.prof && f == p.prof_f && b == 0 && tid == 0;
+    long long ph[6] = {0, 0, 0, 0, 0, 0};
+    long long tp = timed ? (long long)wall_clock64() : 0;
+#define GL_PHASE(k)                                      \
+    if (timed) {                                         \
+        const long long tn = (long long)wall_clock64(); \
+        ph[k] += tn - tp;                                \
+        tp = tn;                                         \
+    }
     for (int it = p.it0; it < p.it0 + p.iters; ++it) {
         const double* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
         double* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
@@ -601,6 +613,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         }
         __syncthreads();
         if (rng[2]) return;
+        GL_PHASE(0)
         // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads),
         // straight into the first butterfly's registers
         double2 v[4];
@@ -619,7 +632,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
             else v[i >> 1].x = wi[i] * (double)yv;
         }
+        GL_PHASE(1)
         const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
+        GL_PHASE(2)
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
             const int k = tid + i * GL_THREADS;
@@ -641,6 +656,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             X[k] = xv;
         }
         __syncthreads();
+        GL_PHASE(3)
 #pragma unroll
         for (int i = 0; i < NH / GL_THREADS; ++i) {
             const int k = tid + i * GL_THREADS;
@@ -652,6 +668,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             v[i] = double2{E.x - O.y, E.y + O.x};
         }
         fft1024_regs<true, true>(v, buf0, buf1, ftw);
+        GL_PHASE(4)
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             const int n = edge_sample(tid, i) - g.woff;
@@ -666,7 +683,11 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         if (tid == 0)
             __hip_atomic_store((gu32_t*)(flb + f), (p.salt << 14) | (unsigned)(it + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        GL_PHASE(5)
     }
+#undef GL_PHASE
+    if (timed)
+        for (int k = 0; k < 6; ++k) p.prof[k] = ph[k];
 }
 
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
@@ -1127,6 +1148,14 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         pa.salt = g->salt;
         pa.tmo = g->tmo;
         pa.status = g->pstatus;
+        long long* prof = nullptr;
+        const char* phases = getenv("TTS_GL_PHASES");
+        if (phases && phases[0]) {  // diagnostic: phase ticks of frame TTS_GL_PHASES (stderr)
+            TTS_HIP(hipMalloc(&prof, 6 * sizeof(long long)));
+            TTS_HIP(hipMemsetAsync(prof, 0, 6 * sizeof(long long), s));
+            pa.prof = prof;
+            pa.prof_f = std::min(atoi(phases), frames_total - 1);
+        }
         const char* one = getenv("TTS_GL_PERSIST_ONE");
         if (!(one && one[0] == '1')) {
             hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, pa);
@@ -1141,6 +1170,19 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                 hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, q);
                 TTS_HIP(hipGetLastError());
             }
+        }
+        if (prof) {
+            long long h[6];
+            TTS_HIP(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s));
+            TTS_HIP(hipStreamSynchronize(s));
+            TTS_HIP(hipFree(prof));
+            int rate_khz = 100000, dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev);
+            static const char* names[6] = {"wait", "ola_loads", "fwd_fft", "spectrum", "inv_fft", "store_publish"};
+            fprintf(stderr, "TTS_GL_PHASES frame %d, us per iteration:", pa.prof_f);
+            for (int k = 0; k < 6; ++k) fprintf(stderr, " %s %.3f", names[k], h[k] * 1e3 / rate_khz / iters);
+            fprintf(stderr, "\n");
         }
     } else if (iters > 0) {
         // one iteration = overlap-add of the previous frames into the float32 signal (every
