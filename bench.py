@@ -71,6 +71,12 @@ def decoder_step_algorithmic(B, L):
     return 4 * 18183458 + 4 * B * L * 640 + 4 * B * (3 * 1024 + 2 * 1024 + 512 + 80 + L)
 
 
+def decoder_step_flops(L):
+    """fp32 flops of one sentence-step (2 x 18 166 864 weight MACs + the attention's
+    1 280 per encoder position) — 36.46 MFLOP at L=100."""
+    return 2 * 18166864 + 1280 * L
+
+
 def kernel_algorithmic_gst(name, B, L, frames_total, r=5):
     """Algorithmic bytes per launch of the TacotronGST decoder-step kernels (weights once per batch
     step + per-sentence activations) and of the GL iteration."""
@@ -152,13 +158,30 @@ def run_step(model, ap, ids, mine, world, seed):
     else:
         # ids -> wav in one native call (tts_synth_run): the same stage entry points as
         # inference_batch + griffin_lim_batch, without the host round trips between them
-        wav, frames = model.synthesize_native([ids[i] for i in mine], ap, seed=seed)
+        wav, frames = model.synthesize_native([ids[i] for i in mine], ap, seed=seed, sync=False)
         out = dict(frames=frames)
     if world > 1:
         # finished waveforms only, gather-v to rank 0 over RCCL (point-to-point, one link per peer)
         rows = [wav[k, :ap.hop_length * (T - 1)] for k, T in enumerate(out["frames"])]
         sharding.gather_waveforms(rows, mine, len(ids))
     return out["frames"], wav
+
+
+def _cpu_model():
+    """lscpu's model name and the logical CPUs this process may run on."""
+    name = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                name = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except Exception:
+        avail = os.cpu_count()
+    return f"{name} ({avail} logical CPUs available to this process)"
 
 
 def _threads():
@@ -189,7 +212,7 @@ def cpu_baseline_gst(args):
     ap.inv_spectrogram(res["linear"].T)
     dt = time.time() - t0
     T = res["mel"].shape[0]
-    return dict(value=T / dt, unit="mel-frames/s", cores=int(_threads()), kind="port",
+    return dict(value=T / dt, unit="mel-frames/s", cores=int(_threads()), kind="port", cpu_model=_cpu_model(),
                 sample=f"1 config-5 sentence (L={L}, {T} frames): numpy oracle TacotronGST (fp32) + linear GL "
                        f"{args.iters} iters (fp64, scipy.fftpack) on the host, {dt:.1f} s",
                 rtf=dt / (275 * (T - 1) / 22050.0))
@@ -220,10 +243,21 @@ def cpu_baseline(args, seconds_target=12.0):
         if time.time() - t0 >= seconds_target or n >= 8:
             break
     dt = time.time() - t0
+    # configs[0]: the reference's own CPU case, synthesize.py with 30-iteration Griffin-Lim, one sentence
+    ap30 = AudioOracle(**{**cfg.audio, "griffin_lim_iters": 30})
+    t1 = time.time()
+    r30 = o.inference(ids)
+    np.random.seed(0)
+    ap30.inv_mel_spectrogram(r30["mel_post"].T)
+    d30 = time.time() - t1
+    T30 = r30["mel"].shape[0]
     return dict(value=frames / dt, unit="mel-frames/s", cores=int(threads), kind="port",
                 sample=f"{n} x one L={args.L} sentence ({res['mel'].shape[0]} frames): numpy oracle decoder+postnet "
-                       f"(fp32) + GL {args.iters} iters (fp64, scipy.fftpack) on the host, {dt:.1f} s",
-                rtf=dt / (n * 275 * (res["mel"].shape[0] - 1) / 22050.0))
+                       f"(fp32, BLAS on {threads} threads) + GL {args.iters} iters (fp64, scipy.fftpack, "
+                       f"single-threaded) on the host, {dt:.1f} s",
+                rtf=dt / (n * 275 * (res["mel"].shape[0] - 1) / 22050.0), cpu_model=_cpu_model(),
+                configs0=dict(value=T30 / d30, unit="mel-frames/s", seconds=d30, rtf=d30 / (275 * (T30 - 1) / 22050.0),
+                              sample=f"configs[0]: one L={args.L} sentence ({T30} frames), GL 30 iters, same port"))
 
 
 def load_traffic(kernel):
@@ -238,61 +272,148 @@ def load_traffic(kernel):
     return None
 
 
-def main():
-    ap_ = argparse.ArgumentParser()
-    ap_.add_argument("--gpus", type=int, default=1)
-    ap_.add_argument("--steps", type=int, default=10)
-    ap_.add_argument("--warmup", type=int, default=3)
-    ap_.add_argument("--batch", type=int, default=1)
-    ap_.add_argument("--L", type=int, default=100)
-    ap_.add_argument("--lengths", choices=["fixed", "uniform"], default="fixed")
-    ap_.add_argument("--iters", type=int, default=60)
-    ap_.add_argument("--no-cpu-baseline", action="store_true")
-    ap_.add_argument("--no-profile", action="store_true")
-    ap_.add_argument("--model", choices=["tacotron2", "gst"], default="tacotron2")
-    args = ap_.parse_args()
+def _sync(device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
 
-    cfg, model, ap = build(args, device)
-    all_ids, mine = make_job(args, world, rank, model.decoder.max_decoder_steps)
-    ids = [all_ids[i] for i in mine]
-
+def timed_region(step, args, world, device, hop, sr):
+    """W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier + device sync on both
+    sides; the MAX elapsed over ranks, the SUM of frames / audio seconds over ranks (driver contract).
+    ``step(seed)`` runs one step and returns this rank's per-sentence frame counts."""
     for w in range(args.warmup):
-        run_step(model, ap, all_ids, mine, world, seed=w)
-    torch.cuda.synchronize()
+        step(w)
+    _sync(device)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(device)
     t0 = time.perf_counter()
-    frames = None
+    frames = []
     for k in range(args.steps):
-        frames, _ = run_step(model, ap, all_ids, mine, world, seed=1000 + k)
-    torch.cuda.synchronize()
+        frames = step(1000 + k)
+    _sync(device)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(device)
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     nfr = torch.tensor([float(sum(frames))], dtype=torch.float64, device=device)
-    aud = torch.tensor([sum(ap.hop_length * (f - 1) for f in frames) / ap.sample_rate], dtype=torch.float64,
-                       device=device)
+    aud = torch.tensor([sum(hop * (f - 1) for f in frames) / sr], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(nfr)
         dist.all_reduce(aud)
     elapsed = float(t.item())
     frames_per_step = float(nfr.item())
-    audio_s_per_step = float(aud.item())
-    ms_per_step = 1000.0 * elapsed / args.steps
-    value = frames_per_step * args.steps / elapsed
-    rtf = (elapsed / args.steps) / audio_s_per_step
+    return dict(elapsed=elapsed, frames_per_step=frames_per_step, ms_per_step=1000.0 * elapsed / args.steps,
+                value=frames_per_step * args.steps / elapsed, rtf=(elapsed / args.steps) / float(aud.item()))
+
+
+def proxy_main(args, world, rank):
+    """CPU rehearsal of the multi-rank bench (``--backend gloo --proxy``): the same launcher, rank
+    environment, configs[3] job + LPT share, timed region and gather-v of finished waveforms, with
+    each sentence's waveform replaced by a deterministic stand-in of its length.  Tests the plumbing
+    only: the line it prints carries ``"proxy": true`` and is not a measurement."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
+    cpu = torch.device("cpu")
+    all_ids, mine = make_job(args, world, rank, 1000)
+    hop = 275
+
+    def step(seed):
+        frames = [sharding.sentence_cost(len(all_ids[i]), 1000) for i in mine]
+        rows = [torch.from_numpy(np.random.Generator(np.random.PCG64(i)).standard_normal(hop * (T - 1)))
+                for i, T in zip(mine, frames)]
+        if world > 1:
+            sharding.gather_waveforms(rows, mine, len(all_ids))
+        return frames
+
+    tm = timed_region(step, args, world, cpu, hop, 22050)
+    if rank == 0:
+        print(json.dumps({"metric": "proxy (launcher rehearsal, not a measurement)", "value": tm["value"],
+                          "unit": "mel-frames/s", "n_gpus": world,
+                          "world_size_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": tm["ms_per_step"], "proxy": True,
+                          "config": {"sentences_per_gpu": args.batch, "sentences_total": len(all_ids),
+                                     "frames_per_step": tm["frames_per_step"], "lengths": args.lengths}}))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc, argv):
+    """``--gpus N`` without a launcher around us: start torch.distributed.run with N ranks on this
+    node as a CHILD process (nothing here has touched the GPU yet) and return its exit code; every
+    rank re-enters this script with RANK / LOCAL_RANK / WORLD_SIZE set (reference process-per-GPU
+    launcher: distribute.py:129-167)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
+    ap_ = argparse.ArgumentParser()
+    ap_.add_argument("--gpus", type=int, default=1)
+    ap_.add_argument("--steps", type=int, default=10)
+    ap_.add_argument("--warmup", type=int, default=3)
+    ap_.add_argument("--batch", type=int, default=None,
+                     help="sentences per rank (default: 1 = configs[1] at N=1, 64 = configs[3] at N>1)")
+    ap_.add_argument("--L", type=int, default=100)
+    ap_.add_argument("--lengths", choices=["fixed", "uniform"], default=None,
+                     help="fixed L (configs[1]) or L ~ U{60..160} (configs[2]/[3]); default by N")
+    ap_.add_argument("--iters", type=int, default=60)
+    ap_.add_argument("--no-cpu-baseline", action="store_true")
+    ap_.add_argument("--no-profile", action="store_true")
+    ap_.add_argument("--model", choices=["tacotron2", "gst"], default="tacotron2")
+    ap_.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                     help="gloo + --proxy: CPU rehearsal of the launcher / partition / gather (no GPU)")
+    ap_.add_argument("--proxy", action="store_true",
+                     help="replace the GPU synthesis by a deterministic stand-in waveform per sentence "
+                          "(launcher test only: the printed value is not a measurement)")
+    args = ap_.parse_args(argv)
+    if args.batch is None:
+        args.batch = 32 if args.model == "gst" else (64 if args.gpus > 1 else 1)
+    if args.lengths is None:
+        args.lengths = "uniform" if args.batch > 1 else "fixed"
+    return args
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.proxy:
+        return proxy_main(args, world, rank)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(args.backend, device_id=device if args.backend == "nccl" else None)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+
+    cfg, model, ap = build(args, device)
+    all_ids, mine = make_job(args, world, rank, model.decoder.max_decoder_steps)
+    ids = [all_ids[i] for i in mine]
+
+    timing = timed_region(lambda seed: run_step(model, ap, all_ids, mine, world, seed=seed)[0], args, world, device,
+                          ap.hop_length, ap.sample_rate)
+    elapsed, frames_per_step, ms_per_step, value, rtf = (timing[k] for k in ("elapsed", "frames_per_step",
+                                                                           "ms_per_step", "value", "rtf"))
 
     if rank != 0:
         if world > 1:
@@ -368,6 +489,21 @@ def main():
         roofline = dict(bound="hbm", kernel=dom, achieved=kdom["achieved_gbs"], peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=kdom["achieved_gbs"] / HBM_PEAK_GBS, traffic=traffic,
                         algorithmic_bytes_per_launch=kdom["algorithmic_bytes"], mean_launch_ms=kdom["mean_ms"])
+        if traffic:
+            roofline["traffic_over_algorithmic"] = traffic / kdom["algorithmic_bytes"]
+        if dom == "resident_decoder":
+            # the SURVEY 8(d) HBM figure prices a weight stream the resident kernel never does (its
+            # weights stay in VGPRs / LDS): state what actually bounds it
+            flops = decoder_step_flops(Lmean) * steps
+            ph = kdom["phases_us_per_step"]["cu0"]
+            edges = {k: ph[k] for k in ("att_early_wait_pre1", "att_cell_gather", "dec_cell_gather")}
+            us = kdom["us_per_decoder_step"]
+            roofline["diagnostics"] = dict(
+                limiter="device-wide hand-off latency (3 all-to-all edges per step); weights on chip",
+                fp32_flops_per_launch=flops, fp32_tflops=flops / (dec_ms * 1e-3) / 1e12,
+                fp32_compute_frac=flops / (dec_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF,
+                device_wide_edges_us_per_step=edges, handoff_floor_us_per_step=sum(edges.values()),
+                us_per_step=us, handoff_share_of_step=sum(edges.values()) / us)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -377,14 +513,25 @@ def main():
                     f"4 speakers, linear GL {args.iters} iters")
     elif args.batch == 1:
         workload = f"configs[1]: Tacotron2 single sentence, HIP decoder loop + HIP Griffin-Lim {args.iters} iters"
+    elif world > 1 and args.lengths == "uniform":
+        workload = (f"configs[3]: Tacotron2, {len(all_ids)} sentences (L ~ U{{60..160}}, seed 3) LPT-sharded "
+                    f"{args.batch} per GPU over {world} GPUs, GL {args.iters} iters, RCCL gather-v to rank 0")
+    elif args.batch == 64 and args.lengths == "uniform":
+        workload = f"configs[2]: Tacotron2 batch=64, L ~ U{{60..160}} (seed 2), GL {args.iters} iters"
     else:
         workload = f"Tacotron2 batch={args.batch} per GPU, {args.lengths} lengths"
+    paths = dict(decoder=("resident" if model.last_timing.get("resident") else "multi-launch") if not gst
+                 else "multi-launch",
+                 encoder_bilstm=("resident" if model.last_timing.get("encoder_resident") else "per-step")
+                 if not gst else "per-step",
+                 griffin_lim=ap.last_gl_path())
     rec = {
         "metric": ("mel-frames/sec + RTF, TacotronGST + 60-iter Griffin-Lim (configs[4])" if gst else
                    "mel-frames/sec + RTF, Tacotron2 + 60-iter Griffin-Lim, LJSpeech"),
         "value": value,
         "unit": "mel-frames/s",
         "n_gpus": world,
+        "world_size_seen": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -405,6 +552,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "stages_rank0": stages,
+        "paths_rank0": paths,
         "kernels_rank0": kernels,
     }
     print(json.dumps(rec))

@@ -64,6 +64,10 @@ tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* le
 tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
                                  const float* state_in, float* state_out, float* out, void* stream);
 
+/* 1 if the last run's BiLSTM took the resident (one co-resident launch) path, 0 for the per-step
+ * launches (batches, or a device where the resident grid cannot be co-resident). */
+tts_status tts_encoder_last_path(tts_encoder* e, int* resident);
+
 /* Decoder flags: the arguments of layers/tacotron2.py:98-100 (Decoder.__init__) that change
  * inference numerics, as mapped from the JSON config by utils/generic_utils.py:275-288. */
 typedef struct tts_decoder_config {
@@ -194,6 +198,15 @@ tts_status tts_gl_melspectrogram(tts_gl* g, const double* wav, const int32_t* N,
 /* Time of the last tts_gl_run's iteration loop (ms, GPU) and kernel launches in it. */
 tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
 
+/* Iteration loop the last tts_gl_run took: TTS_GL_PATH_UNFUSED (overlap-add launch + per-frame
+ * STFT/iSTFT launch per iteration), TTS_GL_PATH_FUSED (one launch per iteration), or
+ * TTS_GL_PATH_PERSISTENT (every iteration in one co-resident launch; when the grid cannot be
+ * co-resident the run falls back to the fused loop, bitwise the same waveform). */
+#define TTS_GL_PATH_UNFUSED 0
+#define TTS_GL_PATH_FUSED 1
+#define TTS_GL_PATH_PERSISTENT 2
+tts_status tts_gl_last_path(tts_gl* g, int* path);
+
 /* Measurement only: re-runs `reps` GL iterations of the last tts_gl_run's batch eagerly with
  * HIP events around each kernel on its stream; returns mean ms of [per-frame STFT/iSTFT kernel,
  * overlap-add kernel] (one iteration launches both).  Clobbers the internal frame and signal
@@ -217,6 +230,10 @@ void tts_synth_destroy(tts_synth* s);
  *          waveform is the first hop*(frames[b]-1) samples of its row, the rest zero. */
 tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, int B, int Lmax, int max_steps,
                          int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames, void* stream);
+/* tts_synth_run returns once Griffin-Lim is enqueued; its completion status (a persistent loop's
+ * hand-off timeout) is otherwise collected by the next run.  This waits for the last run and
+ * returns that status.  A failed run's waveform is NaN, never a plausible-looking signal. */
+tts_status tts_synth_sync(tts_synth* s);
 
 /* ---------------------------------------------------------------- Tacotron / TacotronGST
  * SURVEY config 5 (config_tacotron_gst.json) and config_tacotron.json: the r-frames-per-step

@@ -137,6 +137,21 @@ def istft(stft_matrix, hop_length=None, win_length=None, center=True, dtype=np.f
     return y
 
 
+def device_phase_u(seed: int, b: int, F: int, nb: int = 1025) -> np.ndarray:
+    """The U[0,1) initial phases the HIP Griffin-Lim draws on the device when no host phases are
+    given (griffin_lim.hip: hash_uniform, a splitmix64 finaliser of seed + golden * (idx + 1) with
+    idx = (b * 1025 + k) * 2^20 + f), restated with wrapping uint64 arithmetic: [nb, F] float64."""
+    with np.errstate(over="ignore"):
+        k = np.arange(nb, dtype=np.uint64)[:, None]
+        f = np.arange(F, dtype=np.uint64)[None, :]
+        idx = (np.uint64(b) * np.uint64(nb) + k) * np.uint64(1048576) + f
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (idx + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
 # ---------------------------------------------------------------- AudioProcessor restatement
 
 

@@ -225,6 +225,46 @@ def make_text_fixture():
     print("text_basic:", [len(s) for s in seqs])
 
 
+SPLIT_TEXTS = [
+    "Hello world. This is a test.",
+    "Mr. Smith went to Washington. He arrived at 5 p.m. and left!",
+    "Dr. Jones has a Ph.D. in physics. She works at Acme Inc. They build rockets.",
+    "The U.S.A. is large. The U.K. is not. But the E.U. is.",
+    "Visit www.example.com or mail.org today. It's free?",
+    "He said \"stop.\" Then he left. \"Why?\" she asked! \"Go!\" he replied.",
+    "Curly quotes: “Fine.” Next one. Jr. was here. Mrs. Brown Jr. said hi.",
+    "No terminal punctuation here",
+    "Multi\nline\ntext. Second line! Third?",
+    "A. B. C. single letters. J.R.R. Tolkien wrote books. It was good.",
+    "Acme Co. However we knew. Ltd. is short. St. Louis is a city.",
+    "Ellipsis... and more... done.",
+    "ok. no. x. abc.",
+    "",
+    "   ",
+    "It took me quite a long time to develop a voice, and now that I have it I'm not going to be silent.",
+]
+
+
+def make_split_fixture():
+    """Synthesizer.split_into_sentences (server/synthesizer.py:102-126) run by the reference module
+    itself on a corpus of abbreviations, acronyms, quotes, Ph.D, websites and edge cases; also the
+    list Synthesizer.tts keeps (:130-136: [text + '.'] when nothing splits, drop len < 3)."""
+    _stub_text_deps()
+    _stub_audio_deps()
+    sys.path.insert(0, REF)
+    srv = _load("ref_server_synthesizer", os.path.join(REF, "server", "synthesizer.py"))
+    split = srv.Synthesizer.split_into_sentences
+    out = {"texts": np.array(SPLIT_TEXTS, dtype=object).astype(str)}
+    for i, t in enumerate(SPLIT_TEXTS):
+        sens = split(None, t)
+        kept = sens if len(sens) else [t + "."]
+        kept = [s.strip() for s in kept if len(s) >= 3]
+        out[f"split{i}"] = np.array(sens, dtype=str)
+        out[f"kept{i}"] = np.array(kept, dtype=str)
+        print(f"split {i}: {sens}")
+    np.savez_compressed(os.path.join(HERE, "split_sentences.npz"), **out)
+
+
 def make_gl_fixtures():
     _stub_text_deps()
     _stub_audio_deps()
@@ -285,7 +325,9 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "taco", "truncated", "text", "gl"]
+    which = sys.argv[1:] or ["model", "taco", "truncated", "text", "split", "gl"]
+    if "split" in which:
+        make_split_fixture()
     if "model" in which:
         make_model_fixtures()
     if "taco" in which:

@@ -1,0 +1,118 @@
+"""Persistent kernels (resident decoder, resident encoder BiLSTM, persistent Griffin-Lim) hand data
+between workgroups inside one launch, so they are only launched when every workgroup can be
+resident at once (csrc/runtime.hip: launch_persistent — occupancy check + cooperative launch).
+TTS_CU_CAP pretends the device has fewer CUs: the grids then cannot be co-resident, nothing
+persistent is launched, and each stage must take its multi-launch fallback with unchanged results.
+A persistent Griffin-Lim whose hand-off wait times out (fault injection) must raise and must not
+hand out a plausible waveform."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, golden_flags, load_pkg
+
+pytestmark = pytest.mark.gpu
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _t2():
+    t2 = load_pkg("tacotron2")
+    fl = golden_flags(golden("t2_fwdmask_L100"))
+    m = t2.Tacotron2(130, 0, r=1, attn_win=fl["attn_win"], attn_norm=fl["attn_norm"], forward_attn=fl["forward_attn"],
+                     trans_agent=fl["trans_agent"], forward_attn_mask=fl["forward_attn_mask"],
+                     location_attn=fl["location_attn"], max_batch=4)
+    return m.cuda().eval()
+
+
+def test_persistent_griffin_lim_fallback_is_bitwise(audio_cfg):
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 12})
+    rng = np.random.Generator(np.random.PCG64(3))
+    mel = torch.from_numpy(rng.uniform(0, 1, size=(1, 90, 80)).astype(np.float32)).cuda()
+    pu = rng.uniform(0, 1, size=(1, 1025, 90))
+    a = ap.griffin_lim_batch(mel, [90], phase_u=pu)
+    assert ap.last_gl_path() == "persistent"
+    with _env(TTS_CU_CAP=8):
+        b = ap.griffin_lim_batch(mel, [90], phase_u=pu)
+        assert ap.last_gl_path() == "fused"
+    assert torch.equal(a, b)
+    c = ap.griffin_lim_batch(mel, [90], phase_u=pu)  # and back
+    assert ap.last_gl_path() == "persistent" and torch.equal(a, c)
+
+
+def test_resident_decoder_and_encoder_fallback_match_multilaunch():
+    z = golden("t2_fwdmask_L100")
+    ids = [z["ids"]]
+    m = _t2()
+    ref = m.inference_batch(ids)
+    assert m.last_timing["resident"] and m.last_timing["encoder_resident"]
+    with _env(TTS_RESIDENT=0):
+        ml = _t2()
+        want = ml.inference_batch(ids)
+        assert not ml.last_timing["resident"] and not ml.last_timing["encoder_resident"]
+    with _env(TTS_CU_CAP=64):
+        fb = _t2()
+        got = fb.inference_batch(ids)
+        assert not fb.last_timing["resident"] and not fb.last_timing["encoder_resident"]
+    # the fallback IS the multi-launch path: bitwise equal to it
+    for k in ("mel", "mel_post", "align", "stop"):
+        assert torch.equal(got[k], want[k]), k
+    assert got["frames"] == ref["frames"] == [z["mel"].shape[0]]
+    # ... and within the parity tolerance of the resident path
+    d = (got["mel_post"] - ref["mel_post"]).norm() / ref["mel_post"].norm()
+    assert float(d) < 1e-5
+
+
+def test_persistent_griffin_lim_timeout_raises_and_poisons(audio_cfg):
+    """Fault injection: frame 3 of sentence 0 stops publishing after its first iteration, so its
+    neighbours' hand-off waits time out.  The run must report an error and its waveform must be
+    NaN (never a plausible signal); the same handle then works again."""
+    audio = load_pkg("audio")
+    with _env(TTS_GL_WAIT_TICKS=20000):  # 0.2 ms per wait at the 100 MHz wall clock
+        ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 8})
+        rng = np.random.Generator(np.random.PCG64(4))
+        mel = torch.from_numpy(rng.uniform(0, 1, size=(1, 40, 80)).astype(np.float32)).cuda()
+        pu = rng.uniform(0, 1, size=(1, 1025, 40))
+        good = ap.griffin_lim_batch(mel, [40], phase_u=pu)
+        assert ap.last_gl_path() == "persistent" and torch.isfinite(good).all()
+        with _env(TTS_GL_INJECT_DROP=3):
+            with pytest.raises(RuntimeError, match="timed out"):
+                ap.griffin_lim_batch(mel, [40], phase_u=pu)
+        again = ap.griffin_lim_batch(mel, [40], phase_u=pu)
+        assert torch.equal(again, good)
+
+
+def test_synthesize_native_timeout_surfaces(audio_cfg):
+    """The same fault through tts_synth_run: sync=True raises for the failing call itself; with
+    sync=False the waveform is NaN and the next call raises."""
+    audio = load_pkg("audio")
+    z = golden("t2_fwdmask_L12")
+    m = _t2()
+    with _env(TTS_GL_WAIT_TICKS=20000):
+        ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
+        with _env(TTS_GL_INJECT_DROP=2):
+            with pytest.raises(RuntimeError, match="timed out"):
+                m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
+            wav, _ = m.synthesize_native([z["ids"]], ap, seed=1, sync=False)
+            assert torch.isnan(wav).all()
+        with pytest.raises(RuntimeError, match="timed out"):
+            m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
+        wav, _ = m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
+        assert torch.isfinite(wav).all()

@@ -29,3 +29,19 @@ def test_missing_frontend_dependencies_raise():
         text.phoneme_to_sequence("abc", ["phoneme_cleaners"], "en-us")
     with pytest.raises(Exception, match="Unknown cleaner"):
         text.text_to_sequence("abc", ["nope"])
+
+
+def test_split_into_sentences_matches_reference():
+    """Synthesizer.split_into_sentences and the sentence list Synthesizer.tts keeps
+    (server/synthesizer.py:102-136) vs the reference module run on a hard corpus
+    (tests/golden/split_sentences.npz, made by make_golden.py split)."""
+    import types
+    synth = load_pkg("synthesis")
+    z = golden("split_sentences")
+    dummy = types.SimpleNamespace(eval=lambda: None, decoder=types.SimpleNamespace(max_decoder_steps=1000))
+    s = synth.Synthesizer(dummy, None, None)
+    assert dummy.decoder.max_decoder_steps == 3000  # server/synthesizer.py:66
+    for i, t in enumerate(z["texts"]):
+        t = str(t)
+        assert synth.split_into_sentences(t) == [str(x) for x in z[f"split{i}"]], t
+        assert s.sentences(t) == [str(x) for x in z[f"kept{i}"]], t

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("TTS_HIP_LIB", os.path.join(_HERE, "libtts_hip.so"))
 
 TTS_GL_FROM_MEL = 0
 TTS_GL_FROM_LINEAR = 1
+GL_PATHS = {0: "unfused", 1: "fused", 2: "persistent"}  # TTS_GL_PATH_* (include/tts_hip.h)
 DECODER_STEP_KERNELS = ("prenet2", "att_lstm", "query", "attention", "dec_lstm", "mel_fused")
 GL_KERNELS = ("gl_iter", "gl_ola")
 TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "dec_gru1", "dec_gru2", "mel",
@@ -21,14 +22,14 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 
 # every symbol include/tts_hip.h declares
 EXPORTS = (
-    "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state",
+    "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state", "tts_encoder_last_path",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue",
     "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
-    "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_profile",
+    "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_last_path", "tts_gl_profile",
     "tts_gl_set_mel_basis", "tts_gl_melspectrogram",
-    "tts_synth_create", "tts_synth_destroy", "tts_synth_run",
+    "tts_synth_create", "tts_synth_destroy", "tts_synth_run", "tts_synth_sync",
     "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
     "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_profile",
     "tts_last_error", "tts_version",
@@ -82,6 +83,9 @@ def _declare(lib):
     lib.tts_decoder_run_continue.argtypes = lib.tts_decoder_run.argtypes
     lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_decoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_encoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_gl_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_synth_sync.argtypes = [vp]
     lib.tts_decoder_resident_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     lib.tts_postnet_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
     lib.tts_postnet_destroy.argtypes = [vp]
@@ -118,7 +122,7 @@ def _declare(lib):
     for name in EXPORTS:
         fn = getattr(lib, name)
         if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet", "_state",
-                          "_continue", "_basis", "_melspectrogram")):
+                          "_continue", "_basis", "_melspectrogram", "_path", "_sync", "_phases")):
             fn.restype = ctypes.c_int
 
 

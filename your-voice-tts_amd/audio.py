@@ -114,6 +114,15 @@ class AudioProcessor:
             raise RuntimeError(" !! Preemphasis is applied with factor 0.0. ")
         return scipy.signal.lfilter([1], [1, -self.preemphasis], x)
 
+    def find_endpoint(self, wav, threshold_db=-40, min_silence_sec=0.8):  # utils/audio.py:203-210
+        window_length = int(self.sample_rate * min_silence_sec)
+        hop_length = int(window_length / 4)
+        threshold = self._db_to_amp(threshold_db)
+        for x in range(hop_length, len(wav) - window_length, hop_length):
+            if np.max(wav[x:x + window_length]) < threshold:
+                return x + hop_length
+        return len(wav)
+
     def save_wav(self, wav, path):  # utils/audio.py:56-58
         wav_norm = np.asarray(wav) * (32767 / max(0.01, np.max(np.abs(wav))))
         scipy.io.wavfile.write(path, self.sample_rate, wav_norm.astype(np.int16))
@@ -166,6 +175,13 @@ class AudioProcessor:
         ms, n = ctypes.c_float(), ctypes.c_int()
         lib.tts_gl_last_timing(h, ctypes.byref(ms), ctypes.byref(n))
         return dict(gl_loop_ms=ms.value, gl_iterations=n.value)
+
+    def last_gl_path(self):
+        """Iteration loop of the last run: "persistent", "fused" or "unfused" (tts_gl_last_path)."""
+        lib, h = self._handle()
+        p = ctypes.c_int()
+        _native.check(lib.tts_gl_last_path(h, ctypes.byref(p)), "tts_gl_last_path")
+        return _native.GL_PATHS[p.value]
 
     def profile_gl_kernels(self, reps=20):
         """Mean duration (ms) of the GL iteration and overlap-add kernels for the last batch."""

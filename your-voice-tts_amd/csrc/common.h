@@ -36,6 +36,18 @@ void decoder_set_pipeline(tts_decoder* d, bool on);
 void gl_set_pipeline(tts_gl* g, bool on);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 
+// Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent
+// Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This launches
+// `fn` so that co-residency is GUARANTEED or nothing runs: an occupancy check of the grid against the
+// device's CUs (optionally capped by the TTS_CU_CAP environment variable, which tests use to force
+// the fallback), then hipLaunchCooperativeKernel, whose runtime refuses a grid that cannot be
+// co-resident.  *launched = false (and hipSuccess) when the grid cannot be co-resident: the caller
+// takes its multi-launch path.  TTS_COOP=0 launches plainly after the same check (A/B measurement).
+hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args, size_t smem, hipStream_t s,
+                             bool* launched);
+// the CU count launch_persistent plans with (device CUs, capped by TTS_CU_CAP)
+int usable_cus();
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int WAVE = 64;

@@ -564,7 +564,13 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         d->last_ra = ra;
         TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
         TTS_HIP(hipEventRecord(d->ev_t0, s));
-        TTS_HIP(launch_resident(ra, s));
+        bool launched = false;
+        TTS_HIP(launch_resident(ra, s, &launched));
+        if (!launched) {
+            // the grid cannot be co-resident on this device (launch_persistent): nothing ran and the
+            // initial state is untouched; the multi-launch path takes over for the life of the handle
+            d->resident = false;
+        } else {
         TTS_HIP(hipEventRecord(d->ev_t1, s));
         TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
         TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
@@ -582,6 +588,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             run = n_steps[0];
             res_done = true;
             d->last_resident = 1;
+        }
         }
     }
     if (!res_done) {
@@ -685,7 +692,13 @@ tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n) {
     ra.prof = prof;
     if (!st) {
         TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
-        TTS_HIP(launch_resident(ra, s));
+        bool launched = false;
+        TTS_HIP(launch_resident(ra, s, &launched));
+        if (!launched) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(prof);
+            TTS_CHECK(false, TTS_ERR_UNSUPPORTED, "resident decoder cannot be co-resident on this device now");
+        }
     }
     long long h[2 * RES_PHASES];
     TTS_HIP(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s));

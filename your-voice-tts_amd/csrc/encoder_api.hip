@@ -49,6 +49,7 @@ struct tts_encoder {
     bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
     bool status_pending = false;
     std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
+    int last_resident = 0;                  // the last run's BiLSTM path (tts_encoder_last_path)
 };
 
 namespace {
@@ -132,7 +133,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
 
 // B = 1: the whole recurrence in one direct launch (per-launch salt); h_0 / c_0 come from slot 1 / c,
 // h_n goes to slot (L-1) & 1 (where tts_encoder_run_state reads it) and c_n to c
-tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, hipStream_t s) {
+tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, hipStream_t s, bool* launched) {
     const int64_t hs = (int64_t)e->Bcap * EH;
     TTS_HIP(hipMemsetAsync(e->rgran, 0, sizeof(unsigned long long) * encoder_resident_granules(), s));
     EncResArgs a{};
@@ -150,7 +151,7 @@ tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, hipStream_t s) {
     a.tmo = e->rtmo;
     e->rsalt = (e->rsalt + 1) & 0x3FFFF;
     a.salt = e->rsalt;
-    TTS_HIP(launch_encoder_resident(a, s));
+    TTS_HIP(launch_encoder_resident(a, s, launched));
     return TTS_OK;
 }
 
@@ -315,22 +316,31 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
             rit = e->rgraphs.emplace(Lmax, exec).first;
         }
         TTS_HIP(hipGraphLaunch(rit->second, s));
+        bool launched = false;
         {
-            tts_status st = enqueue_encoder_resident(e, Lmax, s);
+            tts_status st = enqueue_encoder_resident(e, Lmax, s, &launched);
             if (st) return st;
         }
-        TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
-                               hipMemcpyDeviceToHost, s));
-        if (e->pipeline) {  // the pipeline reads the status at its next synchronisation point
-            e->status_pending = true;
-            goto done;
-        }
-        TTS_HIP(hipStreamSynchronize(s));
-        if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
-            e->resident = false;  // rerun below with the per-step launches (same state, untouched)
+        if (!launched) {
+            // the grid cannot be co-resident on this device (launch_persistent): nothing ran, the
+            // per-step launches below take over for the life of the handle
+            e->resident = false;
         } else {
-            TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP, "resident encoder: a hand-off wait timed out (internal error)");
-            goto done;
+            e->last_resident = 1;
+            TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
+                                   hipMemcpyDeviceToHost, s));
+            if (e->pipeline) {  // the pipeline reads the status at its next synchronisation point
+                e->status_pending = true;
+                goto done;
+            }
+            TTS_HIP(hipStreamSynchronize(s));
+            if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
+                e->resident = false;  // rerun below with the per-step launches (same state, untouched)
+            } else {
+                TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP,
+                          "resident encoder: a hand-off wait timed out (internal error)");
+                goto done;
+            }
         }
     }
     {
@@ -350,6 +360,7 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         git = e->graphs.emplace(key, exec).first;
     }
     TTS_HIP(hipGraphLaunch(git->second, s));
+    e->last_resident = 0;
     }
 done:
     TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
@@ -392,6 +403,12 @@ tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
 }  // namespace tts
 
 extern "C" {
+
+tts_status tts_encoder_last_path(tts_encoder* e, int* resident) {
+    TTS_CHECK(e && resident, TTS_ERR_INVALID, "null argument");
+    *resident = e->last_resident;
+    return TTS_OK;
+}
 
 tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax, float* out,
                            void* stream) {

@@ -26,6 +26,7 @@ struct EncResArgs {
 size_t encoder_resident_weight_float4();
 size_t encoder_resident_granules();  // includes the trailing status word
 hipError_t encoder_resident_pack(const float* whh_fwd, const float* whh_bwd, float4* out, hipStream_t s);
-hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s);
+// co-residency guaranteed or nothing launched (*launched = false): common.h launch_persistent
+hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s, bool* launched);
 
 }  // namespace tts

@@ -181,9 +181,11 @@ hipError_t encoder_resident_pack(const float* whh_f, const float* whh_b, float4*
     return hipGetLastError();
 }
 
-hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(encoder_resident_kernel, dim3(256), dim3(ER_THREADS), 0, s, a);
-    return hipGetLastError();
+hipError_t launch_encoder_resident(const EncResArgs& a, hipStream_t s, bool* launched) {
+    EncResArgs arg = a;
+    void* args[] = {&arg};
+    return launch_persistent(reinterpret_cast<const void*>(&encoder_resident_kernel), dim3(256), dim3(ER_THREADS),
+                             args, 0, s, launched);
 }
 
 }  // namespace tts

@@ -491,6 +491,8 @@ struct PersArgs {
     int* status;
     long long* prof;    // diagnostic (TTS_GL_PHASES): per-phase wall_clock64 ticks of frame prof_f, or null
     int prof_f;
+    int drop_f;         // fault injection (tests, TTS_GL_INJECT_DROP): sentence 0's frame drop_f stops
+                        // after its first iteration without publishing (-1: none)
 };
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned gu32_t;
@@ -680,6 +682,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
         __syncthreads();  // ... before one lane signals; the LDS buffers are reused next iteration
+        if (b == 0 && f == p.drop_f) return;  // fault injection only: never publishes
         if (tid == 0)
             __hip_atomic_store((gu32_t*)(flb + f), (p.salt << 14) | (unsigned)(it + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -699,6 +702,7 @@ struct FinArgs {
     GLConst c;
     float* y;  // [B][Nmax]
     int64_t Nmax;
+    const int* status;  // the persistent loop's status word, or null: nonzero poisons the signal (NaN)
 };
 
 __global__ void gl_ola_kernel(const FinArgs a) {
@@ -707,7 +711,11 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     const int N = a.g.hop * (Fb - 1);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= N) return;
-    a.y[(int64_t)b * a.Nmax + p] = ola_sample(a.frames + (int64_t)b * a.Fmax * a.g.winp, p + NFFT / 2, Fb, a.g, a.c.win2);
+    // a persistent loop whose hand-off wait timed out left frames unwritten: never hand out a
+    // plausible-looking waveform for it (the run's error status is raised when it is collected)
+    const bool bad = a.status && *a.status != 0;
+    a.y[(int64_t)b * a.Nmax + p] =
+        bad ? __builtin_nanf("") : ola_sample(a.frames + (int64_t)b * a.Fmax * a.g.winp, p + NFFT / 2, Fb, a.g, a.c.win2);
 }
 
 // y[n] = x[n] + c*y[n-1] in float64 (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136).
@@ -896,6 +904,7 @@ struct tts_gl {
     int last_launches = 0;
     bool last_fused = false;
     bool last_persistent = false;
+    int last_path = TTS_GL_PATH_UNFUSED;
     unsigned* flags = nullptr;  // persistent loop: [flags_n] tags
     size_t flags_n = 0;
     double* pfr = nullptr;      // persistent loop: one frame slot per iteration
@@ -988,6 +997,9 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256 &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0)
             g->tmo = (long long)rate_khz * 50;
+        // tests only: a tiny per-wait budget forces the timeout path (status, NaN-poisoned signal)
+        const char* tk = getenv("TTS_GL_WAIT_TICKS");
+        if (tk && tk[0] && g->tmo > 0) g->tmo = std::max(1LL, atoll(tk));
     }
     *out = g;
     return TTS_OK;
@@ -1136,7 +1148,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.y = g->y;
     fa.Nmax = Nmax;
     const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
-    g->last_persistent = persistent;
+    bool persistent_ran = false;
     if (persistent) {
         PersArgs pa{};
         pa.it = ia;
@@ -1148,6 +1160,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         pa.salt = g->salt;
         pa.tmo = g->tmo;
         pa.status = g->pstatus;
+        pa.drop_f = -1;
+        if (const char* inj = getenv("TTS_GL_INJECT_DROP"); inj && inj[0]) pa.drop_f = atoi(inj);
         long long* prof = nullptr;
         const char* phases = getenv("TTS_GL_PHASES");
         if (phases && phases[0]) {  // diagnostic: phase ticks of frame TTS_GL_PHASES (stderr)
@@ -1156,19 +1170,18 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             pa.prof = prof;
             pa.prof_f = std::min(atoi(phases), frames_total - 1);
         }
-        const char* one = getenv("TTS_GL_PERSIST_ONE");
-        if (!(one && one[0] == '1')) {
-            hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, pa);
-            TTS_HIP(hipGetLastError());
-        } else {  // debug: one iteration per launch (no in-launch hand-offs)
-            for (int i = 0; i < iters; ++i) {
-                PersArgs q = pa;
-                q.it0 = i;
-                q.iters = 1;
-                g->salt = (g->salt + 1) & 0x3FFFF;
-                q.salt = g->salt;
-                hipLaunchKernelGGL(gl_persistent_kernel, grid, block, 0, s, q);
-                TTS_HIP(hipGetLastError());
+        // every workgroup waits on its neighbours inside the launch: co-residency guaranteed, or
+        // nothing runs and the fused loop below takes the iterations (bitwise the same waveform)
+        void* kargs[] = {&pa};
+        TTS_HIP(launch_persistent(reinterpret_cast<const void*>(&gl_persistent_kernel), grid, block, kargs, 0, s,
+                                  &persistent_ran));
+        if (!persistent_ran) {
+            // the initial iSTFT wrote slot 0 of the persistent frame buffer: hand it to the fused loop
+            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(double), hipMemcpyDeviceToDevice, s));
+            if (prof) {
+                TTS_HIP(hipStreamSynchronize(s));
+                TTS_HIP(hipFree(prof));
+                prof = nullptr;
             }
         }
         if (prof) {
@@ -1184,7 +1197,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             for (int k = 0; k < 6; ++k) fprintf(stderr, " %s %.3f", names[k], h[k] * 1e3 / rate_khz / iters);
             fprintf(stderr, "\n");
         }
-    } else if (iters > 0) {
+    }
+    if (!persistent_ran && iters > 0) {
         // one iteration = overlap-add of the previous frames into the float32 signal (every
         // sample once) + one workgroup per frame for STFT -> phase -> iSTFT of that signal
         GraphKey key{B, Fmax, iters};
@@ -1218,8 +1232,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
     TTS_HIP(hipEventRecord(g->ev_t1, s));
-    fa.frames = persistent ? g->pfr + (size_t)iters * fstride : g->frames + (iters & 1) * fstride;
+    fa.frames = persistent_ran ? g->pfr + (size_t)iters * fstride : g->frames + (iters & 1) * fstride;
+    fa.status = persistent_ran ? g->pstatus : nullptr;
     hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, fa);
+    fa.status = nullptr;
     TTS_HIP(hipGetLastError());
     {
         // de-emphasis chunks: each starts `look` samples early, |c|^look <= 1e-22; one chunk per
@@ -1236,8 +1252,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                            c != 0.0 ? 1 : 0, chunk, look, wav);
     }
     TTS_HIP(hipGetLastError());
-    g->last_launches = persistent ? 1 : (fused ? 1 : 2) * iters;
-    if (persistent) TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
+    g->last_persistent = persistent_ran;
+    g->last_path = persistent_ran ? TTS_GL_PATH_PERSISTENT : fused ? TTS_GL_PATH_FUSED : TTS_GL_PATH_UNFUSED;
+    g->last_launches = persistent_ran ? 1 : (fused ? 1 : 2) * iters;
+    if (persistent_ran) TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
     TTS_HIP(hipEventRecord(g->ev_done, s));
     if (s != cs) TTS_HIP(hipStreamWaitEvent(cs, g->ev_done, 0));
     g->pending = true;
@@ -1349,6 +1367,12 @@ tts_status tts_gl_melspectrogram(tts_gl* g, const double* wav, const int32_t* N,
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_out, s));
     TTS_HIP(hipStreamWaitEvent(cs, g->ev_out, 0));
+    return TTS_OK;
+}
+
+tts_status tts_gl_last_path(tts_gl* g, int* path) {
+    TTS_CHECK(g && path, TTS_ERR_INVALID, "null argument");
+    *path = g->last_path;
     return TTS_OK;
 }
 

@@ -95,6 +95,7 @@ void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc, size_t* ws);
 hipError_t resident_pack(const ResSrc& src, const ResWeights& w, hipStream_t s);
 size_t resident_smem_bytes();
 hipError_t resident_prepare();
-hipError_t launch_resident(const ResArgs& a, hipStream_t s);
+// co-residency guaranteed or nothing launched (*launched = false): common.h launch_persistent
+hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched);
 
 }  // namespace tts

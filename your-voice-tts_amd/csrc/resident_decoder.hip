@@ -749,10 +749,13 @@ hipError_t resident_prepare() {
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
 }
 
-hipError_t launch_resident(const ResArgs& a, hipStream_t s) {
+hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched) {
+    *launched = false;
     if (a.L < 2 || a.L > RES_LMAX || a.nrows >= 2 * RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(resident_decoder_kernel, dim3(RES_CUS), dim3(RES_THREADS), resident_smem_bytes(), s, a);
-    return hipGetLastError();
+    ResArgs arg = a;
+    void* args[] = {&arg};
+    return launch_persistent(reinterpret_cast<const void*>(&resident_decoder_kernel), dim3(RES_CUS), dim3(RES_THREADS),
+                             args, resident_smem_bytes(), s, launched);
 }
 
 }  // namespace tts

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "common.h"
@@ -56,6 +57,11 @@ struct PipelineScope {
         tts::gl_set_pipeline(s->g, on);
     }
 };
+
+// the stages of one tts_synth_run after the host staging (defined below)
+tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* h_frames, int B, int Lmax,
+                        int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
+                        void* stream);
 }  // namespace
 
 extern "C" {
@@ -86,7 +92,8 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
 void tts_synth_destroy(tts_synth* s) {
     if (!s) return;
     if (s->stream) (void)hipStreamSynchronize(s->stream);
-    (void)tts::gl_collect(s->g);
+    if (tts::gl_collect(s->g) != TTS_OK)  // the last pipelined run's status was never collected
+        std::fprintf(stderr, "tts_synth_destroy: the last run failed: %s\n", tts_last_error());
     for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post, (void*)s->spec})
         if (q) (void)hipFree(q);
     for (int32_t* q : s->pin)
@@ -131,13 +138,39 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
         TTS_HIP(hipHostMalloc(reinterpret_cast<void**>(&s->pin[par]), pin_need * sizeof(int32_t)));
         s->pin_n[par] = pin_need;
     }
-    ++s->calls;
     int32_t* h_ids = s->pin[par];
     int32_t* h_lens = h_ids + (size_t)B * Lmax;
     int32_t* h_frames = h_lens + B;
     std::copy(ids, ids + (size_t)B * Lmax, h_ids);
     std::copy(lens, lens + B, h_lens);
+    // a call that fails after staging may still have copies from pin[par] in flight: drain them
+    // before returning, so the next call can restage the same buffer
+    st = synth_stages(s, h_ids, h_lens, h_frames, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
+    if (st) {
+        (void)hipStreamSynchronize(s->stream);
+        return st;
+    }
+    ++s->calls;  // only now: a failed call leaves the parity (and its drained buffer) to the next
+    return TTS_OK;
+}
 
+tts_status tts_synth_sync(tts_synth* s) {
+    TTS_CHECK(s, TTS_ERR_INVALID, "null handle");
+    TTS_HIP(hipStreamSynchronize(s->stream));
+    return tts::gl_collect(s->g);
+}
+
+}  // extern "C"
+
+namespace {
+tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* h_frames, int B, int Lmax,
+                        int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
+                        void* stream) {
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t ss = s->stream;
+    const int cap = max_steps + 21;
+    const size_t T = (size_t)cap * s->r;
+    tts_status st;
     PipelineScope scope(s);
     TTS_HIP(hipEventRecord(s->ev_in, cs));
     TTS_HIP(hipStreamWaitEvent(ss, s->ev_in, 0));
@@ -176,5 +209,4 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
     TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
     return TTS_OK;
 }
-
-}  // extern "C"
+}  // namespace

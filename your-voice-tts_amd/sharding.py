@@ -76,8 +76,20 @@ def gather_waveforms(wavs, indices, n_total: int, group=None, dst: int = 0):
     dtype = wavs[0].dtype if len(wavs) else torch.float64
     if rank != dst:
         if len(wavs):
-            dist.send(torch.cat([w.reshape(-1) for w in wavs]), dst=_global(dst, group), group=group)
+            op = dist.P2POp(dist.isend, torch.cat([w.reshape(-1) for w in wavs]), _global(dst, group), group)
+            for req in dist.batch_isend_irecv([op]):
+                req.wait()
         return None
+    # every peer's receive is posted at once (one group: over xGMI each peer streams on its own
+    # link concurrently), then waited on together
+    bufs = {}
+    ops = []
+    for r in range(world):
+        if r != rank and counts[r] > 0:
+            bufs[r] = torch.empty(int(hdr[r][1]), dtype=dtype, device=dev)
+            ops.append(dist.P2POp(dist.irecv, bufs[r], _global(r, group), group))
+    for req in (dist.batch_isend_irecv(ops) if ops else []):
+        req.wait()
     out = [None] * n_total
     for r in range(world):
         tab = tables[r][:counts[r]].cpu().tolist()
@@ -86,8 +98,7 @@ def gather_waveforms(wavs, indices, n_total: int, group=None, dst: int = 0):
         else:
             if counts[r] == 0:
                 continue
-            buf = torch.empty(int(hdr[r][1]), dtype=dtype, device=dev)
-            dist.recv(buf, src=_global(r, group), group=group)
+            buf = bufs[r]
         off = 0
         for i, n in tab:
             out[i] = buf[off:off + n]
@@ -125,8 +136,10 @@ def join_int16(wavs, peak: float | None = None) -> np.ndarray:
 def synthesize_sharded(model, ap, ids_list, group=None, seed=0, max_batch=None):
     """Synthesizer.tts over all ranks: LPT shard, local batched synthesis, gather-v to rank 0.
 
-    Returns (int16 waveform with 10 000-sample gaps on rank 0 / None elsewhere, info).  Initial
-    Griffin-Lim phases come from the device generator seeded with ``seed + rank``."""
+    Returns (int16 waveform with 10 000-sample gaps on rank 0 / None elsewhere, info); on rank 0
+    ``info["wavs"]`` holds every sentence's float64 waveform (device tensors, global order).
+    Initial Griffin-Lim phases come from the device generator seeded with ``seed + rank``, sentence
+    b of the rank's batch (its ``partition`` list, ascending) at generator row b."""
     from .synthesis import synthesize_batch
 
     world = dist.get_world_size(group)
@@ -144,10 +157,12 @@ def synthesize_sharded(model, ap, ids_list, group=None, seed=0, max_batch=None):
         wav_dev = inf["wav_dev"]
         wavs = [wav_dev[k, :n] for k, n in enumerate(inf["samples"])]
         info["frames"] = inf["frames"]
+        info["gl_iterations"] = inf["gl_iterations"]
     peak = global_peak(wavs, group)
     allw = gather_waveforms(wavs, mine, len(ids_list), group)
     if rank != 0:
         return None, info
+    info["wavs"] = allw
     return join_int16(allw, peak), info
 
 

@@ -124,29 +124,40 @@ def compute_style_mel(style_wav, ap, use_cuda=True):
     return style.cuda() if use_cuda else style
 
 
+def run_model(model, inputs, CONFIG, truncated, speaker_id=None, style_mel=None):
+    """utils/synthesis.py:38-49: GST with a style mel -> inference(style_mel=...); otherwise
+    inference_truncated (continuous mode) or inference."""
+    if CONFIG.model == "TacotronGST" and style_mel is not None:
+        return model.inference(inputs, style_mel=style_mel, speaker_ids=speaker_id)
+    if truncated:
+        return model.inference_truncated(inputs, speaker_ids=speaker_id)
+    return model.inference(inputs, speaker_ids=speaker_id)
+
+
 def synthesis(model, text, CONFIG, use_cuda, ap, speaker_id=None, style_wav=None, truncated=False,
               enable_eos_bos_chars=False, trim_silence=False):
     """utils/synthesis.py:78-124: returns (wav, alignment [T,L], decoder_output [T*r,80],
-    postnet_output [T*r,80] (Tacotron2) or [T*r,1025] (Tacotron / TacotronGST), stop_tokens)."""
-    if truncated:
-        return model.inference_truncated(_ids_tensor(text, CONFIG))
+    postnet_output [T*r,80] (Tacotron2) or [T*r,1025] (Tacotron / TacotronGST), stop_tokens) for
+    both values of ``truncated`` (run_model picks inference / inference_truncated; parse_outputs and
+    the Griffin-Lim tail are the same)."""
+    style_mel = None
+    if CONFIG.model == "TacotronGST" and style_wav is not None:
+        style_mel = compute_style_mel(style_wav, ap, use_cuda)
     inputs = _ids_tensor(text, CONFIG)
     sid = None if speaker_id is None or speaker_id is False else torch.as_tensor([speaker_id])
-    if CONFIG.model == "TacotronGST" and style_wav is not None:  # run_model (utils/synthesis.py:38-49)
-        style_mel = compute_style_mel(style_wav, ap, use_cuda)
-        decoder_output, postnet_output, alignments, stop_tokens = model.inference(
-            inputs, style_mel=style_mel, speaker_ids=sid)
-    else:
-        decoder_output, postnet_output, alignments, stop_tokens = model.inference(inputs, speaker_ids=sid)
+    decoder_output, postnet_output, alignments, stop_tokens = run_model(model, inputs, CONFIG, truncated, sid,
+                                                                        style_mel)
     postnet_output = postnet_output[0].cpu().numpy()  # parse_outputs (utils/synthesis.py:52-56)
     decoder_output = decoder_output[0].cpu().numpy()
     alignment = alignments[0].cpu().numpy()
-    if CONFIG.model in ("Tacotron", "TacotronGST"):
+    if CONFIG.model in ("Tacotron", "TacotronGST"):  # inv_spectrogram (utils/synthesis.py:63-68)
         wav = ap.inv_spectrogram(postnet_output.T)
     else:
         wav = ap.inv_mel_spectrogram(postnet_output.T)
     if trim_silence:
-        raise NotImplementedError("trim_silence needs AudioProcessor.find_endpoint (not on the path)")
+        # the reference's intent (utils/synthesis.py:59-60): cut at AudioProcessor.find_endpoint.
+        # (Its parameter shadows the module function, so the reference itself raises TypeError here.)
+        wav = wav[:ap.find_endpoint(wav)]
     return wav, alignment, decoder_output, postnet_output, stop_tokens
 
 
@@ -181,11 +192,16 @@ class Synthesizer:
     def save_wav(self, wav, path):
         self.ap.save_wav(np.array(wav), path)
 
-    def tts(self, text):
+    def sentences(self, text):
+        """The sentences Synthesizer.tts synthesises (server/synthesizer.py:130-136): the split,
+        or [text + '.'] when nothing splits, without those shorter than 3 characters."""
         sens = self.split_into_sentences(text)
         if len(sens) == 0:
             sens = [text + "."]
-        sens = [s.strip() for s in sens if len(s) >= 3]  # server/synthesizer.py:134-136
+        return [s.strip() for s in sens if len(s) >= 3]
+
+    def tts(self, text):
+        sens = self.sentences(text)
         adapter = self.input_adapter or (lambda sen: text_to_seqvec(sen, self.tts_config))
         ids = [np.asarray(adapter(s)) for s in sens]
         wavs = []

@@ -9,8 +9,8 @@ Where the compute runs:
     ``tts_decoder_run`` — HIP kernels, hipGraph-replayed steps;
   * Postnet + residual (layers/tacotron2.py:30-45, models/tacotron2.py:69-70): libtts_hip
     ``tts_postnet_run`` — fp32 MFMA implicit-GEMM convolutions;
-  * embedding + encoder (layers/tacotron2.py:78-83): PyTorch-ROCm ops on the GPU for now
-    (SURVEY 8(f) row 1 moves it to HIP).
+  * embedding + encoder (layers/tacotron2.py:78-83): libtts_hip ``tts_encoder_run`` — the
+    embedding gather fused into the first MFMA conv, BN folded, persistent BiLSTM.
 There is no CPU path: without a GPU or without libtts_hip.so, ``inference`` raises.
 
 Batches: the reference decoder is batch-1 (its stop rule reads item 0,
@@ -241,12 +241,7 @@ class Tacotron2:
         _native.check(lib.tts_postnet_run(hpost, ctypes.c_void_p(mel.data_ptr()), _native.i32_array(frames), B,
                                           cap * r, ctypes.c_void_p(mel_post.data_ptr()), stream), "tts_postnet_run")
         T, S = max(frames), max(steps)
-        ms = ctypes.c_float()
-        ns = ctypes.c_int()
-        lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
-        res = ctypes.c_int()
-        lib.tts_decoder_last_path(hdec, ctypes.byref(res))
-        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value))
+        self.last_timing = self._path_timing(lib, hdec)
         self.last_lengths = frames
         return dict(mel=mel[:, :T], mel_post=mel_post[:, :T], align=align[:, :S], stop=stop[:, :S],
                     frames=frames, steps=steps, lens=lens)
@@ -261,12 +256,16 @@ class Tacotron2:
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
     @torch.no_grad()
-    def synthesize_native(self, ids_list, ap, seed=0, iters=None):
+    def synthesize_native(self, ids_list, ap, seed=0, iters=None, sync=True):
         """utils/synthesis.py:synthesis (model.inference, :50-57 -> ap.inv_mel_spectrogram, :69-77)
         for a ragged batch in ONE native call (tts_synth_run): encoder -> decoder -> postnet ->
         Griffin-Lim with device phases from ``seed``, bitwise what inference_batch followed by
         ap.griffin_lim_batch(mel_post, frames, seed=seed) returns, without the host round trips
-        between the stages.  Returns (wav: CUDA fp64 [B, hop*(Fmax-1)], frames)."""
+        between the stages.  Returns (wav: CUDA fp64 [B, hop*(Fmax-1)], frames).
+
+        sync=True waits for the run and raises on its completion status; sync=False returns once
+        Griffin-Lim is enqueued (the next call overlaps it and raises a failure of this one; a
+        failed run's waveform is NaN, never a plausible signal)."""
         if "speaker_embedding.weight" in self._params:
             raise ValueError("synthesize_native: speaker embeddings go through inference_batch")
         lens = [len(x) for x in ids_list]
@@ -290,7 +289,9 @@ class Tacotron2:
         ids = np.zeros((B, Lmax), np.int32)
         for b, x in enumerate(ids_list):
             ids[b, :lens[b]] = np.asarray(x, dtype=np.int32)
-        cap = B * ap.hop_length * max_steps * self.n_frames_per_step
+        # the decoder may legally run max_steps + 20 steps (the elif cap of layers/tacotron2.py:271-277
+        # is skipped once every stop flag is set): size for the decoder's own steps_cap
+        cap = B * ap.hop_length * ((max_steps + 21) * self.n_frames_per_step - 1)
         if self._wav_buf is None or self._wav_buf.numel() < cap:
             self._wav_buf = torch.empty(cap, dtype=torch.float64, device=self.device)
         frames = (ctypes.c_int32 * B)()
@@ -299,13 +300,21 @@ class Tacotron2:
                                         max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
                                         cap, frames, _native.stream_handle()), "tts_synth_run")
         frames = [int(f) for f in frames]
-        ms, ns, res = ctypes.c_float(), ctypes.c_int(), ctypes.c_int()
-        lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
-        lib.tts_decoder_last_path(hdec, ctypes.byref(res))
-        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value))
+        if sync:
+            _native.check(lib.tts_synth_sync(hs), "tts_synth_sync")
+        self.last_timing = self._path_timing(lib, hdec)
         self.last_lengths = frames
         n = ap.hop_length * (max(frames) - 1)
         return self._wav_buf[:B * n].view(B, n), frames
+
+    def _path_timing(self, lib, hdec):
+        """Decoder loop time and the paths the last run took (resident decoder / encoder BiLSTM)."""
+        ms, ns, res, enc = ctypes.c_float(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        lib.tts_decoder_last_timing(hdec, ctypes.byref(ms), ctypes.byref(ns))
+        lib.tts_decoder_last_path(hdec, ctypes.byref(res))
+        lib.tts_encoder_last_path(self._native[3], ctypes.byref(enc))
+        return dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value),
+                    encoder_resident=bool(enc.value))
 
     RESIDENT_PHASES = ("att_early_wait_pre1", "prenet2_row", "wait_prenet2", "att_lstm_prenet", "att_cell_gather",
                        "query_dec_early", "wait_query", "energies_max", "weights_ctx_publish", "next_prefetch",
