@@ -114,6 +114,17 @@ tts_status tts_decoder_run_continue(tts_decoder* d, const float* enc, const int3
                                     int max_steps, int steps_cap, float* mel, float* stop, float* align,
                                     int32_t* n_steps, void* stream);
 
+/* Teacher forcing: replaces Decoder.forward(inputs, memories, mask) (layers/tacotron2.py:227-247)
+ * in eval mode.  Step t decodes from the go frame (t = 0) or teacher row t-1 (80*r values: frames
+ * (t-1)r .. tr-1), with no stop rule: exactly `steps` steps for every sentence, each sentence at its
+ * own encoder length (padding positions are never attended, as the reference's mask would do).
+ *   memories [dev] fp32 [B][mem_ldb] teacher frames, row t at t * 80 * r
+ *   mel   [dev] fp32 [B][steps][80*r]; stop [dev] fp32 [B][steps] stopnet LOGITS (no sigmoid, as
+ *         Decoder.forward returns them); align [dev] fp32 [B][steps][Lmax] or null. */
+tts_status tts_decoder_run_teacher(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
+                                   const float* memories, int64_t mem_ldb, int steps, float* mel, float* stop,
+                                   float* align, void* stream);
+
 /* Per-step timing of the last tts_decoder_run (ms of GPU time of the step loop, steps run). */
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run);
 

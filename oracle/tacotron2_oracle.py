@@ -95,8 +95,11 @@ class Tacotron2Oracle:
         return (out, (hN, cN)) if return_state else out
 
     # ------------------------------------------------------------------ decoder
-    def decoder(self, memory_in, carry=None, return_carry=False):
-        """Decoder.inference (layers/tacotron2.py:249-285) for one sentence.
+    def decoder(self, memory_in, carry=None, return_carry=False, teacher=None):
+        """Decoder.inference (layers/tacotron2.py:249-285) for one sentence; with ``teacher`` ([T, 80]
+        frames) Decoder.forward (:227-247) instead: step t decodes from the go frame (t = 0) or teacher
+        row t-1 (_reshape_memory: r frames per row), exactly T/r steps, no stop rule, and the stop
+        outputs are the stopnet logits (forward applies no sigmoid).
         memory_in [L, 512] -> mel [T*r, 80], stop [T], align [T, L].  ``carry`` = (h_att, c_att,
         h_dec, c_dec, ctx, memory) continues from a previous call (Decoder.inference_truncated,
         :287-328: RNN states, context and the last mel frame kept; attention restarts)."""
@@ -122,6 +125,8 @@ class Tacotron2Oracle:
         if carry is not None:
             h_att, c_att, h_dec, c_dec, ctx, memory = [np.array(v, dtype=dt) for v in carry]
         outs, stops, aligns = [], [], []
+        if teacher is not None:
+            teacher = np.asarray(teacher, dtype=dt).reshape(-1, 80 * self.r)  # [T/r, 80 r]
         flag1 = False
         stop_count = 0
         t = 0
@@ -200,8 +205,14 @@ class Tacotron2Oracle:
             st = w["decoder.stopnet.1.linear_layer.weight"][0] @ np.concatenate([h_dec, mel]) + \
                 w["decoder.stopnet.1.linear_layer.bias"][0]
             outs.append(mel)
-            stops.append(_sig(st))
+            stops.append(st if teacher is not None else _sig(st))
             aligns.append(att_w.copy())
+            if teacher is not None:
+                if len(outs) == teacher.shape[0]:
+                    break
+                memory = teacher[t]
+                t += 1
+                continue
             # stop rule (:267-277); stop_flags[0] starts True and is never cleared
             flag1 = flag1 or (att_w[-2:].sum() > 0.8 and t > L)
             flag2 = t > 2 * L
@@ -241,6 +252,13 @@ class Tacotron2Oracle:
             mel, stop, align, carry = self.decoder(enc, carry, return_carry=True)
             res.append(dict(enc=enc, mel=mel, mel_post=self.postnet(mel), stop=stop, align=align))
         return res
+
+    def forward(self, ids, teacher, speaker_id=None):
+        """Tacotron2.forward (models/tacotron2.py:47-60) in eval mode for one sentence: encoder at its
+        length, teacher-forced decoder, postnet + residual."""
+        enc = self.encoder(np.asarray(ids), speaker_id)
+        mel, stop, align = self.decoder(enc, teacher=teacher)
+        return dict(enc=enc, mel=mel, mel_post=self.postnet(mel), stop=stop, align=align)
 
     def infer_batch(self, ids_list):
         return [self.inference(ids) for ids in ids_list]

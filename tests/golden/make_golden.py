@@ -204,6 +204,48 @@ def make_truncated_fixture():
     np.savez_compressed(os.path.join(HERE, "trunc_t2_3texts.npz"), flags=np.array(repr(flags)), **out)
 
 
+TF_CASES = [
+    # name, L, id seed, teacher frames, teacher seed, config overrides (+ forward_attn_mask)
+    ("tf_fwdmask_L12", 12, 11, 40, 71, dict(forward_attn_mask=True)),
+    ("tf_loc_softmax_L20", 20, 14, 30, 72,
+     dict(location_attn=True, attention_norm="softmax", use_forward_attn=False, forward_attn_mask=False)),
+    ("tf_win_fwdmask_L16", 16, 16, 24, 73, dict(windowing=True, forward_attn_mask=True)),
+]
+
+
+def make_teacher_fixtures():
+    """Teacher-forced Decoder.forward(inputs, memories, mask=None) (layers/tacotron2.py:227-247) of the
+    reference in eval mode on seeded U[0,1) teacher mels, plus Postnet + residual on its output
+    (models/tacotron2.py:56-57).  (The reference's Tacotron2.forward itself cannot run on torch >= 1.2:
+    common_layers.py:234 computes `1 - mask` on a bool mask; with mask=None the decoder runs.)"""
+    import torch
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    from utils.generic_utils import load_config, setup_model
+    for name, L, seed, T, tseed, over in TF_CASES:
+        C = load_config(os.path.join(REF, "config_tacotron2.json"))
+        C.num_speakers = 0
+        C.update(over)
+        model = setup_model(130, 0, C)
+        sd = weights.tacotron2_weights(0, num_chars=130, location_attn=C.location_attn, trans_agent=C.transition_agent)
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        model.eval()
+        ids = weights.synthetic_ids(L, seed)
+        teacher = np.random.Generator(np.random.PCG64(tseed)).uniform(0, 1, size=(T, 80)).astype(np.float32)
+        with torch.no_grad():
+            x = torch.from_numpy(ids).unsqueeze(0)
+            enc = model.encoder.inference(model.embedding(x).transpose(1, 2))
+            mel, stop, align = model.decoder(enc, torch.from_numpy(teacher)[None], None)
+            mel_post = mel + model.postnet(mel)
+        flags = dict(attn_norm=C.attention_norm, forward_attn=C.use_forward_attn, trans_agent=C.transition_agent,
+                     forward_attn_mask=C.forward_attn_mask, location_attn=C.location_attn, attn_win=C.windowing,
+                     max_decoder_steps=model.decoder.max_decoder_steps)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), ids=ids, enc=enc[0].numpy(), teacher=teacher,
+                            mel=mel[0].numpy(), mel_post=mel_post[0].numpy(), stop=stop[0].numpy(),
+                            align=align[0].numpy(), flags=np.array(repr(flags)))
+        print(f"{name}: L={L} T={T} mel {tuple(mel.shape)} stop {tuple(stop.shape)} align {tuple(align.shape)}")
+
+
 TEXTS = ["Hello world.", "It took me quite a long time to develop a voice, and now that I have it I'm not going "
          "to be silent.", "  Mixed   CASE\twhitespace;  (and) punctuation: ok?  ", "Turn left on {HH AW1 S S T AH0 N} Street.",
          "Numbers 1234 & symbols #%* are dropped!"]
@@ -325,7 +367,9 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "taco", "truncated", "text", "split", "gl"]
+    which = sys.argv[1:] or ["model", "taco", "truncated", "teacher", "text", "split", "gl"]
+    if "teacher" in which:
+        make_teacher_fixtures()
     if "split" in which:
         make_split_fixture()
     if "model" in which:

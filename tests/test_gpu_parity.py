@@ -319,3 +319,49 @@ def test_synthesize_native_back_to_back(audio_cfg):
         wav, frames = outs[k]
         assert frames == out["frames"]
         assert torch.equal(wav, ref), k
+
+
+TF_CASES = ["tf_fwdmask_L12", "tf_loc_softmax_L20", "tf_win_fwdmask_L16"]
+
+
+@pytest.mark.parametrize("case", TF_CASES)
+def test_decoder_forward_teacher_forcing_vs_reference(case):
+    """Decoder.forward (teacher forcing, layers/tacotron2.py:227-247) vs the reference run on the same
+    encoder output and teacher mel: mel [B, 80, T], stop LOGITS [B, T], alignments [B, T, L]."""
+    z = golden(case)
+    fl = golden_flags(z)
+    m = _model(fl)
+    mel, stop, align = m.decoder_forward(torch.from_numpy(z["enc"])[None], torch.from_numpy(z["teacher"])[None])
+    assert tuple(mel.shape) == (1,) + z["mel"].shape and tuple(stop.shape) == (1,) + z["stop"].shape
+    assert tuple(align.shape) == (1,) + z["align"].shape
+    assert rel_rms(mel[0].cpu().numpy(), z["mel"]) < MEL_RTOL
+    np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"].argmax(1))
+    assert np.abs(align[0].cpu().numpy() - z["align"]).max() < ALIGN_ATOL
+    assert np.abs(stop[0].cpu().numpy() - z["stop"]).max() < ALIGN_ATOL * max(1.0, np.abs(z["stop"]).max())
+
+
+def test_tacotron2_forward_ragged_batch_teacher_forcing():
+    """Tacotron2.forward (models/tacotron2.py:47-60, eval) on a padded batch: the fixture sentence
+    (its first 20 teacher frames: teacher forcing is causal, so its outputs are the fixture's first 20
+    steps) next to a shorter sentence checked against the oracle's forward at its own length."""
+    z = golden("tf_fwdmask_L12")
+    fl = golden_flags(z)
+    m = _model(fl)
+    w = weights_mod()
+    ids2 = w.synthetic_ids(7, 88)
+    T = 20
+    teacher2 = np.random.Generator(np.random.PCG64(89)).uniform(0, 1, size=(T, 80)).astype(np.float32)
+    text = torch.zeros(2, 12, dtype=torch.long)
+    text[0] = torch.from_numpy(z["ids"])
+    text[1, :7] = torch.from_numpy(ids2)
+    mels = torch.from_numpy(np.stack([z["teacher"][:T], teacher2]))
+    mel, mel_post, align, stop = m.forward(text, torch.tensor([12, 7]), mels)
+    assert tuple(mel.shape) == (2, T, 80) and tuple(align.shape) == (2, T, 12) and tuple(stop.shape) == (2, T)
+    assert rel_rms(mel[0].cpu().numpy(), z["mel"].T[:T]) < MEL_RTOL
+    np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"][:T].argmax(1))
+    ref = Tacotron2Oracle(w.tacotron2_weights(0), dtype=np.float32, **fl).forward(ids2, teacher2)
+    assert rel_rms(mel[1].cpu().numpy(), ref["mel"]) < MEL_RTOL
+    assert rel_rms(mel_post[1].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
+    al = align[1, :, :7].cpu().numpy()
+    np.testing.assert_array_equal(al.argmax(1), ref["align"].argmax(1))
+    assert np.abs(stop[1].cpu().numpy() - ref["stop"]).max() < 1e-3

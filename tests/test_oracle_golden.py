@@ -161,3 +161,20 @@ def test_melspectrogram_oracle_matches_reference_glue(audio_cfg):
     mel = ap.melspectrogram(z["wav"])
     assert mel.shape == z["mel"].shape == (80, 1 + len(z["wav"]) // 275)
     assert np.abs(mel - z["mel"]).max() < 1e-12
+
+
+@pytest.mark.parametrize("case", ["tf_fwdmask_L12", "tf_loc_softmax_L20", "tf_win_fwdmask_L16"])
+def test_teacher_forced_oracle_matches_reference(case):
+    """Decoder.forward (teacher forcing, layers/tacotron2.py:227-247) restated vs the reference run on
+    the same encoder output and teacher mel (tests/golden/tf_*.npz)."""
+    z = golden(case)
+    fl = golden_flags(z)
+    o = Tacotron2Oracle(weights_mod().tacotron2_weights(0, location_attn=fl["location_attn"]), dtype=np.float64,
+                        **fl)
+    mel, stop, align = o.decoder(z["enc"], teacher=z["teacher"])
+    assert mel.shape == z["mel"].T.shape and stop.shape == z["stop"].shape and align.shape == z["align"].shape
+    assert np.abs(mel - z["mel"].T).max() < 1e-5
+    assert np.abs(stop - z["stop"]).max() < 1e-5
+    assert np.abs(align - z["align"]).max() < 1e-6
+    np.testing.assert_array_equal(align.argmax(1), z["align"].argmax(1))
+    assert np.abs(o.postnet(mel) - z["mel_post"].T).max() < 1e-5

@@ -23,7 +23,7 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 # every symbol include/tts_hip.h declares
 EXPORTS = (
     "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state", "tts_encoder_last_path",
-    "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue",
+    "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue", "tts_decoder_run_teacher",
     "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
@@ -81,6 +81,8 @@ def _declare(lib):
                                     I32P, vp]
     lib.tts_encoder_run_state.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]
     lib.tts_decoder_run_continue.argtypes = lib.tts_decoder_run.argtypes
+    lib.tts_decoder_run_teacher.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int,
+                                            vp, vp, vp, vp]
     lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_decoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     lib.tts_encoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
@@ -122,7 +124,7 @@ def _declare(lib):
     for name in EXPORTS:
         fn = getattr(lib, name)
         if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet", "_state",
-                          "_continue", "_basis", "_melspectrogram", "_path", "_sync", "_phases")):
+                          "_continue", "_basis", "_melspectrogram", "_path", "_sync", "_phases", "_teacher")):
             fn.restype = ctypes.c_int
 
 

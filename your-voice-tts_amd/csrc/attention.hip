@@ -52,6 +52,23 @@ hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Teacher forcing (Decoder.forward, layers/tacotron2.py:227-247): the memory of step t is the go
+// frame at t = 0 (left by decoder_init_kernel) and teacher row t-1 otherwise (_reshape_memory:
+// frames (t-1) r .. t r - 1 of sentence b, contiguous in [B][T][80]); t comes from the device step slot.
+__global__ void teacher_memory_kernel(const float* frames, int64_t ldb, int width, const int* step, float* mem) {
+    const int b = blockIdx.x;
+    const int t = step[0];
+    if (t == 0) return;
+    const float* src = frames + (int64_t)b * ldb + (int64_t)(t - 1) * width;
+    for (int k = threadIdx.x; k < width; k += blockDim.x) mem[(int64_t)b * width + k] = src[k];
+}
+
+hipError_t launch_teacher_memory(const float* frames, int64_t ldb, int width, const int* step, float* mem, int B,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(teacher_memory_kernel, dim3(B), dim3(128), 0, s, frames, ldb, width, step, mem);
+    return hipGetLastError();
+}
+
 // Zero rows [n_steps[b], nmax) of a per-sentence history dst[b][step][width].
 __global__ void zero_tail_kernel(float* dst, int64_t ldb, const int* n_steps, int width, int nmax) {
     const int b = blockIdx.x;

@@ -94,6 +94,9 @@ hipError_t launch_query_energy(const QEArgs& a, int B, hipStream_t s);
 bool attention_uses_epart(const AttnArgs& a);
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
+// teacher forcing: mem[b] = teacher row step-1 of frames[b] (ldb floats per sentence), go frame at step 0
+hipError_t launch_teacher_memory(const float* frames, int64_t ldb, int width, const int* step, float* mem, int B,
+                                 hipStream_t s);
 hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int width, int nmax, int B, hipStream_t s);
 // enc_dim 512 (Tacotron2) or 256 (Tacotron / TacotronGST)
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s,

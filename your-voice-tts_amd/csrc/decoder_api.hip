@@ -108,7 +108,7 @@ tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, 
 // Launches of one decoder step of parity p (0: even step, 1: odd step).  `ev` (optional, 7
 // events) brackets every launch for tts_decoder_profile.
 tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, hipStream_t s,
-                        hipEvent_t* ev = nullptr) {
+                        hipEvent_t* ev = nullptr, int rule = 0) {
     int mark = 0;
 #define MARK() \
     if (ev) TTS_HIP(hipEventRecord(ev[mark++], s));
@@ -210,6 +210,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         m.done = d->done; m.n_steps = d->n_steps;
         m.state_next = d->state + 2 * q;
         m.max_steps = max_steps;
+        m.rule = rule;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_MEL_FUSED, s));
     }
@@ -233,11 +234,12 @@ tts_status build_graph(tts_decoder* d, int B, int Lmax, int max_steps, int first
     return TTS_OK;
 }
 
-// Step-0 prenet layer 1 on the go frame (later steps get it from the fused mel launch).
-tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s) {
+// Step-0 prenet layer 1 on the go frame (later steps get it from the fused mel launch; under
+// teacher forcing every step runs it on the teacher frame in mem, `slot` = that step's state slot).
+tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s, int* slot = nullptr) {
     SGemmArgs a{};
     a.B = B;
-    a.step = d->state;
+    a.step = slot ? slot : d->state;
     a.out_par = -1;
     a.seg[0] = Seg{d->mem, d->nmel, d->nmel};
     a.nseg = 1;
@@ -479,6 +481,58 @@ void tts_decoder_destroy(tts_decoder* d) {
 tts_status tts_decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax, int max_steps,
                            int steps_cap, float* mel, float* stop, float* align, int32_t* n_steps, void* stream) {
     return decoder_run(d, enc, lens, B, Lmax, max_steps, steps_cap, mel, stop, align, n_steps, stream, false);
+}
+
+tts_status tts_decoder_run_teacher(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,
+                                   const float* memories, int64_t mem_ldb, int steps, float* mel, float* stop,
+                                   float* align, void* stream) {
+    TTS_CHECK(d && enc && lens && memories && mel && stop, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(B >= 1 && B <= d->Bcap, TTS_ERR_INVALID, "batch exceeds decoder capacity");
+    TTS_CHECK(Lmax >= 2 && Lmax <= d->Lcap, TTS_ERR_INVALID, "Lmax exceeds decoder capacity");
+    TTS_CHECK(steps >= 1 && steps <= d->hist_cap, TTS_ERR_INVALID, "teacher steps exceed the decoder's history capacity");
+    TTS_CHECK(mem_ldb >= (int64_t)(steps - 1) * d->nmel, TTS_ERR_INVALID, "teacher memory rows too short");
+    for (int b = 0; b < B; ++b)
+        TTS_CHECK(lens[b] >= 2 && lens[b] <= Lmax, TTS_ERR_INVALID, "encoder length out of range [2, Lmax]");
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t s = d->stream;
+    TTS_HIP(hipEventRecord(d->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(s, d->ev_in, 0));
+    TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4, B,
+                             hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    TTS_HIP(launch_project_inputs(d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
+    InitArgs ia{};
+    ia.B = B; ia.Lcap = d->Lcap; ia.nmel = d->nmel; ia.lens = d->lens;
+    ia.att_init = d->att_init; ia.dec_init = d->dec_init; ia.go = d->go;
+    ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
+    ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
+    ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
+    ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
+    ia.step = d->state; ia.n_active = d->state + 1;
+    TTS_HIP(launch_decoder_init(ia, s));
+    // step t: memory = go frame (t = 0) or teacher row t-1 -> prenet layer 1 (reference weights, no
+    // fold) -> the inference step with the stop rule off (its fused launch's prenet-1 output is
+    // overwritten by the next step's teacher frame)
+    for (int t = 0; t < steps; ++t) {
+        const int p = t & 1;
+        TTS_HIP(launch_teacher_memory(memories, mem_ldb, d->nmel, d->state + 2 * p, d->mem, B, s));
+        tts_status st = enqueue_prenet_go(d, B, s, d->state + 2 * p);
+        if (!st) st = enqueue_step(d, B, Lmax, steps, p, s, nullptr, 2);
+        if (st) return st;
+    }
+    const size_t nm = d->nmel;
+    TTS_HIP(hipMemcpy2DAsync(mel, (size_t)steps * nm * 4, d->mel_hist, (size_t)d->hist_cap * nm * 4, (size_t)steps * nm * 4,
+                             B, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipMemcpy2DAsync(stop, (size_t)steps * 4, d->stop_hist, (size_t)d->hist_cap * 4, (size_t)steps * 4, B,
+                             hipMemcpyDeviceToDevice, s));
+    if (align)
+        TTS_HIP(hipMemcpy2DAsync(align, (size_t)steps * Lmax * 4, d->align_hist, (size_t)d->hist_cap * Lmax * 4,
+                                 (size_t)steps * Lmax * 4, B, hipMemcpyDeviceToDevice, s));
+    TTS_HIP(hipEventRecord(d->ev_out, s));
+    TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
+    d->last_resident = 0;
+    d->last_steps_done = 0;  // a later run_continue must start from a regular run
+    return TTS_OK;
 }
 
 tts_status tts_decoder_run_continue(tts_decoder* d, const float* enc, const int32_t* lens, int B, int Lmax,

@@ -288,10 +288,16 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             if (b < a.B) {
                 int nd = sr_done;
                 if (!nd) {
-                    const float stv = sigmoidf_(fin[b][col] + sr_bias);
+                    const float logit = fin[b][col] + sr_bias;
+                    // teacher forcing (rule 2, Decoder.forward) returns the stopnet logits
+                    const float stv = m.rule == 2 ? logit : sigmoidf_(logit);
                     if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
                     const int L = sr_len;
-                    if (m.rule == 1) {
+                    if (m.rule == 2) {
+                        // Decoder.forward (layers/tacotron2.py:227-247): no stop rule, the host runs
+                        // exactly the teacher's step count
+                        m.n_steps[b] = step + 1;
+                    } else if (m.rule == 1) {
                         // Tacotron (layers/tacotron.py:459-469), t = step + 1 after the append:
                         // t > L/4 and (stop > 0.6 [float32 compare] or alignment[-1].item() > 0.6
                         // [double compare]); elif t > max_decoder_steps

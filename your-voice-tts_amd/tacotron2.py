@@ -138,11 +138,12 @@ class Tacotron2:
             pass
 
     # ------------------------------------------------------------------ native handles
-    def _handles(self, Lmax, B):
+    def _handles(self, Lmax, B, need_steps=0):
         lib = _native.lib()
         if self.device.type != "cuda":
             self.cuda()
-        max_steps = int(self.decoder.max_decoder_steps)
+        # the decoder's history holds max_steps + 21 steps (teacher forcing may need more)
+        max_steps = max(int(self.decoder.max_decoder_steps), need_steps - 21)
         key = (max_steps, max(self.max_len, Lmax), max(self.max_batch, B))
         if self._native is not None and (self._native[2][0] != max_steps or self._native[2][1] < Lmax
                                          or self._native[2][2] < B):
@@ -245,6 +246,63 @@ class Tacotron2:
         self.last_lengths = frames
         return dict(mel=mel[:, :T], mel_post=mel_post[:, :T], align=align[:, :S], stop=stop[:, :S],
                     frames=frames, steps=steps, lens=lens)
+
+    @torch.no_grad()
+    def decoder_forward(self, inputs, memories, mask=None):
+        """Decoder.forward(inputs, memories, mask) (layers/tacotron2.py:227-247), eval mode, teacher
+        forcing: inputs [B, L, 512] encoder outputs, memories [B, T, 80] teacher mels, mask [B, L]
+        (True = valid position; None = every sentence spans L).  Step t decodes from the go frame or
+        teacher frame group t-1, T/r steps, no stop rule.  Returns (mel [B, 80, T], stop logits
+        [B, T/r], alignments [B, T/r, L]) like the reference; each sentence is decoded at its own
+        length (padding never attended)."""
+        _native.lib()
+        inputs = torch.as_tensor(inputs).to(self.device if self.device.type == "cuda" else "cuda").float().contiguous()
+        B, L = inputs.shape[0], inputs.shape[1]
+        lens = [L] * B if mask is None else [int(x) for x in torch.as_tensor(mask).reshape(B, -1).sum(1)]
+        if min(lens) < 2:
+            raise ValueError("encoder length must be >= 2 (common_layers.py:213)")
+        r = self.n_frames_per_step
+        memories = torch.as_tensor(memories).to(inputs.device).float().contiguous()
+        T = memories.shape[1]
+        if memories.dim() != 3 or memories.shape[0] != B or memories.shape[2] != 80 or T % r or T < r:
+            raise ValueError(f"memories must be [B, T, 80] with T a positive multiple of r={r}")
+        steps = T // r
+        lib, hdec, _ = self._handles(L, B, need_steps=steps)
+        mel = torch.empty(B, steps, 80 * r, device=inputs.device)
+        stop = torch.empty(B, steps, device=inputs.device)
+        align = torch.empty(B, steps, L, device=inputs.device)
+        _native.check(lib.tts_decoder_run_teacher(hdec, ctypes.c_void_p(inputs.data_ptr()), _native.i32_array(lens), B, L,
+                                                  ctypes.c_void_p(memories.data_ptr()), T * 80, steps,
+                                                  ctypes.c_void_p(mel.data_ptr()), ctypes.c_void_p(stop.data_ptr()),
+                                                  ctypes.c_void_p(align.data_ptr()), _native.stream_handle()),
+                      "tts_decoder_run_teacher")
+        return mel.view(B, steps * r, 80).transpose(1, 2), stop, align
+
+    @torch.no_grad()
+    def forward(self, text, text_lengths, mel_specs=None, speaker_ids=None):
+        """Tacotron2.forward (models/tacotron2.py:47-60) in eval mode (training is out of scope):
+        embedding + encoder at each sentence's length, teacher-forced decoder on mel_specs
+        [B, T, 80], Postnet + residual.  Returns (mel [B, T, 80], mel_post [B, T, 80],
+        alignments [B, T/r, L], stop logits [B, T/r]).  The reference's own forward cannot run on
+        torch >= 1.2 (`1 - mask` on a bool mask, common_layers.py:234); this is its intended result."""
+        if mel_specs is None:
+            raise ValueError("Tacotron2.forward needs mel_specs (teacher forcing)")
+        text = torch.as_tensor(text)
+        lens = [int(x) for x in torch.as_tensor(text_lengths).reshape(-1)]
+        B, Lmax = text.shape[0], max(lens)
+        if self.device.type != "cuda":
+            self.cuda()
+        enc = self.encode(text[:, :Lmax].to(self.device), lens, speaker_ids)
+        mask = torch.arange(Lmax)[None, :] < torch.as_tensor(lens)[:, None]
+        mel, stop, align = self.decoder_forward(enc, mel_specs, mask)
+        mel = mel.transpose(1, 2).contiguous()  # [B, T, 80]
+        T = mel.shape[1]
+        lib, _, hpost = self._handles(Lmax, B, need_steps=T // self.n_frames_per_step)
+        mel_post = torch.empty_like(mel)
+        _native.check(lib.tts_postnet_run(hpost, ctypes.c_void_p(mel.data_ptr()), _native.i32_array([T] * B), B, T,
+                                          ctypes.c_void_p(mel_post.data_ptr()), _native.stream_handle()),
+                      "tts_postnet_run")
+        return mel, mel_post, align, stop
 
     @torch.no_grad()
     def inference(self, text, speaker_ids=None):
