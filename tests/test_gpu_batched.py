@@ -53,7 +53,8 @@ def test_config2_batch64_unfused_griffin_lim_vs_oracle(audio_cfg):
 def test_config3_rank_share_sharded_vs_oracle_chain(audio_cfg):
     """configs[3]'s per-rank workload: rank 0's LPT share (64 sentences) of the 512-sentence seed-3
     job, through sharding.synthesize_sharded on a 1-rank RCCL group; two sentences (shortest,
-    longest) vs the full oracle chain ids -> Tacotron2 -> GL 60 with the device phases restated."""
+    longest) vs the oracle chain ids -> Tacotron2 -> GL 60 with the device phases restated, stage by
+    stage at 1e-4 (mel_post; GL of that mel_post) and compounded at 1e-3."""
     import torch.distributed as dist
     sh = load_pkg("sharding")
     w = weights_mod()
@@ -81,12 +82,22 @@ def test_config3_rank_share_sharded_vs_oracle_chain(audio_cfg):
     ao = AudioOracle(**audio_cfg)
     Ls = [len(x) for x in ids]
     for b in (int(np.argmin(Ls)), int(np.argmax(Ls))):
+        T = frames[b]
         ref = o.inference(ids[b])
-        assert ref["mel"].shape[0] == frames[b]
-        wav_ref = ao.inv_mel_spectrogram(ref["mel_post"].T, device_phase_u(40, b, frames[b]))
+        assert ref["mel"].shape[0] == T
+        # stage by stage at the north_star tolerance: the model's mel_post, then Griffin-Lim on it
+        mel_post = info["mel_post"][b, :T].cpu().numpy()
+        assert rel_rms(mel_post, ref["mel_post"]) < MEL_RTOL, b
+        pu = device_phase_u(40, b, T)
         got = info["wavs"][b].cpu().numpy()
-        assert got.shape == wav_ref.shape
-        assert rel_rms(got, wav_ref) < WAV_RTOL, b
+        gl_ref = ao.inv_mel_spectrogram(mel_post.T, pu)
+        assert got.shape == gl_ref.shape
+        assert rel_rms(got, gl_ref) < WAV_RTOL, b
+        # the compounded chain: Griffin-Lim amplifies the model's ~1e-7 fp32 reduction-order
+        # differences (60 iterations, phase retrieval is unstable where |X| ~ 0) by ~10^3 on the
+        # longest sentences, so the end-to-end waveform is held to 1e-3 (measured 1.5e-4 at T=342)
+        wav_ref = ao.inv_mel_spectrogram(ref["mel_post"].T, pu)
+        assert rel_rms(got, wav_ref) < 1e-3, b
 
 
 def test_config4_gst_batch32_linear_unfused_griffin_lim_vs_oracle():

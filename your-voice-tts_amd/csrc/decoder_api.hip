@@ -57,8 +57,6 @@ struct tts_decoder {
     unsigned long long* gran = nullptr;  // [2][GR_TOTAL] granules, then int status[4]
     long long res_ticks = 0;
     unsigned res_salt = 0;
-    float* sk_part = nullptr;     // batch > 16 split-K GEMM workspace (sgemm.h), null at max_batch <= 16
-    unsigned* sk_cnt = nullptr;
     float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
@@ -130,8 +128,6 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     g.step = st_cur;
     g.done = d->done;
     g.out_par = -1;
-    g.part = d->sk_part;
-    g.part_cnt = d->sk_cnt;
     // 1) prenet layer 2 -> xa_cur[b][0:256]   (common_layers.py:77-83; dropout off in eval)
     {
         SGemmArgs a = g;
@@ -452,14 +448,6 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->mel_hist, (size_t)Bc * d->hist_cap * nmel));
     CK(dmalloc(d, &d->stop_hist, (size_t)Bc * d->hist_cap));
     CK(dmalloc(d, &d->align_hist, (size_t)Bc * d->hist_cap * Lc));
-    if (Bc > 16) {  // the batch > 16 split-K GEMM path (sgemm.h) of the step launches
-        size_t ws = 0;
-        const int nk[4][2] = {{PRE, PRE}, {4 * HATT, XA + HATT}, {4 * HDEC, HATT + ENC + HDEC}, {nfused, HDEC + ENC}};
-        for (const auto& x : nk) ws = std::max(ws, sgemm_workspace_floats(x[0], x[1], Bc));
-        CK(dmalloc(d, &d->sk_part, ws));
-        CK(dmalloc(d, &d->sk_cnt, SGEMM_MAX_GROUPS));
-        HK(hipMemsetAsync(d->sk_cnt, 0, sizeof(unsigned) * SGEMM_MAX_GROUPS, s));
-    }
     HK(attention_prepare(Lc, cfg->location_attn));
     HK(hipMemsetAsync(d->xa, 0, sizeof(float) * 2 * Bc * XA, s));
     HK(hipMemsetAsync(d->h_att, 0, sizeof(float) * 2 * Bc * HATT, s));

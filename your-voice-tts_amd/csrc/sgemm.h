@@ -114,17 +114,7 @@ struct SGemmArgs {
     MelFused mf;          // EPI_MEL_FUSED only
     EncLstm enc;          // EPI_ENC_LSTM only
     GruEpi gru;           // EPI_GRU only
-    // batch > 16 split-K path (sgemm.hip: sgemm_sk_kernel), taken when both are set: partial
-    // fragments (>= sgemm_workspace_floats) and one zero-initialised counter per 64-row group
-    // (the kernel re-arms them); one launch at a time per workspace
-    float* part;
-    unsigned* part_cnt;
 };
-
-// split-K factor and workspace floats of the batch > 16 path for an N x K GEMM at batch B
-int sgemm_split_k(int N, int K);
-size_t sgemm_workspace_floats(int N, int K, int B);
-constexpr int SGEMM_MAX_GROUPS = 1024;  // counters to allocate (N <= 65536)
 
 // Row maps used when repacking reference matrices.
 enum RowMap { ROWMAP_IDENTITY = 0, ROWMAP_LSTM = 1, ROWMAP_GRU = 2 };

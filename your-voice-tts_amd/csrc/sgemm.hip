@@ -5,8 +5,6 @@
 //   prenet linear+relu, query_layer, linear_projection.
 // Roofline at B <= ~40: HBM/Infinity-Cache bound on the weight stream (each packed weight
 // byte is read exactly once per step by exactly one wave).
-#include <algorithm>
-
 #include "sgemm.h"
 
 namespace tts {
@@ -363,237 +361,6 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     }
 }
 
-// ---------------------------------------------------------------- batched split-K path (B > 16)
-// At batch 17..64 the kernel above is bound by its activation loads, not by the weight stream: every
-// one of its N/16 workgroups reads the whole [B x K] activation block as row-strided MFMA fragments
-// straight from L2.  Here a workgroup of 4 waves owns 64 output rows (one 16-row tile per wave) and
-// 1/ks of K: each k-chunk's activation block [B x 16] is staged once per workgroup through LDS
-// (coalesced, double-buffered) and read by all 4 waves, so activation traffic drops 4x and the
-// grid is N/64 x ks workgroups.  Partial accumulator fragments go to a workspace; the last
-// workgroup of a 64-row group to finish (device-scope counter) sums the ks parts in a FIXED order
-// (deterministic) and runs the epilogue, then re-arms the counter for the next launch.
-constexpr int SK_WAVES = 4;
-constexpr int SK_AST = 20;  // LDS row stride (floats) of a staged activation chunk (16 + pad)
-constexpr int SK_DEPTH = 8;  // k-chunks of loads in flight per thread
-
-template <int MT, int EPI, int ROLE>
-__global__ __launch_bounds__(64 * SK_WAVES) void sgemm_sk_kernel(const SGemmArgs a, int ks) {
-    const int grp = blockIdx.x, kp = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ntiles = (a.N + 15) >> 4;
-    const int ntile = grp * SK_WAVES + wave;
-    const bool has_tile = ntile < ntiles;
-    const int nchunks = a.K >> 4;
-    const int cbeg = kp * nchunks / ks, cend = (kp + 1) * nchunks / ks;
-    const int* sp = a.step ? a.step : kOneActive;
-    const int step = sp[0], n_active = sp[1];
-    if (n_active == 0) {
-        // every sentence is done: the fused stop launch still forwards {step+1, 0}
-        if (EPI == EPI_MEL_FUSED && grp == 0 && kp == 0 && tid == 0)
-            *reinterpret_cast<int2*>(a.mf.state_next) = make_int2(step + 1, 0);
-        return;
-    }
-    __shared__ __align__(16) float As[2][MT * 16][SK_AST];
-    __shared__ float fin[SK_WAVES][MT * 16][17];
-    __shared__ int s_last;
-    // activation staging: thread -> (row, k quad) of the [MT*16 x 16] chunk
-    const int arow = tid >> 2, aq = tid & 3;
-    const bool aload = arow < MT * 16 && arow < a.B;
-    const float* xs[3];
-    int cb[3];
-    {
-        int kstart = 0;
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            const Seg& g = a.seg[s];
-            const bool live = s < a.nseg;
-            xs[s] = (live && aload) ? g.p + (int64_t)arow * g.ld + aq * 4 - kstart : nullptr;
-            kstart += live ? g.len : 0;
-            cb[s] = kstart >> 4;
-        }
-    }
-    auto load_a = [&](int c) -> float4 {
-        if (c >= cend) return float4{0.f, 0.f, 0.f, 0.f};
-        const float* p = c < cb[0] ? xs[0] : (c < cb[1] ? xs[1] : xs[2]);
-        return p ? *reinterpret_cast<const float4*>(p + c * 16) : float4{0.f, 0.f, 0.f, 0.f};
-    };
-    const float4* __restrict__ Wp =
-        reinterpret_cast<const float4*>(a.W) + (size_t)(has_tile ? ntile : 0) * nchunks * 64 + lane;
-    auto load_w = [&](int c) -> float4 {
-        return (has_tile && c < cend) ? Wp[(size_t)c * 64] : float4{0.f, 0.f, 0.f, 0.f};
-    };
-    floatx4 acc[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // one workgroup per CU at the decoder shapes: latency is hidden by a register queue of
-    // SK_DEPTH chunks of activation + weight loads in flight per thread, not by occupancy
-    float4 aq_[SK_DEPTH], wq_[SK_DEPTH];
-#pragma unroll
-    for (int i = 0; i < SK_DEPTH; ++i) {
-        aq_[i] = load_a(cbeg + i);
-        wq_[i] = load_w(cbeg + i);
-    }
-    int buf = 0;
-    for (int c0 = cbeg; c0 < cend; c0 += SK_DEPTH) {
-#pragma unroll
-        for (int i = 0; i < SK_DEPTH; ++i) {
-            const int c = c0 + i;
-            if (c >= cend) break;  // uniform over the workgroup
-            if (arow < MT * 16) *reinterpret_cast<float4*>(&As[buf][arow][aq * 4]) = aq_[i];
-            __syncthreads();  // double buffer: the other buffer's readers all passed this barrier
-            aq_[i] = load_a(c + SK_DEPTH);
-            const float4 wv = wq_[i];
-            wq_[i] = load_w(c + SK_DEPTH);
-            if (has_tile) {
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const float4 xv =
-                        *reinterpret_cast<const float4*>(&As[buf][mt * 16 + (lane & 15)][(lane >> 4) * 4]);
-                    acc[mt] = mfma16x16x4(xv.x, wv.x, acc[mt]);
-                    acc[mt] = mfma16x16x4(xv.y, wv.y, acc[mt]);
-                    acc[mt] = mfma16x16x4(xv.z, wv.z, acc[mt]);
-                    acc[mt] = mfma16x16x4(xv.w, wv.w, acc[mt]);
-                }
-            }
-            buf ^= 1;
-        }
-    }
-    // partial fragments -> workspace [ks][ntiles][64 lanes][MT] float4
-    float4* part = reinterpret_cast<float4*>(a.part);
-    if (has_tile) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-            part[(((size_t)kp * ntiles + ntile) * 64 + lane) * MT + mt] =
-                float4{acc[mt][0], acc[mt][1], acc[mt][2], acc[mt][3]};
-    }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(&a.part_cnt[grp], 1u) == (unsigned)(ks - 1);
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    if (has_tile) {
-        floatx4 t[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) t[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < ks; ++k) {  // fixed order: deterministic
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                t[mt] += __builtin_nontemporal_load(
-                    reinterpret_cast<const floatx4*>(&part[(((size_t)k * ntiles + ntile) * 64 + lane) * MT + mt]));
-            }
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) fin[wave][mt * 16 + (lane >> 4) * 4 + r][lane & 15] = t[mt][r];
-    }
-    if (tid == 0) a.part_cnt[grp] = 0u;  // re-arm for the next launch (stream-ordered)
-    __syncthreads();
-
-    const bool track = a.hist != nullptr && step < a.hist_cap;
-    const int B = a.B;
-    if (EPI == EPI_LINEAR) {
-        float* out = a.out ? a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0) : nullptr;
-        for (int e = tid; e < SK_WAVES * B * 16; e += blockDim.x) {
-            const int w = e / (B * 16), b = (e >> 4) % B, col = e & 15;
-            const int n = (grp * SK_WAVES + w) * 16 + col;
-            if (n >= a.N) continue;
-            float v = fin[w][b][col] + (a.bias ? a.bias[n] : 0.f);
-            if (a.act == ACT_RELU) v = fmaxf(v, 0.f);
-            else if (a.act == ACT_SIGMOID) v = sigmoidf_(v);
-            if (out) out[(int64_t)b * a.ldo + n] = v;
-            if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
-            if (track && !(a.done && a.done[b])) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
-        }
-    } else if (EPI == EPI_LSTM || EPI == EPI_GRU) {
-        float* out = a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0);
-        for (int e = tid; e < SK_WAVES * B * 4; e += blockDim.x) {
-            const int w = e / (B * 4), b = (e >> 2) % B, u = e & 3;
-            const int nt = grp * SK_WAVES + w;
-            if (nt >= ntiles) continue;
-            const int unit = nt * 4 + u;
-            const float* bias = a.bias + nt * 16;
-            if (EPI == EPI_LSTM) {
-                const float gi = fin[w][b][u] + bias[u];
-                const float gf = fin[w][b][4 + u] + bias[4 + u];
-                const float gg = fin[w][b][8 + u] + bias[8 + u];
-                const float go = fin[w][b][12 + u] + bias[12 + u];
-                const float c2 = sigmoidf_(gf) * a.cell[(int64_t)b * a.ldc + unit] + sigmoidf_(gi) * tanhf(gg);
-                a.cell[(int64_t)b * a.ldc + unit] = c2;
-                out[(int64_t)b * a.ldo + unit] = sigmoidf_(go) * tanhf(c2);
-            } else {
-                const float hprev = a.gru.h[(int64_t)b * a.gru.ldh + unit];
-                const float r = sigmoidf_(fin[w][b][u] + bias[u]);
-                const float z = sigmoidf_(fin[w][b][4 + u] + bias[4 + u]);
-                const float n = tanhf((fin[w][b][8 + u] + bias[8 + u]) + r * (fin[w][b][12 + u] + bias[12 + u]));
-                const float h = (hprev - n) * z + n;
-                out[(int64_t)b * a.ldo + unit] = h;
-                if (a.gru.dout) a.gru.dout[(int64_t)b * a.gru.ldd + unit] = h + (a.gru.res ? a.gru.res[(int64_t)b * a.gru.ldr + unit] : 0.f);
-            }
-        }
-    } else if (EPI == EPI_MEL_FUSED) {
-        const MelFused& m = a.mf;
-        const int nrow = m.nmel + PRE_DIM + 1;
-        for (int e = tid; e < SK_WAVES * B * 16; e += blockDim.x) {
-            const int w = e / (B * 16), b = (e >> 4) % B, col = e & 15;
-            const int n = (grp * SK_WAVES + w) * 16 + col;
-            if (n >= nrow - 1) continue;  // the stop row below
-            const float v = fin[w][b][col] + a.bias[n];
-            if (n < m.nmel) {
-                // unguarded by done[] (as the small-batch kernel): rows past n_steps are masked by the host
-                if (track) a.hist[(int64_t)b * a.ldh + (int64_t)step * m.nmel + n] = v;
-            } else {
-                m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
-            }
-        }
-        const int stop_tile = (nrow - 1) >> 4;
-        if (stop_tile / SK_WAVES == grp) {
-            // stopnet + stop rule: as the small-batch kernel (tacotron2.py:219-224, 257-277;
-            // tacotron.py:464-469; rule 2 = teacher forcing)
-            __shared__ int sdone[64];
-            const int w = stop_tile - grp * SK_WAVES, col = (nrow - 1) & 15;
-            const int b = tid;
-            if (b < B) {
-                int nd = a.done[b];
-                if (!nd) {
-                    const float logit = fin[w][b][col] + a.bias[nrow - 1];
-                    const float stv = m.rule == 2 ? logit : sigmoidf_(logit);
-                    if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
-                    const int L = m.lens[b];
-                    if (m.rule == 2) {
-                        m.n_steps[b] = step + 1;
-                    } else if (m.rule == 1) {
-                        const int t1 = step + 1;
-                        if ((4 * t1 > L && (stv > 0.6f || (double)m.tail[b] > 0.6)) || t1 > m.max_steps) nd = 1;
-                    } else {
-                        const int f1 = m.flag1[b] | ((m.tail[b] > 0.8f && step > L) ? 1 : 0);
-                        m.flag1[b] = f1;
-                        if (f1 && step > 2 * L) {
-                            const int cnt = m.count[b] + 1;
-                            m.count[b] = cnt;
-                            if (cnt > 20) nd = 1;
-                        } else if (step + 1 == m.max_steps) {
-                            nd = 1;
-                        }
-                    }
-                    if (nd) {
-                        m.done[b] = 1;
-                        m.n_steps[b] = step + 1;
-                    }
-                }
-                sdone[b] = nd;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                int na = 0;
-                for (int k = 0; k < B; ++k) na += sdone[k] ? 0 : 1;
-                *reinterpret_cast<int2*>(m.state_next) = make_int2(step + 1, na);
-            }
-        }
-    }
-}
-
 __global__ void sgemm_pack_kernel(const float* A, int K1, const float* Bm, int K2, int N, int rowmap, int H,
                                   float* packed, size_t total) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -663,32 +430,12 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
     return hipGetLastError();
 }
 
-int sgemm_split_k(int N, int K) {
-    const int ngroups = ((N + 15) / 16 + SK_WAVES - 1) / SK_WAVES;
-    return std::max(1, std::min((K >> 4) / 4, (256 + ngroups - 1) / ngroups));
-}
-
-size_t sgemm_workspace_floats(int N, int K, int B) {
-    const int mt = B > 32 ? 4 : 2;
-    return (size_t)sgemm_split_k(N, K) * ((N + 15) / 16) * 64 * mt * 4;
-}
-
 template <int EPI, int ROLE>
 static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
-    const int mt = (a.B + 15) / 16;
-    if (EPI != EPI_ENC_LSTM && a.part && a.part_cnt && mt >= 2) {
-        // batch > 16: split-K with the activation chunk staged once per 64-row workgroup
-        const int ks = sgemm_split_k(a.N, a.K);
-        const dim3 grid(((a.N + 15) / 16 + SK_WAVES - 1) / SK_WAVES, ks), block(SK_WAVES * 64);
-        if (mt <= 2)
-            hipLaunchKernelGGL((sgemm_sk_kernel<2, EPI, ROLE>), grid, block, 0, s, a, ks);
-        else
-            hipLaunchKernelGGL((sgemm_sk_kernel<4, EPI, ROLE>), grid, block, 0, s, a, ks);
-        return hipGetLastError();
-    }
     // always 16 waves (waves past K's chunk count contribute zeros): the epilogues give every
     // (row, column) of the tile its own thread, B * 16 <= 1024
     const dim3 grid((a.N + 15) / 16), block(MAX_WAVES * 64);
+    const int mt = (a.B + 15) / 16;
     if (a.B == 1)
         hipLaunchKernelGGL((sgemm_kernel<0, EPI, ROLE>), grid, block, 0, s, a);
     else if (mt <= 1)

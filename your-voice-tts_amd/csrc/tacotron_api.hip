@@ -88,8 +88,6 @@ struct tts_tacotron {
     float *W_ll = nullptr, *b_ll = nullptr;
     // decoder workspace
     int Bcap = 0, Lcap = 0, hist_cap = 0;
-    float* sk_part = nullptr;    // batch > 16 split-K GEMM workspace (sgemm.h), null at max_batch <= 16
-    unsigned* sk_cnt = nullptr;
     float *denc = nullptr, *Pt = nullptr, *h_att = nullptr, *h1 = nullptr, *h2 = nullptr, *xa = nullptr;
     float *mem = nullptr, *pre1 = nullptr, *q = nullptr, *din = nullptr, *d1 = nullptr, *d2 = nullptr;
     float *epart = nullptr, *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
@@ -443,8 +441,6 @@ tts_status enqueue_step(tts_tacotron* t, int B, int Lmax, int max_steps, int p, 
     g.step = st_cur;
     g.done = t->done;
     g.out_par = -1;
-    g.part = t->sk_part;
-    g.part_cnt = t->sk_cnt;
     {  // 1) prenet layer 2 (common_layers.py:77-83) -> xa_cur[0:128]
         SGemmArgs a = g;
         a.seg[0] = Seg{t->pre1, T_PRE1, T_PRE1};
@@ -791,20 +787,6 @@ tts_status create_workspace(tts_tacotron* t, hipStream_t s) {
     CK(talloc(t, &t->d1, (size_t)Bc * T_DEC));
     CK(talloc(t, &t->d2, (size_t)Bc * T_DEC));
     CK(talloc(t, &t->epart, (size_t)Bc * QE_TILES * Lc));
-    if (Bc > 16) {  // the batch > 16 split-K GEMM path (sgemm.h) of the step launches
-        size_t ws = 0;
-        const int nk[7][2] = {{T_PRE2, T_PRE1}, {4 * T_DEC, T_XA + T_DEC}, {ADIM, T_DEC}, {T_DEC, 2 * T_DEC},
-                              {4 * T_DEC, 2 * T_DEC}, {t->nmel, T_DEC}, {T_PRE1 + 1, t->nmel + T_DEC}};
-        for (const auto& x : nk) ws = std::max(ws, sgemm_workspace_floats(x[0], x[1], Bc));
-        CK(talloc(t, &t->sk_part, ws));
-        float* cnt = nullptr;
-        CK(talloc(t, &cnt, SGEMM_MAX_GROUPS));
-        t->sk_cnt = reinterpret_cast<unsigned*>(cnt);
-        if (hipMemsetAsync(t->sk_cnt, 0, sizeof(unsigned) * SGEMM_MAX_GROUPS, s) != hipSuccess) {
-            set_error("hipMemsetAsync failed");
-            return TTS_ERR_HIP;
-        }
-    }
     CK(talloc(t, &t->alpha, (size_t)Bc * Lc));
     CK(talloc(t, &t->att_w, (size_t)Bc * Lc));
     CK(talloc(t, &t->att_cum, (size_t)Bc * Lc));

@@ -158,6 +158,7 @@ def synthesize_sharded(model, ap, ids_list, group=None, seed=0, max_batch=None):
         wavs = [wav_dev[k, :n] for k, n in enumerate(inf["samples"])]
         info["frames"] = inf["frames"]
         info["gl_iterations"] = inf["gl_iterations"]
+        info["mel_post"] = inf["mel_post"]  # this rank's batch, padded [B, Tmax, 80] (batch order = partition)
     peak = global_peak(wavs, group)
     allw = gather_waveforms(wavs, mine, len(ids_list), group)
     if rank != 0:
