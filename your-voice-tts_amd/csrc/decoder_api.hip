@@ -209,6 +209,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         m.lens = d->lens; m.tail = d->tail; m.flag1 = d->flag1; m.count = d->count;
         m.done = d->done; m.n_steps = d->n_steps;
         m.state_next = d->state + 2 * q;
+        m.stop_acc = d->state + 4;
         m.max_steps = max_steps;
         m.rule = rule;
         MARK();
@@ -444,7 +445,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->count, Bc));
     CK(dmalloc(d, &d->done, Bc));
     CK(dmalloc(d, &d->n_steps, Bc));
-    CK(dmalloc(d, &d->state, 4));  // {step, n_active} x 2 parities; kernels load one slot as int2
+    CK(dmalloc(d, &d->state, 8));  // {step, n_active} x 2 parities (kernels load one slot as int2), stop_acc
     CK(dmalloc(d, &d->mel_hist, (size_t)Bc * d->hist_cap * nmel));
     CK(dmalloc(d, &d->stop_hist, (size_t)Bc * d->hist_cap));
     CK(dmalloc(d, &d->align_hist, (size_t)Bc * d->hist_cap * Lc));
@@ -455,7 +456,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     HK(hipMemsetAsync(d->mem, 0, sizeof(float) * Bc * nmel, s));
     HK(hipMemsetAsync(d->enc, 0, sizeof(float) * Bc * Lc * ENC, s));
     HK(hipMemsetAsync(d->Pt, 0, sizeof(float) * Bc * ADIM * Lc, s));
-    HK(hipMemsetAsync(d->state, 0, sizeof(int) * 4, s));
+    HK(hipMemsetAsync(d->state, 0, sizeof(int) * 8, s));
     HK(hipStreamSynchronize(s));
 #undef CK
 #undef HK

@@ -84,6 +84,7 @@ struct MelFused {
     int* done;
     int* n_steps;
     int* state_next;  // int2 {t+1, n_active} read by the next step (other parity slot)
+    int* stop_acc;    // zero at rest: the row groups' active counts meet here (grid.y > 1)
     int max_steps;
     int rule;  // 0: Tacotron2 stop rule (layers/tacotron2.py:267-277); 1: Tacotron (layers/tacotron.py:464-469);
                // 2: teacher forcing (Decoder.forward, layers/tacotron2.py:227-247): no rule, stop logits

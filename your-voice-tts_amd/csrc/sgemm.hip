@@ -5,6 +5,8 @@
 //   prenet linear+relu, query_layer, linear_projection.
 // Roofline at B <= ~40: HBM/Infinity-Cache bound on the weight stream (each packed weight
 // byte is read exactly once per step by exactly one wave).
+#include <cstdlib>
+
 #include "sgemm.h"
 
 namespace tts {
@@ -15,6 +17,89 @@ constexpr int MAX_WAVES = 16;
 #endif
 constexpr int PRE_DIM = 256;  // prenet width (layers/tacotron2.py:108)
 __device__ const int kOneActive[2] = {0, 1};  // {step 0, 1 active} for launches without step state
+
+// Activation addressing of one lane: segments p0 | p1 | p2 of the concatenated row (wave-uniform
+// bases shifted by each segment's first k, row strides, first chunk past segments 0 and 1) and
+// the lane's rows (one per m-tile) and k offset.
+template <int NT>
+struct XAddr {
+    const float *p0 = nullptr, *p1 = nullptr, *p2 = nullptr;
+    int ld0 = 0, ld1 = 0, ld2 = 0, cb0 = 0, cb1 = 0;
+    int row[NT];
+    int xk = 0;
+};
+
+// One pipeline stage: the weight fragment and the NT activation fragments of chunks
+// [c0, c0 + UP).  Chunks past cend load chunk cend-1 again (callers skip their FMAs): every load
+// is unconditional, so the wait before a stage's MFMAs counts exactly the next stage's loads
+// (a load under a branch makes the compiler wait for everything).  Requires cend > c0.
+template <int UP, int NT, int ROLE>
+__device__ __forceinline__ void sg_load(const float4* __restrict__ Wp, const XAddr<NT> xa, int c0, int cend,
+                                        float4 (&wv)[UP], float4 (&xv)[UP][NT]) {
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+        const int c = min(c0 + u, cend - 1);
+        if ((TTS_NT_ROLES >> ROLE) & 1) {
+            // non-temporal (stream) policy: this matrix passes through L2 without evicting the
+            // default-policy matrices that stay resident there across steps
+            const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(Wp + (size_t)c * 64));
+            wv[u] = float4{t[0], t[1], t[2], t[3]};
+        } else {
+            wv[u] = Wp[(size_t)c * 64];
+        }
+        // wave-uniform segment: scalar base + c*16 and row stride, per-lane row and k
+        const bool s0 = c < xa.cb0, s1 = c < xa.cb1;
+        const float* base = (s0 ? xa.p0 : (s1 ? xa.p1 : xa.p2)) + c * 16 + xa.xk;
+        const int ld = s0 ? xa.ld0 : (s1 ? xa.ld1 : xa.ld2);
+#pragma unroll
+        for (int mt = 0; mt < NT; ++mt) xv[u][mt] = *reinterpret_cast<const float4*>(base + xa.row[mt] * ld);
+    }
+}
+
+// The MFMAs of one stage; chunk u accumulates into chain u & 1 at NT == 1 (two independent
+// chains hide the MFMA latency), into the m-tile's one chain otherwise (NT chains interleave).
+template <int UP, int NT>
+__device__ __forceinline__ void sg_mfma(int c0, int cend, const float4 (&wv)[UP], const float4 (&xv)[UP][NT],
+                                        floatx4 (&acc)[2][NT]) {
+    if (NT == 1) {
+        static_assert(NT != 1 || UP % 2 == 0, "NT == 1 pairs chunks");
+#pragma unroll
+        for (int u = 0; u < UP; u += 2) {
+            floatx4& a0 = acc[0][0];
+            floatx4& a1 = acc[1][0];
+            if (c0 + u + 1 < cend) {  // wave-uniform
+                a0 = mfma16x16x4(xv[u][0].x, wv[u].x, a0);
+                a1 = mfma16x16x4(xv[u + 1][0].x, wv[u + 1].x, a1);
+                a0 = mfma16x16x4(xv[u][0].y, wv[u].y, a0);
+                a1 = mfma16x16x4(xv[u + 1][0].y, wv[u + 1].y, a1);
+                a0 = mfma16x16x4(xv[u][0].z, wv[u].z, a0);
+                a1 = mfma16x16x4(xv[u + 1][0].z, wv[u + 1].z, a1);
+                a0 = mfma16x16x4(xv[u][0].w, wv[u].w, a0);
+                a1 = mfma16x16x4(xv[u + 1][0].w, wv[u + 1].w, a1);
+            } else if (c0 + u < cend) {
+                a0 = mfma16x16x4(xv[u][0].x, wv[u].x, a0);
+                a0 = mfma16x16x4(xv[u][0].y, wv[u].y, a0);
+                a0 = mfma16x16x4(xv[u][0].z, wv[u].z, a0);
+                a0 = mfma16x16x4(xv[u][0].w, wv[u].w, a0);
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+        if (c0 + u < cend) {  // wave-uniform: no MFMAs on the padding of the last stage
+            floatx4* ac = acc[0];
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, ac[mt]);
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, ac[mt]);
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, ac[mt]);
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, ac[mt]);
+        }
+    }
+}
 
 // ROLE only names the instantiation (distinct kernel names in rocprof traces per decoder stage).
 // MT = m-tiles of 16 batch rows on the MFMA path; MT = 0 is the batch-1 VALU path.
@@ -36,36 +121,41 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
     const int nw = blockDim.x >> 6;
     const int tid = threadIdx.x;
+    // row group: this workgroup's batch rows [m0, m0 + Bh) (grid.y > 1 splits the batch over
+    // workgroups, sgemm_launch)
+    const int m0 = blockIdx.y * 16 * NT;
+    const int Bh = min(a.B - m0, 16 * NT);
     float pre_bias[4] = {0.f, 0.f, 0.f, 0.f}, pre_cell = 0.f;
     int pre_done = 0;
-    if ((EPI == EPI_LINEAR || EPI == EPI_MEL_FUSED) && tid < a.B * 16) {
+    if ((EPI == EPI_LINEAR || EPI == EPI_MEL_FUSED) && tid < Bh * 16) {
         const int n = ntile * 16 + (tid & 15);
         if (a.bias && n < a.N) pre_bias[0] = a.bias[n];
-        if (a.done) pre_done = a.done[tid >> 4];
+        if (a.done) pre_done = a.done[m0 + (tid >> 4)];
     }
-    // stop-rule operands of the fused mel launch (one workgroup, one thread per sentence)
+    // stop-rule operands of the fused mel launch (one workgroup per row group, one thread per
+    // sentence)
     const int stop_tile = EPI == EPI_MEL_FUSED ? (a.mf.nmel + PRE_DIM) >> 4 : -1;
     int sr_done = 1, sr_len = 0, sr_flag = 0, sr_count = 0;
     float sr_tail = 0.f, sr_bias = 0.f;
-    if (EPI == EPI_MEL_FUSED && ntile == stop_tile && tid < a.B) {
-        sr_done = a.done[tid];
-        sr_len = a.mf.lens[tid];
-        sr_flag = a.mf.flag1[tid];
-        sr_count = a.mf.count[tid];
-        sr_tail = a.mf.tail[tid];
+    if (EPI == EPI_MEL_FUSED && ntile == stop_tile && tid < Bh) {
+        sr_done = a.done[m0 + tid];
+        sr_len = a.mf.lens[m0 + tid];
+        sr_flag = a.mf.flag1[m0 + tid];
+        sr_count = a.mf.count[m0 + tid];
+        sr_tail = a.mf.tail[m0 + tid];
         // lane-dependent index (B <= 64, so tid & (B >> 8) == 0): a vector load, waited late,
         // not a scalar one waited at the next kernel-argument load
         sr_bias = a.bias[a.mf.nmel + PRE_DIM + (tid & (a.B >> 8))];
     }
-    if (EPI == EPI_LSTM && tid < a.B * 4) {
-        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+    if (EPI == EPI_LSTM && tid < Bh * 4) {
+        const int b = m0 + (threadIdx.x >> 2), u = threadIdx.x & 3;
 #pragma unroll
         for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
         pre_cell = a.cell[(int64_t)b * a.ldc + ntile * 4 + u];
     }
     float pre_res = 0.f;  // EPI_GRU: residual input of this (sentence, unit)
-    if (EPI == EPI_GRU && tid < a.B * 4) {
-        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+    if (EPI == EPI_GRU && tid < Bh * 4) {
+        const int b = m0 + (threadIdx.x >> 2), u = threadIdx.x & 3;
 #pragma unroll
         for (int g = 0; g < 4; ++g) pre_bias[g] = a.bias[ntile * 16 + g * 4 + u];
         pre_cell = a.gru.h[(int64_t)b * a.gru.ldh + ntile * 4 + u];  // h_{t-1}
@@ -73,9 +163,9 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     }
     const int dir = EPI == EPI_ENC_LSTM ? ntile / a.enc.tiles_per_dir : 0;
     int enc_pos = -1;  // encoder position this thread's (b, unit) updates, -1 when idle
-    if (EPI == EPI_ENC_LSTM && (int)threadIdx.x < a.B * 4) {
+    if (EPI == EPI_ENC_LSTM && (int)threadIdx.x < Bh * 4) {
         const EncLstm& E = a.enc;
-        const int b = threadIdx.x >> 2, u = threadIdx.x & 3;
+        const int b = m0 + (threadIdx.x >> 2), u = threadIdx.x & 3;
         const int unit = (ntile - dir * E.tiles_per_dir) * 4 + u;
         const int L = E.lens[b];
         if (E.s < L) {
@@ -90,97 +180,74 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     const int cbeg = wave * nchunks / nw;
     const int cend = (wave + 1) * nchunks / nw;
 
-    // Per-lane activation base pointers: row b = mt*16 + (lane&15) (VALU path: row 0 for every
-    // lane), k offset (lane>>4)*4.
+    // Activation addressing (XAddr): a wave-uniform base and stride per segment, per lane the
+    // row b = m0 + mt*16 + (lane&15) of each m-tile (VALU path: row 0 for every lane) and the k
+    // offset (lane>>4)*4.  Rows past the batch read row B-1 instead: an MFMA output row depends
+    // on its own input row only, and the epilogue never stores rows >= B.
     const int xrow = VALU ? 0 : lane & 15;
     const int xk = (lane >> 4) * 4;
-    const float* xb[3][NT];
-    int cb[3];
+    XAddr<NT> xa;
     int kstart = 0;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
         // the encoder LSTM reads one segment: its direction's previous hidden state
         const Seg& g = a.seg[EPI == EPI_ENC_LSTM ? (s == 0 ? dir : 2) : s];
         const bool live = EPI == EPI_ENC_LSTM ? s == 0 : s < a.nseg;
-#pragma unroll
-        for (int mt = 0; mt < NT; ++mt) {
-            const int b = mt * 16 + xrow;
-            xb[s][mt] = (live && b < a.B) ? g.p + (int64_t)b * g.ld + xk - kstart : nullptr;
-        }
+        const float* base = live ? g.p - kstart : nullptr;
+        const int ld = live ? g.ld : 0;
         kstart += live ? g.len : 0;
-        cb[s] = kstart >> 4;  // first chunk past segment s
+        if (s == 0) { xa.p0 = base; xa.ld0 = ld; xa.cb0 = kstart >> 4; }
+        if (s == 1) { xa.p1 = base; xa.ld1 = ld; xa.cb1 = kstart >> 4; }
+        if (s == 2) { xa.p2 = base; xa.ld2 = ld; }
     }
-
-    // two independent accumulator chains per m-tile (even / odd chunk) hide the MFMA latency
-    floatx4 acc[NT], acc2[NT];
 #pragma unroll
-    for (int mt = 0; mt < NT; ++mt) acc[mt] = acc2[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < NT; ++mt) xa.row[mt] = min(m0 + mt * 16 + xrow, a.B - 1);
+    xa.xk = xk;
+
+    floatx4 acc[2][NT];  // MFMA accumulators (see sg_mfma)
+#pragma unroll
+    for (int mt = 0; mt < NT; ++mt) acc[0][mt] = acc[1][mt] = floatx4{0.f, 0.f, 0.f, 0.f};
     float vacc = 0.f, vacc2 = 0.f;  // VALU path
 
     const float4* __restrict__ Wp = reinterpret_cast<const float4*>(a.W) + (size_t)ntile * nchunks * 64 + lane;
-    // U chunks of loads (U KiB of weights per wave) in flight before the first FMA; at batch
-    // <= 16 one round covers every decoder shape (<= 10 chunks per wave at 16 waves, K <= 2560)
-    constexpr int U = NT == 1 ? 10 : (NT == 2 ? 4 : 2);
-    for (int c0 = cbeg; c0 < cend; c0 += U) {
+    if (!VALU) {
+        // Two register stages of UP chunks: the loads of stage s+1 are in flight while stage s
+        // runs its MFMAs (one memory round trip exposed per wave, not one per stage).  At batch
+        // <= 16 one stage of 4 covers most of a wave's chunks; at 64 a wave owns 10 chunks of
+        // the widest GEMM, 5 stages of 2.
+        constexpr int UP = NT == 1 ? 4 : 2;
+        float4 wA[UP], xA[UP][NT], wB[UP], xB[UP][NT];
+        if (cbeg < cend) sg_load<UP, NT, ROLE>(Wp, xa, cbeg, cend, wA, xA);
+        for (int c0 = cbeg; c0 < cend; c0 += 2 * UP) {
+            sg_load<UP, NT, ROLE>(Wp, xa, c0 + UP, cend, wB, xB);
+            sg_mfma<UP, NT>(c0, cend, wA, xA, acc);
+            if (c0 + UP >= cend) break;
+            sg_load<UP, NT, ROLE>(Wp, xa, c0 + 2 * UP, cend, wA, xA);
+            sg_mfma<UP, NT>(c0 + UP, cend, wB, xB, acc);
+        }
+    }
+    // VALU path (batch 1): U chunks of loads (U KiB of weights per wave) in flight before the
+    // first FMA; one round covers every decoder shape (<= 10 chunks per wave at 16 waves, K <= 2560)
+    constexpr int U = 10;
+    for (int c0 = cbeg; VALU && c0 < cend; c0 += U) {
         float4 wv[U];
         float4 xv[U][NT];
+        sg_load<U, NT, ROLE>(Wp, xa, c0, cend, wv, xv);
+        // lane (row n = lane&15, k-group lane>>4) dots its 4 weights with x; the MFMA path would
+        // pad the batch to 16 rows and pay 16x the multiplies
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int c = c0 + u;
-            if (c < cend) {
-                if ((TTS_NT_ROLES >> ROLE) & 1) {
-                    // non-temporal (stream) policy: this matrix passes through L2 without evicting
-                    // the default-policy matrices that stay resident there across steps
-                    const floatx4 t = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(Wp + (size_t)c * 64));
-                    wv[u] = float4{t[0], t[1], t[2], t[3]};
-                } else {
-                    wv[u] = Wp[(size_t)c * 64];
-                }
-                const int s = c < cb[0] ? 0 : (c < cb[1] ? 1 : 2);
-#pragma unroll
-                for (int mt = 0; mt < NT; ++mt) {
-                    const float* p = s == 0 ? xb[0][mt] : (s == 1 ? xb[1][mt] : xb[2][mt]);
-                    xv[u][mt] = p ? *reinterpret_cast<const float4*>(p + c * 16) : float4{0.f, 0.f, 0.f, 0.f};
-                }
-            } else {
-                wv[u] = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int mt = 0; mt < NT; ++mt) xv[u][mt] = float4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < U; u += 2) {
+            if (c0 + u < cend) {
+                vacc = fmaf(wv[u].x, xv[u][0].x, vacc);
+                vacc = fmaf(wv[u].y, xv[u][0].y, vacc);
+                vacc = fmaf(wv[u].z, xv[u][0].z, vacc);
+                vacc = fmaf(wv[u].w, xv[u][0].w, vacc);
             }
-        }
-        if (VALU) {
-            // batch 1: lane (row n = lane&15, k-group lane>>4) dots its 4 weights with x; the
-            // MFMA path would pad the batch to 16 rows and pay 16x the multiplies
-#pragma unroll
-            for (int u = 0; u < U; u += 2) {
-                if (c0 + u < cend) {
-                    vacc = fmaf(wv[u].x, xv[u][0].x, vacc);
-                    vacc = fmaf(wv[u].y, xv[u][0].y, vacc);
-                    vacc = fmaf(wv[u].z, xv[u][0].z, vacc);
-                    vacc = fmaf(wv[u].w, xv[u][0].w, vacc);
-                }
-                if (c0 + u + 1 < cend) {
-                    vacc2 = fmaf(wv[u + 1].x, xv[u + 1][0].x, vacc2);
-                    vacc2 = fmaf(wv[u + 1].y, xv[u + 1][0].y, vacc2);
-                    vacc2 = fmaf(wv[u + 1].z, xv[u + 1][0].z, vacc2);
-                    vacc2 = fmaf(wv[u + 1].w, xv[u + 1][0].w, vacc2);
-                }
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; u += 2) {
-                if (c0 + u >= cend) break;  // no MFMAs on the zero padding of the last round
-#pragma unroll
-                for (int mt = 0; mt < NT; ++mt) {
-                    acc[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, acc[mt]);
-                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].x, wv[u + 1].x, acc2[mt]);
-                    acc[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, acc[mt]);
-                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].y, wv[u + 1].y, acc2[mt]);
-                    acc[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, acc[mt]);
-                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].z, wv[u + 1].z, acc2[mt]);
-                    acc[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, acc[mt]);
-                    acc2[mt] = mfma16x16x4(xv[u + 1][mt].w, wv[u + 1].w, acc2[mt]);
-                }
+            if (c0 + u + 1 < cend) {
+                vacc2 = fmaf(wv[u + 1].x, xv[u + 1][0].x, vacc2);
+                vacc2 = fmaf(wv[u + 1].y, xv[u + 1][0].y, vacc2);
+                vacc2 = fmaf(wv[u + 1].z, xv[u + 1][0].z, vacc2);
+                vacc2 = fmaf(wv[u + 1].w, xv[u + 1][0].w, vacc2);
             }
         }
     }
@@ -190,10 +257,9 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         float v = vacc + vacc2;
         v += __shfl_xor(v, 16, 64);
         v += __shfl_xor(v, 32, 64);
-        acc[0] = floatx4{lane < 16 ? v : 0.f, 0.f, 0.f, 0.f};
-    } else {
-#pragma unroll
-        for (int mt = 0; mt < NT; ++mt) acc[mt] += acc2[mt];
+        acc[0][0] = floatx4{lane < 16 ? v : 0.f, 0.f, 0.f, 0.f};
+    } else if (NT == 1) {
+        acc[0][0] += acc[1][0];
     }
 
     // Operands loaded in the prologue are consumed only from here on; the empty asm redefines
@@ -203,7 +269,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     if (st_y == 0) {
         // every sentence is done: steps past the end are no-ops, but the fused stop launch
         // still forwards {step+1, 0} so the next parity slot reads "done" as well
-        if (EPI == EPI_MEL_FUSED && ntile == 0 && tid == 0)
+        if (EPI == EPI_MEL_FUSED && ntile == 0 && blockIdx.y == 0 && tid == 0)
             *reinterpret_cast<int2*>(a.mf.state_next) = make_int2(st_x + 1, 0);
         return;
     }
@@ -214,10 +280,10 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     __shared__ float fin[NT * 16][17];
 #pragma unroll
     for (int mt = 0; mt < NT; ++mt) {
-        red[wave][mt][lane][0] = acc[mt].x;
-        red[wave][mt][lane][1] = acc[mt].y;
-        red[wave][mt][lane][2] = acc[mt].z;
-        red[wave][mt][lane][3] = acc[mt].w;
+        red[wave][mt][lane][0] = acc[0][mt].x;
+        red[wave][mt][lane][1] = acc[0][mt].y;
+        red[wave][mt][lane][2] = acc[0][mt].z;
+        red[wave][mt][lane][3] = acc[0][mt].w;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
@@ -231,11 +297,11 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     const bool track = a.hist != nullptr && step < a.hist_cap;
     if (EPI == EPI_LINEAR) {
         float* out = a.out ? a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0) : nullptr;
-        if (tid < a.B * 16) {  // B <= 64: one element per thread
-            const int b = tid >> 4, col = tid & 15;
+        if (tid < Bh * 16) {  // B <= 64: one element per thread
+            const int bl = tid >> 4, col = tid & 15, b = m0 + bl;
             const int n = ntile * 16 + col;
             if (n < a.N) {
-                float v = fin[b][col] + pre_bias[0];
+                float v = fin[bl][col] + pre_bias[0];
                 if (a.act == ACT_RELU) v = fmaxf(v, 0.f);
                 else if (a.act == ACT_SIGMOID) v = sigmoidf_(v);
                 if (out) out[(int64_t)b * a.ldo + n] = v;
@@ -246,13 +312,13 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     } else if (EPI == EPI_ENC_LSTM) {
         const EncLstm& E = a.enc;
         const int e = threadIdx.x;
-        if (e < a.B * 4 && enc_pos >= 0) {
-            const int b = e >> 2, u = e & 3;
+        if (e < Bh * 4 && enc_pos >= 0) {
+            const int bl = e >> 2, u = e & 3, b = m0 + bl;
             const int unit = (ntile - dir * E.tiles_per_dir) * 4 + u;
-            const float gi = fin[b][u] + pre_bias[0];
-            const float gf = fin[b][4 + u] + pre_bias[1];
-            const float gg = fin[b][8 + u] + pre_bias[2];
-            const float go = fin[b][12 + u] + pre_bias[3];
+            const float gi = fin[bl][u] + pre_bias[0];
+            const float gf = fin[bl][4 + u] + pre_bias[1];
+            const float gg = fin[bl][8 + u] + pre_bias[2];
+            const float go = fin[bl][12 + u] + pre_bias[3];
             const float c2 = sigmoidf_(gf) * pre_cell + sigmoidf_(gi) * tanhf(gg);
             const float h = sigmoidf_(go) * tanhf(c2);
             E.c[dir * E.cstride + (int64_t)b * E.H + unit] = c2;
@@ -262,11 +328,11 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     } else if (EPI == EPI_MEL_FUSED) {
         const MelFused& m = a.mf;
         const int nrow = m.nmel + PRE_DIM + 1;
-        if (tid < a.B * 16) {
-            const int b = tid >> 4, col = tid & 15;
+        if (tid < Bh * 16) {
+            const int bl = tid >> 4, col = tid & 15, b = m0 + bl;
             const int n = ntile * 16 + col;
             if (n < nrow - 1) {  // stop row handled below
-                const float v = fin[b][col] + pre_bias[0];
+                const float v = fin[bl][col] + pre_bias[0];
                 if (n < m.nmel) {
                     // unguarded by done[]: the stop WG of this same launch may set it; rows past
                     // n_steps are garbage the host masks out (tts_decoder_run zero-fills them)
@@ -282,13 +348,13 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             // checked only in the `elif`, so a sentence whose flags are all set may pass it.
             __shared__ int sdone[64];
             const int col = (nrow - 1) & 15;
-            const int b = tid;
+            const int bl = tid, b = m0 + tid;
             asm volatile("" : "+v"(sr_done), "+v"(sr_len), "+v"(sr_flag), "+v"(sr_count), "+v"(sr_tail),
                          "+v"(sr_bias));
-            if (b < a.B) {
+            if (bl < Bh) {
                 int nd = sr_done;
                 if (!nd) {
-                    const float logit = fin[b][col] + sr_bias;
+                    const float logit = fin[bl][col] + sr_bias;
                     // teacher forcing (rule 2, Decoder.forward) returns the stopnet logits
                     const float stv = m.rule == 2 ? logit : sigmoidf_(logit);
                     if (track) m.stop_hist[(int64_t)b * m.stop_ldb + step] = stv;
@@ -319,12 +385,21 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                         m.n_steps[b] = step + 1;
                     }
                 }
-                sdone[b] = nd;
+                sdone[bl] = nd;
             }
             __syncthreads();
             if (threadIdx.x == 0) {
                 int na = 0;
-                for (int k = 0; k < a.B; ++k) na += sdone[k] ? 0 : 1;
+                for (int k = 0; k < Bh; ++k) na += sdone[k] ? 0 : 1;
+                if (gridDim.y > 1) {
+                    // row groups: each stop workgroup adds (1 << 16 | its active count) to the
+                    // zeroed accumulator; the last to arrive owns the total (the counts travel in
+                    // the atomic itself: no other data is handed over), publishes it and re-zeroes
+                    const int old = atomicAdd(m.stop_acc, (1 << 16) + na);
+                    if ((old >> 16) != (int)gridDim.y - 1) return;
+                    na += old & 0xffff;
+                    (void)atomicExch(m.stop_acc, 0);
+                }
                 *reinterpret_cast<int2*>(m.state_next) = make_int2(step + 1, na);
             }
         }
@@ -333,12 +408,12 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         // h' = (h - n) z + n; optional residual dout = h' + res
         float* out = a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0);
         const int e = threadIdx.x;
-        if (e < a.B * 4) {
-            const int b = e >> 2, u = e & 3;
+        if (e < Bh * 4) {
+            const int bl = e >> 2, u = e & 3, b = m0 + bl;
             const int unit = ntile * 4 + u;
-            const float r = sigmoidf_(fin[b][u] + pre_bias[0]);
-            const float z = sigmoidf_(fin[b][4 + u] + pre_bias[1]);
-            const float n = tanhf((fin[b][8 + u] + pre_bias[2]) + r * (fin[b][12 + u] + pre_bias[3]));
+            const float r = sigmoidf_(fin[bl][u] + pre_bias[0]);
+            const float z = sigmoidf_(fin[bl][4 + u] + pre_bias[1]);
+            const float n = tanhf((fin[bl][8 + u] + pre_bias[2]) + r * (fin[bl][12 + u] + pre_bias[3]));
             const float h = (pre_cell - n) * z + n;
             out[(int64_t)b * a.ldo + unit] = h;
             if (a.gru.dout) a.gru.dout[(int64_t)b * a.gru.ldd + unit] = h + pre_res;
@@ -347,13 +422,13 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         // LSTM cell (torch LSTMCell, gate order i, f, g, o): c' = s(f)c + s(i)tanh(g); h' = s(o)tanh(c')
         float* out = a.out + (a.out_par >= 0 ? (int64_t)((step + a.out_par) & 1) * a.out_pstride : 0);
         const int e = threadIdx.x;  // blockDim >= 256 >= B*4 for the LSTM shapes (K >= 1792)
-        if (e < a.B * 4) {
-            const int b = e >> 2, u = e & 3;
+        if (e < Bh * 4) {
+            const int bl = e >> 2, u = e & 3, b = m0 + bl;
             const int unit = ntile * 4 + u;
-            const float gi = fin[b][u] + pre_bias[0];
-            const float gf = fin[b][4 + u] + pre_bias[1];
-            const float gg = fin[b][8 + u] + pre_bias[2];
-            const float go = fin[b][12 + u] + pre_bias[3];
+            const float gi = fin[bl][u] + pre_bias[0];
+            const float gf = fin[bl][4 + u] + pre_bias[1];
+            const float gg = fin[bl][8 + u] + pre_bias[2];
+            const float go = fin[bl][12 + u] + pre_bias[3];
             const float c2 = sigmoidf_(gf) * pre_cell + sigmoidf_(gi) * tanhf(gg);
             a.cell[(int64_t)b * a.ldc + unit] = c2;
             out[(int64_t)b * a.ldo + unit] = sigmoidf_(go) * tanhf(c2);
@@ -430,16 +505,32 @@ hipError_t sgemm_pack_bias(const float* a, const float* b, int N, int rowmap, in
     return hipGetLastError();
 }
 
+// Narrow GEMMs (fewer n-tiles than this) split the batch into row groups of 16, one workgroup
+// per (n-tile, row group): at B = 64 the fused mel launch has 22 n-tiles, and 22 workgroups
+// carrying four m-tiles each leave 234 CUs idle while they run 4x the MFMAs.  Wide GEMMs keep
+// every m-tile in one workgroup, which then reads each weight fragment once for the whole batch.
+// TTS_SGEMM_SPLIT overrides the n-tile threshold (0: never split).
+static int split_below() {
+    static const int v = [] {
+        const char* e = std::getenv("TTS_SGEMM_SPLIT");
+        return e && e[0] ? std::atoi(e) : 128;
+    }();
+    return v;
+}
+
 template <int EPI, int ROLE>
 static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
     // always 16 waves (waves past K's chunk count contribute zeros): the epilogues give every
     // (row, column) of the tile its own thread, B * 16 <= 1024
-    const dim3 grid((a.N + 15) / 16), block(MAX_WAVES * 64);
+    const int ntiles = (a.N + 15) / 16;
+    const dim3 grid(ntiles), block(MAX_WAVES * 64);
     const int mt = (a.B + 15) / 16;
     if (a.B == 1)
         hipLaunchKernelGGL((sgemm_kernel<0, EPI, ROLE>), grid, block, 0, s, a);
     else if (mt <= 1)
         hipLaunchKernelGGL((sgemm_kernel<1, EPI, ROLE>), grid, block, 0, s, a);
+    else if (ntiles < split_below())
+        hipLaunchKernelGGL((sgemm_kernel<1, EPI, ROLE>), dim3(ntiles, mt), block, 0, s, a);
     else if (mt <= 2)
         hipLaunchKernelGGL((sgemm_kernel<2, EPI, ROLE>), grid, block, 0, s, a);
     else

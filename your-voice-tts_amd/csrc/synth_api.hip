@@ -4,8 +4,11 @@
 // point the host package binds one by one (same numerics, bitwise); this call only removes the
 // host round trips between them: one H2D of the ids, the decoder's stop-step readback (the
 // sentence length is decided on the device) and the stages' own completion waits.  The stages
-// run in pipeline mode (common.h) on one stream of this handle, and the call returns once
-// Griffin-Lim is enqueued: the waveform is ready when the caller's stream reaches it.
+// run in pipeline mode (common.h) and the call returns once Griffin-Lim is enqueued: the
+// waveform is ready when the caller's stream reaches it.  Griffin-Lim runs on a second stream of
+// this handle, so call k+1's encoder + decoder (which read only host inputs and this handle's
+// buffers) overlap call k's Griffin-Lim on the device; the stage buffers Griffin-Lim reads
+// (mel_post, its compacted copy) alternate per call.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,15 +24,25 @@ struct tts_synth {
     tts_gl* g = nullptr;
     int r = 1, nmel = 80, hop = 0;
     int32_t* ids = nullptr;  // [dev] [B][Lmax]
-    float *enc = nullptr, *mel = nullptr, *stop = nullptr, *post = nullptr, *spec = nullptr;
+    float *enc = nullptr, *mel = nullptr, *stop = nullptr;
+    // Griffin-Lim inputs, one pair per call parity: call k+1's postnet writes the other pair while
+    // call k's Griffin-Lim reads this one (call k+2 comes after call k+1 collected call k's run)
+    float *post[2] = {nullptr, nullptr}, *spec[2] = {nullptr, nullptr};
     size_t ids_n = 0, enc_n = 0, mel_n = 0, stop_n = 0, spec_n = 0;
     std::vector<int32_t> steps;
-    // the whole pipeline runs on this stream (one hand-off in from the caller's, one out); the
-    // call returns once Griffin-Lim is enqueued, so the next call's host work overlaps it
-    hipStream_t stream = nullptr;
-    hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    // encoder -> decoder -> postnet on `stream` (higher priority: its launches are latency-bound
+    // and leave most CUs idle), Griffin-Lim on `gl_stream`.  Neither front stage touches caller
+    // memory, so `stream` does not wait for the caller's; Griffin-Lim waits for the caller's
+    // stream (it writes the caller's waveform buffer) and for the postnet, and the caller's stream
+    // waits for Griffin-Lim.
+    hipStream_t stream = nullptr, gl_stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_post = nullptr, ev_out = nullptr;
+    // the last Griffin-Lim was the persistent launch (its workgroups wait on each other): the next
+    // call's resident encoder / decoder launches (which do too) must not run beside it
+    bool gl_spins = false;
     // pinned host staging of ids / lens / frames, alternated per call: call k reuses call k-2's
-    // buffer, whose copies completed before call k-1's decoder synchronisation
+    // buffer, whose copies completed before call k-1's decoder synchronisation and Griffin-Lim
+    // collection
     int32_t* pin[2] = {nullptr, nullptr};
     size_t pin_n[2] = {0, 0};
     unsigned calls = 0;
@@ -78,8 +91,12 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
     s->r = r;
     s->nmel = n_mel;
     s->hop = hop;
-    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+    if (hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&s->gl_stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_post, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming) != hipSuccess) {
         tts_synth_destroy(s);
         tts::set_error("tts_synth_create: stream / event creation failed");
@@ -91,16 +108,19 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
 
 void tts_synth_destroy(tts_synth* s) {
     if (!s) return;
-    if (s->stream) (void)hipStreamSynchronize(s->stream);
+    for (hipStream_t q : {s->stream, s->gl_stream})
+        if (q) (void)hipStreamSynchronize(q);
     if (tts::gl_collect(s->g) != TTS_OK)  // the last pipelined run's status was never collected
         std::fprintf(stderr, "tts_synth_destroy: the last run failed: %s\n", tts_last_error());
-    for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post, (void*)s->spec})
+    for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post[0],
+                    (void*)s->post[1], (void*)s->spec[0], (void*)s->spec[1]})
         if (q) (void)hipFree(q);
     for (int32_t* q : s->pin)
         if (q) (void)hipHostFree(q);
-    for (hipEvent_t ev : {s->ev_in, s->ev_out})
+    for (hipEvent_t ev : {s->ev_in, s->ev_post, s->ev_out})
         if (ev) (void)hipEventDestroy(ev);
-    if (s->stream) (void)hipStreamDestroy(s->stream);
+    for (hipStream_t q : {s->stream, s->gl_stream})
+        if (q) (void)hipStreamDestroy(q);
     delete s;
 }
 
@@ -108,7 +128,6 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
                          int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames, void* stream) {
     TTS_CHECK(s && ids && lens && wav && frames && B >= 1 && Lmax >= 2 && max_steps >= 1 && gl_iters >= 0,
               TTS_ERR_INVALID, "bad synth arguments");
-    hipStream_t cs = static_cast<hipStream_t>(stream);
     hipStream_t ss = s->stream;
     const int cap = max_steps + 21;  // decoder steps_cap (>= max_steps + 20)
     const size_t T = (size_t)cap * s->r;
@@ -118,18 +137,26 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
                         (size_t)B * T * s->nmel > s->mel_n || (size_t)B * cap > s->stop_n;
     const int par = s->calls & 1;
     const size_t pin_need = (size_t)B * Lmax + 2 * (size_t)B;
-    if (regrow || pin_need > s->pin_n[par]) TTS_HIP(hipStreamSynchronize(ss));
+    if (regrow || pin_need > s->pin_n[par]) {
+        TTS_HIP(hipStreamSynchronize(ss));
+        TTS_HIP(hipStreamSynchronize(s->gl_stream));
+    }
     if ((st = grow(&s->ids, s->ids_n, (size_t)B * Lmax))) return st;
     if ((st = grow(&s->enc, s->enc_n, (size_t)B * Lmax * 512))) return st;
     if ((st = grow(&s->mel, s->mel_n, (size_t)B * T * s->nmel))) return st;
     if ((st = grow(&s->stop, s->stop_n, (size_t)B * cap))) return st;
-    if (!s->post || s->spec_n < s->mel_n) {
-        // mel_post and the compacted GL input share the mel buffer's capacity
-        if (s->post) TTS_HIP(hipFree(s->post));
-        if (s->spec) TTS_HIP(hipFree(s->spec));
-        s->post = s->spec = nullptr;
-        TTS_HIP(hipMalloc(&s->post, s->mel_n * sizeof(float)));
-        TTS_HIP(hipMalloc(&s->spec, s->mel_n * sizeof(float)));
+    if (!s->post[0] || s->spec_n < s->mel_n) {
+        // mel_post and the compacted GL input share the mel buffer's capacity (mel_n only grows
+        // on a regrow, which drained both streams above)
+        for (int k = 0; k < 2; ++k) {
+            if (s->post[k]) TTS_HIP(hipFree(s->post[k]));
+            if (s->spec[k]) TTS_HIP(hipFree(s->spec[k]));
+            s->post[k] = s->spec[k] = nullptr;
+        }
+        for (int k = 0; k < 2; ++k) {
+            TTS_HIP(hipMalloc(&s->post[k], s->mel_n * sizeof(float)));
+            TTS_HIP(hipMalloc(&s->spec[k], s->mel_n * sizeof(float)));
+        }
         s->spec_n = s->mel_n;
     }
     if (pin_need > s->pin_n[par]) {
@@ -148,15 +175,17 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
     st = synth_stages(s, h_ids, h_lens, h_frames, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
     if (st) {
         (void)hipStreamSynchronize(s->stream);
+        (void)hipStreamSynchronize(s->gl_stream);
         return st;
     }
-    ++s->calls;  // only now: a failed call leaves the parity (and its drained buffer) to the next
+    ++s->calls;  // only now: a failed call leaves the parity (and its drained buffers) to the next
     return TTS_OK;
 }
 
 tts_status tts_synth_sync(tts_synth* s) {
     TTS_CHECK(s, TTS_ERR_INVALID, "null handle");
     TTS_HIP(hipStreamSynchronize(s->stream));
+    TTS_HIP(hipStreamSynchronize(s->gl_stream));
     return tts::gl_collect(s->g);
 }
 
@@ -171,9 +200,11 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     const int cap = max_steps + 21;
     const size_t T = (size_t)cap * s->r;
     tts_status st;
+    const int par = s->calls & 1;
     PipelineScope scope(s);
-    TTS_HIP(hipEventRecord(s->ev_in, cs));
-    TTS_HIP(hipStreamWaitEvent(ss, s->ev_in, 0));
+    // the front stages do not wait for the caller's stream (they read host inputs and write this
+    // handle's buffers only), nor for the previous call's Griffin-Lim unless that one spins
+    if (s->gl_spins) TTS_HIP(hipStreamWaitEvent(ss, s->ev_out, 0));
     TTS_HIP(hipMemcpyAsync(s->ids, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
     s->steps.assign(B, 0);
     for (int attempt = 0;; ++attempt) {
@@ -195,17 +226,27 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_CHECK(Fmax >= 2, TTS_ERR_INVALID, "a sentence decoded to fewer than 2 frames");
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
     std::copy(h_frames, h_frames + B, frames);
-    if ((st = tts_postnet_run(s->p, s->mel, h_frames, B, (int)T, s->post, ss))) return st;
-    const float* spec = s->post;
-    if (B > 1) {  // GL input is [B][Fmax][nmel]: compact the rows of each sentence; shorter
-                  // sentences leave their waveform tail unwritten: zero it
+    float* const post = s->post[par];
+    if ((st = tts_postnet_run(s->p, s->mel, h_frames, B, (int)T, post, ss))) return st;
+    const float* spec = post;
+    if (B > 1) {  // GL input is [B][Fmax][nmel]: compact the rows of each sentence
         const size_t row = (size_t)s->nmel * sizeof(float);
-        TTS_HIP(hipMemcpy2DAsync(s->spec, Fmax * row, s->post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, ss));
-        spec = s->spec;
-        TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), ss));
+        TTS_HIP(hipMemcpy2DAsync(s->spec[par], Fmax * row, post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, ss));
+        spec = s->spec[par];
     }
-    if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, ss))) return st;
-    TTS_HIP(hipEventRecord(s->ev_out, ss));
+    hipStream_t gs = s->gl_stream;
+    TTS_HIP(hipEventRecord(s->ev_post, ss));
+    TTS_HIP(hipEventRecord(s->ev_in, cs));
+    TTS_HIP(hipStreamWaitEvent(gs, s->ev_post, 0));
+    TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
+    // shorter sentences leave their waveform tail unwritten: zero it
+    if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
+    s->gl_spins = false;
+    if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, gs))) return st;
+    int path = 0;
+    if ((st = tts_gl_last_path(s->g, &path))) return st;
+    s->gl_spins = path == TTS_GL_PATH_PERSISTENT;
+    TTS_HIP(hipEventRecord(s->ev_out, gs));
     TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
     return TTS_OK;
 }

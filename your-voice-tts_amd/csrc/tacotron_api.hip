@@ -545,6 +545,7 @@ tts_status enqueue_step(tts_tacotron* t, int B, int Lmax, int max_steps, int p, 
         m.lens = t->lens; m.tail = t->tail; m.flag1 = t->flag1; m.count = t->count;
         m.done = t->done; m.n_steps = t->n_steps;
         m.state_next = t->state + 2 * q;
+        m.stop_acc = t->state + 4;
         m.max_steps = max_steps;
         m.rule = 1;
         MARK();
@@ -799,7 +800,7 @@ tts_status create_workspace(tts_tacotron* t, hipStream_t s) {
     CK(talloc(t, &t->count, Bc));
     CK(talloc(t, &t->done, Bc));
     CK(talloc(t, &t->n_steps, Bc));
-    CK(talloc(t, &t->state, 4));
+    CK(talloc(t, &t->state, 8));  // {step, n_active} x 2 parities, stop_acc
     CK(talloc(t, &t->mel_hist, (size_t)Bc * t->hist_cap * t->nmel));
     CK(talloc(t, &t->stop_hist, (size_t)Bc * t->hist_cap));
     CK(talloc(t, &t->align_hist, (size_t)Bc * t->hist_cap * Lc));
@@ -813,7 +814,7 @@ tts_status create_workspace(tts_tacotron* t, hipStream_t s) {
     TTS_HIP(hipMemsetAsync(t->d2, 0, sizeof(float) * Bc * T_DEC, s));
     TTS_HIP(hipMemsetAsync(t->denc, 0, sizeof(float) * Bc * Lc * T_DEC, s));
     TTS_HIP(hipMemsetAsync(t->Pt, 0, sizeof(float) * Bc * ADIM * Lc, s));
-    TTS_HIP(hipMemsetAsync(t->state, 0, sizeof(int) * 4, s));
+    TTS_HIP(hipMemsetAsync(t->state, 0, sizeof(int) * 8, s));
     return TTS_OK;
 }
 
