@@ -110,10 +110,18 @@ __device__ double2* fft1024(double2* src, double2* dst, const FftTw& tw) {
     return src;
 }
 
+// LDS slot of complex point i in the fft1024_regs buffers: rows of 16 points (256 B, all 64
+// banks) with the 16-byte columns XOR-swizzled by 5 * (row mod 4).  The Ns = 1 pass stores lane
+// j's points at 4j + r (16 lanes span 4 rows, columns {0, 4, 8, 12}) and the Ns = 4 pass at
+// 16 (j/4) + j%4 + 4r (4 rows, columns {0..3}): both land on 16 distinct columns instead of
+// 4-way bank conflicts; contiguous reads stay a permutation of one row.
+__device__ __forceinline__ int swz(int i) { return i ^ (5 * ((i >> 4) & 3)); }
+
 // fft1024 with register edges: thread j enters with z[j + 256 r] (r = 0..3) in v -- the operands of
 // its first radix-4 butterfly (Ns = 1, untwiddled) -- so the first pass reads no LDS; with TO_REGS
 // the last pass (Ns = 256, whose outputs of thread j are z[j + 256 r] again) leaves its results in v
 // instead of LDS (returns null).  Same operations in the same order as fft1024: bitwise equal.
+// The buffers hold point i at swz(i).
 // Pass 0 writes `dst`; the caller's previous readers of both buffers must have passed a barrier.
 template <bool INV, bool TO_REGS>
 __device__ double2* fft1024_regs(double2 (&v)[4], double2* src, double2* dst, const FftTw& tw) {
@@ -123,7 +131,7 @@ __device__ double2* fft1024_regs(double2 (&v)[4], double2* src, double2* dst, co
         const int k = j & (Ns - 1);
         if (Ns > 1) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = src[j + r * 256];
+            for (int r = 0; r < 4; ++r) v[r] = src[swz(j + r * 256)];
 #pragma unroll
             for (int r = 1; r < 4; ++r) {
                 double2 w = tw.w[p][r - 1];
@@ -143,7 +151,57 @@ __device__ double2* fft1024_regs(double2 (&v)[4], double2* src, double2* dst, co
         if (TO_REGS && Ns == NH / 4) return nullptr;  // idxD = j: v[r] is z[j + 256 r]
         const int idxD = (j / Ns) * Ns * 4 + k;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[idxD + r * Ns] = v[r];
+        for (int r = 0; r < 4; ++r) dst[swz(idxD + r * Ns)] = v[r];
+        __syncthreads();
+        double2* t = src;
+        src = dst;
+        dst = t;
+    }
+    return src;
+}
+
+// fft1024_regs with the twiddles read from the global table pass by pass (each pass's three
+// issued one pass ahead, so only the first waits on memory) instead of living in 48 VGPRs for the
+// whole kernel: the occupancy form of gl_iter_kernel.  Same values, same operations: bitwise
+// equal to fft1024_regs.
+template <bool INV, bool TO_REGS>
+__device__ double2* fft1024_regs_gtw(double2 (&v)[4], double2* src, double2* dst, const double2* __restrict__ tw) {
+    const int j = threadIdx.x;
+    double2 w[3];
+#pragma unroll
+    for (int r = 1; r < 4; ++r) w[r - 1] = tw[(j & 3) * r * 128];  // Ns = 4: 512 / Ns = 128
+#pragma unroll
+    for (int Ns = 1; Ns < NH; Ns *= 4) {
+        const int k = j & (Ns - 1);
+        if (Ns > 1) {
+            double2 wn[3];
+            if (Ns < NH / 4) {  // next pass's twiddles (Ns' = 4 Ns, stride 512 / Ns')
+                const int k2 = j & (4 * Ns - 1);
+#pragma unroll
+                for (int r = 1; r < 4; ++r) wn[r - 1] = tw[k2 * r * (128 / Ns)];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = src[swz(j + r * 256)];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) v[r] = cmul(v[r], INV ? cconj(w[r - 1]) : w[r - 1]);
+            if (Ns < NH / 4) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) w[r] = wn[r];
+            }
+        }
+        const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
+        const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
+        const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
+        const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
+        const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
+        v[0] = double2{a0.x + a2.x, a0.y + a2.y};
+        v[1] = double2{a1.x + m3.x, a1.y + m3.y};
+        v[2] = double2{a0.x - a2.x, a0.y - a2.y};
+        v[3] = double2{a1.x - m3.x, a1.y - m3.y};
+        if (TO_REGS && Ns == NH / 4) return nullptr;
+        const int idxD = (j / Ns) * Ns * 4 + k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[swz(idxD + r * Ns)] = v[r];
         __syncthreads();
         double2* t = src;
         src = dst;
@@ -165,6 +223,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 
 // np.pad(..., mode='reflect') index map for a signal of length N (any overhang).
 __device__ __forceinline__ int reflect_idx(int p, int N) {
+    if ((unsigned)p < (unsigned)N) return p;  // interior: no division
     if (N == 1) return 0;
     const int period = 2 * (N - 1);
     int pp = p % period;
@@ -345,7 +404,9 @@ __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned
 // previous iteration's frames inside this launch (bitwise the values gl_ola_kernel would store),
 // so an iteration is one launch instead of two.
 template <bool INIT, bool FUSED = false>
-__global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
+// Four workgroups per CU (32 KB of LDS, <= 128 VGPRs each).  Measured at B = 64: the same speed
+// as three workgroups with the FFT twiddles held in registers, faster than five (which spill).
+__global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a) {
     const int b = blockIdx.y;
     const int f = xcd_remap(blockIdx.x, gridDim.x);
     const int Fb = a.F[b];
@@ -358,22 +419,27 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     }
     __shared__ __align__(16) double2 buf0[NH];
     __shared__ __align__(16) double2 buf1[NH];
-    __shared__ __align__(16) double2 X[NB + 1];
+    // the spectrum X[0, 1024) reuses buf0 (free once the forward FFT's last pass has read it; the
+    // inverse FFT writes it again only after every thread has read X), and the Nyquist bin
+    // X[1024] stays in a register of thread 0, the thread that writes and reads it: 32 KB of LDS
+    double2* const X = buf0;
+    double2 xnyq = double2{0.0, 0.0};
     const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
-    // ---- phase 0: every global operand of the frame is issued before anything waits (one memory
-    // round trip per frame instead of one per FFT pass): twiddles, window, |S|, the input samples
+    // ---- phase 0: the frame's global operands are issued before anything waits: window, |S|,
+    // split twiddles, the input samples (the FFT twiddles follow pass by pass, fft1024_regs_gtw)
     constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;   // bins per thread (5)
     constexpr int PN = NFFT / GL_THREADS;                    // samples per thread (8)
-    const FftTw ftw = load_fft_tw(a.c.tw);
-    double2 tk[PK];
+    // |S| (streamed from HBM) is issued here; the split twiddles (an L2-resident table) are read
+    // where they are used: holding them across the forward FFT would cost a wave per SIMD
     double sk[PK];
 #pragma unroll
     for (int i = 0; i < PK; ++i) {
         const int k = tid + i * GL_THREADS;
-        tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
         sk[i] = k < NB ? Sf[k] : 0.0;
     }
-    // synthesis window at this thread's output samples (the register edge of the inverse FFT)
+    // the padded Hann at this thread's samples: the analysis window of the STFT input (the first
+    // butterfly's register operands) and the synthesis window of the iSTFT output (the last
+    // butterfly's) sit at the same sample indices
     double wo[PN];
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
@@ -385,13 +451,11 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         // ---- STFT frame f of the previous iteration's float32 signal (librosa stft, centre reflect pad)
         const int N = g.hop * (Fb - 1);
         const float* yb = a.y + (int64_t)b * a.Nmax;
-        double wi[PN];
         float yi[PN];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             const int n = edge_sample(tid, i);  // the first butterfly's operands stay in registers
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
-            wi[i] = sup ? a.c.win[n] : 0.0;
             if (FUSED) {
                 const double* fb = a.prev + (int64_t)b * a.Fmax * g.winp;
                 yi[i] = sup ? ola_sample_unrolled(fb, reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2, Fb, g, a.c.win2)
@@ -402,19 +466,19 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
         }
         double2 v[4];  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = double2{wi[2 * r] * (double)yi[2 * r], wi[2 * r + 1] * (double)yi[2 * r + 1]};
-        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
+        for (int r = 0; r < 4; ++r) v[r] = double2{wo[2 * r] * (double)yi[2 * r], wo[2 * r + 1] * (double)yi[2 * r + 1]};
+        const double2* Z = fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw);
         // real-FFT split; the STFT value is stored complex64 (librosa stft dtype) and its phase
         // exp(i angle(X)) (angle(0) = 0) is applied to |S| in float64 (utils/audio.py:187-188)
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
             const int k = tid + i * GL_THREADS;
             if (k >= NB) break;
-            const double2 zk = Z[k & (NH - 1)];
-            const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
+            const double2 zk = Z[swz(k & (NH - 1))];
+            const double2 zc = cconj(Z[swz((NH - k) & (NH - 1))]);
             const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
             const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};  // -i (zk - zc) / 2
-            const double2 t = tk[i];
+            const double2 t = a.c.tw[k];
             const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
             const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
             // unit phase X / |X| by one reciprocal square root (the float-rounded components
@@ -424,7 +488,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
             const double s = sk[i];
             double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
             if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
-            X[k] = xv;
+            if (k == NH) xnyq = xv;
+            else X[k] = xv;
         }
     } else {
         // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183)
@@ -436,7 +501,10 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
             sincos(2.0 * M_PI * u, &sn, &cs);
-            X[k] = double2{sk[i] * cs, (k == 0 || k == NB - 1) ? 0.0 : sk[i] * sn};
+            const double sv = sk[i];
+            const double2 xv = double2{sv * cs, (k == 0 || k == NB - 1) ? 0.0 : sv * sn};
+            if (k == NH) xnyq = xv;
+            else X[k] = xv;
         }
     }
     __syncthreads();
@@ -447,13 +515,13 @@ __global__ __launch_bounds__(GL_THREADS) void gl_iter_kernel(const IterArgs a) {
     for (int i = 0; i < NH / GL_THREADS; ++i) {
         const int k = tid + i * GL_THREADS;
         const double2 xk = X[k];
-        const double2 xc = cconj(X[NH - k]);
+        const double2 xc = cconj(k == 0 ? xnyq : X[NH - k]);
         const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
         const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
-        const double2 O = cmul(D, cconj(tk[i]));
+        const double2 O = cmul(D, cconj(a.c.tw[k]));
         v[i] = double2{E.x - O.y, E.y + O.x};  // E + i O
     }
-    fft1024_regs<true, true>(v, buf0, buf1, ftw);
+    fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
     // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft), from
     // the last butterfly's registers
     double* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
@@ -641,8 +709,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         for (int i = 0; i < PK; ++i) {
             const int k = tid + i * GL_THREADS;
             if (k >= NB) break;
-            const double2 zk = Z[k & (NH - 1)];
-            const double2 zc = cconj(Z[(NH - k) & (NH - 1)]);
+            const double2 zk = Z[swz(k & (NH - 1))];
+            const double2 zc = cconj(Z[swz((NH - k) & (NH - 1))]);
             const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
             const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};
             const double2 t = tk[i];
@@ -1095,7 +1163,9 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     // 256 frames in all: the whole loop as one persistent launch (one workgroup per frame), whose
     // iterations write slots of their own: a frame slot is never rewritten inside the launch, so no
     // XCD's L2 can hold an earlier copy of the bytes an iteration reads
-    const bool fused = (int64_t)B * Fmax <= 1024 && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
+    // (TTS_GL_FUSED=1 forces the fused form at any batch: measurement knob)
+    const char* fz = getenv("TTS_GL_FUSED");
+    const bool fused = ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
     int frames_total = 0;
     for (int b = 0; b < B; ++b) frames_total += F[b];
     const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
