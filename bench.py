@@ -42,6 +42,10 @@ sharding = importlib.import_module("your-voice-tts_amd.sharding")
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA peak (same table)
+FP64_VECTOR_PEAK_TF = 78.6  # fp64 vector FMA peak (same table)
+# one GL frame-iteration: forward + inverse 1024-point complex FFT (5 N log2 N each) plus the
+# real-FFT split / merge and the phase projection (~20 flops per bin each way)
+GL_FLOPS_PER_FRAME_ITER = 2 * 5 * 1024 * 10 + 2 * 20 * 1025
 POSTNET_FLOP_PER_FRAME = 2 * 5 * (80 * 512 + 3 * 512 * 512 + 512 * 80)
 GL_BYTES_PER_FRAME_ITER = 4 * 1025 + 2 * 4 * 275                        # 6300 B
 
@@ -491,6 +495,16 @@ def main():
                         algorithmic_bytes_per_launch=kdom["algorithmic_bytes"], mean_launch_ms=kdom["mean_ms"])
         if traffic:
             roofline["traffic_over_algorithmic"] = traffic / kdom["algorithmic_bytes"]
+        if dom in ("gl_iter", "gl_persistent"):
+            # the fp64 STFT/iSTFT of every frame: the SURVEY 8(d) byte count prices the |S| read and
+            # the float32 signal, but the kernel's time goes to fp64 FFT passes through LDS
+            flops = GL_FLOPS_PER_FRAME_ITER * frames_total * (1 if dom == "gl_iter" else args.iters)
+            tf = flops / (kdom["mean_ms"] * 1e-3) / 1e12
+            roofline["diagnostics"] = dict(
+                limiter="fp64 VALU issue + LDS passes of the per-frame Stockham FFTs (workgroup barriers); "
+                        "HBM traffic is the fp64 |S| row and the fp64 windowed frames written and overlap-added",
+                fp64_flops_per_launch=flops, fp64_tflops=tf, fp64_vector_frac=tf / FP64_VECTOR_PEAK_TF,
+                traffic_gbs=(traffic / (kdom["mean_ms"] * 1e-3) / 1e9) if traffic else None)
         if dom == "resident_decoder":
             # the SURVEY 8(d) HBM figure prices a weight stream the resident kernel never does (its
             # weights stay in VGPRs / LDS): state what actually bounds it

@@ -1,6 +1,6 @@
 """Persistent kernels (resident decoder, resident encoder BiLSTM, persistent Griffin-Lim) hand data
 between workgroups inside one launch, so they are only launched when every workgroup can be
-resident at once (csrc/runtime.hip: launch_persistent — occupancy check + cooperative launch).
+resident at once (csrc/runtime.hip: launch_persistent — occupancy check, then a plain launch; TTS_COOP=1 for a cooperative one).
 TTS_CU_CAP pretends the device has fewer CUs: the grids then cannot be co-resident, nothing
 persistent is launched, and each stage must take its multi-launch fallback with unchanged results.
 A persistent Griffin-Lim whose hand-off wait times out (fault injection) must raise and must not

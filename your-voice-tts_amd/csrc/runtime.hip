@@ -1,7 +1,10 @@
 // Error reporting shared by every entry point of libtts_hip.
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "common.h"
 
@@ -30,23 +33,51 @@ int usable_cus() {
     return ncu;
 }
 
+// Co-residency of a persistent grid: the occupancy of `fn` at this block size (queried once per
+// kernel and cached: the query costs tens of microseconds) times the usable CUs must cover the
+// grid, else the caller falls back.  The launch itself is a plain one by default; the kernels'
+// waits are bounded and report a grid that still failed to become resident (another process
+// holding CUs), which the callers turn into their fallback or an error.  TTS_COOP=1 launches with
+// hipLaunchCooperativeKernel instead (the runtime's own guarantee; measured ~30 us per launch on
+// this ROCm, ~2.5% of a configs[1] sentence over its three persistent launches).
 hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args, size_t smem, hipStream_t s,
                              bool* launched) {
     *launched = false;
     const long long blocks = (long long)grid.x * grid.y * grid.z;
-    int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)(block.x * block.y * block.z), smem);
-    if (e != hipSuccess) return e;
-    if ((long long)per_cu * usable_cus() < blocks) return hipSuccess;  // cannot be co-resident: fall back
-    const char* coop = std::getenv("TTS_COOP");
-    if (coop && coop[0] == '0') {
-        e = hipLaunchKernel(fn, grid, block, args, smem, s);
-    } else {
+    const int threads = (int)(block.x * block.y * block.z);
+    struct Key {
+        const void* fn;
+        int threads;
+        size_t smem;
+    };
+    static std::mutex mu;
+    static std::vector<std::pair<Key, int>> cache;
+    static const bool coop = [] {
+        const char* c = std::getenv("TTS_COOP");
+        return c && c[0] == '1';
+    }();
+    int per_cu = -1;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const auto& kv : cache)
+            if (kv.first.fn == fn && kv.first.threads == threads && kv.first.smem == smem) per_cu = kv.second;
+        if (per_cu < 0) {
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, smem);
+            if (e != hipSuccess) return e;
+            cache.push_back({Key{fn, threads, smem}, per_cu});
+        }
+    }
+    // cannot be co-resident: fall back (TTS_CU_CAP is read per call: tests set it)
+    if ((long long)per_cu * usable_cus() < blocks) return hipSuccess;
+    hipError_t e;
+    if (coop) {
         e = hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)smem, s);
         if (e == hipErrorCooperativeLaunchTooLarge) {
             (void)hipGetLastError();  // refused before anything ran: fall back
             return hipSuccess;
         }
+    } else {
+        e = hipLaunchKernel(fn, grid, block, args, smem, s);
     }
     if (e == hipSuccess) *launched = true;
     return e;
