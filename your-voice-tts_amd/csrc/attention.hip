@@ -418,7 +418,10 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             for (int p = 1; p < PARTS; ++p) ctx += red[p * ENC_ + tid];
         }
     }
-    if (tid < ENC_) a.ctx[(int64_t)b * a.ctx_ld + tid] = ctx;
+    if (tid < ENC_) {
+        a.ctx[(int64_t)b * a.ctx_ld + tid] = ctx;
+        if (a.ctxf) a.ctxf[frag_idx(b, a.ctxf_k0 + tid, a.ntf)] = ctx;
+    }
     if (a.forward_attn && a.trans_agent) {
         // u = sigmoid(ta([context, query]))  (:220-222)
         const float* h = a.h_att + (int64_t)b * HATT_;
@@ -539,6 +542,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_fm_kernel(const AttnArg
             if (clo + k <= chi) ctx += weight(clo + k) * (clo + k == cx ? ex : erow[k]);
         if (cx > chi) ctx += weight(cx) * ex;
         a.ctx[(int64_t)b * XA + tid] = ctx;
+        if (a.ctxf) a.ctxf[frag_idx(b, a.ctxf_k0 + tid, a.ntf)] = ctx;
     }
 }
 

@@ -54,6 +54,14 @@ constexpr int WAVE = 64;
 
 // v_mfma_f32_16x16x4_f32: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];
 // D lane l holds C[(l>>4)*4 + r][l&15], r = 0..3.  Exact f32 fma chain.
+// Fragment-order mirror of an activation matrix [rows][K] (rows padded to nt m-tiles of 16, K a
+// multiple of 16): element (b, k) sits where lane (b & 15) + 16 ((k & 15) >> 2), component k & 3
+// of the v_mfma_f32_16x16x4_f32 A-operand float4 of (chunk k >> 4, m-tile b >> 4) loads it, so a
+// wave's operand load is one contiguous 1 KiB instead of 16 rows x 64 B (sgemm.h).
+__device__ __forceinline__ int64_t frag_idx(int b, int k, int nt) {
+    return ((((int64_t)(k >> 4) * nt + (b >> 4)) * 64 + (b & 15) + 16 * ((k & 15) >> 2)) << 2) + (k & 3);
+}
+
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }

@@ -47,6 +47,8 @@ struct AttnArgs {
     float* tail;           // [B] att_w[L-2] + att_w[L-1]
     // outputs
     float* ctx;            // [B] rows of stride ctx_ld: context written to ctx[b*ctx_ld + d]
+    float* ctxf;           // fragment mirror (frag_idx(b, ctxf_k0 + d, ntf)) or null
+    int ctxf_k0, ntf;
     float* align_hist;     // [B][hist_cap][Lalign] or null
     int64_t align_ldb;     // stride per sentence
     int Lalign;

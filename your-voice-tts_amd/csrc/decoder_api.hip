@@ -50,6 +50,11 @@ struct tts_decoder {
     int Lcap = 0, Bcap = 0, hist_cap = 0;
     float *enc = nullptr, *Pt = nullptr, *h_att = nullptr, *c_att = nullptr, *h_dec = nullptr, *c_dec = nullptr;
     float *xa = nullptr, *mem = nullptr, *pre1 = nullptr, *q = nullptr, *epart = nullptr;
+    // fragment-order mirrors (common.h: frag_idx, ntf m-tiles) of the GEMM inputs for batches
+    // above 16: written beside the row-major buffers by their producers, read by the 4-wave
+    // batched GEMM (sgemm.h: Seg::pf).  Null when max_batch <= 16.
+    int ntf = 0;
+    float *xaf = nullptr, *hattf = nullptr, *hdecf = nullptr, *pre1f = nullptr;
     bool fast_attention = false;  // attention_uses_epart(): energies evaluated in the query launch
     // resident (persistent, one launch per sentence) batch-1 decoder, resident.h
     bool resident = false;
@@ -105,6 +110,41 @@ tts_status copy_weight(tts_decoder* d, float** dst, const float* src, size_t n, 
     return TTS_OK;
 }
 
+// The batched GEMMs read fragment mirrors above 16 sentences (TTS_FRAG=0: row-major always).
+bool frag_on(const tts_decoder* d, int B) {
+    static const bool off = [] {
+        const char* e = std::getenv("TTS_FRAG");
+        return e && e[0] == '0';
+    }();
+    return d->xaf && B > 16 && !off;
+}
+
+__global__ void frag_mirror_kernel(const float* src, int64_t ld, int B, int K, float* dst, int ntf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * K) return;
+    const int b = i / K, k = i % K;
+    dst[frag_idx(b, k, ntf)] = src[(int64_t)b * ld + k];
+}
+
+// Mirrors of the state a run starts from (after launch_decoder_init): both parities of xa, h_att
+// and h_dec (pre1 is mirrored by the prenet launch that writes it).
+tts_status enqueue_frag_sync(tts_decoder* d, int B, hipStream_t s) {
+    const int64_t hps = (int64_t)d->Bcap * HATT, xps = (int64_t)d->Bcap * XA;
+    const int64_t fh = (int64_t)d->ntf * 16 * HATT, fx = (int64_t)d->ntf * 16 * XA;
+    for (int p = 0; p < 2; ++p) {
+        struct { const float* src; int64_t ld; int K; float* dst; } jobs[3] = {
+            {d->xa + p * xps, XA, XA, d->xaf + p * fx},
+            {d->h_att + p * hps, HATT, HATT, d->hattf + p * fh},
+            {d->h_dec + p * hps, HDEC, HDEC, d->hdecf + p * fh}};
+        for (auto& j : jobs) {
+            const int n = B * j.K;
+            hipLaunchKernelGGL(frag_mirror_kernel, dim3((n + 255) / 256), dim3(256), 0, s, j.src, j.ld, B, j.K, j.dst, d->ntf);
+            TTS_HIP(hipGetLastError());
+        }
+    }
+    return TTS_OK;
+}
+
 // Launches of one decoder step of parity p (0: even step, 1: odd step).  `ev` (optional, 7
 // events) brackets every launch for tts_decoder_profile.
 tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, hipStream_t s,
@@ -123,29 +163,42 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     float* xa_cur = d->xa + p * xps;   // [prenet_t | ctx_{t-1}]
     float* ctx_cur = d->xa + q * xps + PRE;  // ctx_t (row stride XA)
     int* st_cur = d->state + 2 * p;
+    // fragment mirrors of the same buffers (batches above 16)
+    const bool fr = frag_on(d, B);
+    const int64_t fh = (int64_t)d->ntf * 16 * HATT, fx = (int64_t)d->ntf * 16 * XA;
+    const int64_t fchunk = (int64_t)d->ntf * 256;  // floats per 16-column chunk of a mirror
+    float* hattf_cur = fr ? d->hattf + p * fh : nullptr;
+    float* hattf_prev = fr ? d->hattf + q * fh : nullptr;
+    float* hdecf_cur = fr ? d->hdecf + p * fh : nullptr;
+    float* hdecf_prev = fr ? d->hdecf + q * fh : nullptr;
+    float* xaf_cur = fr ? d->xaf + p * fx : nullptr;
+    float* ctxf_cur = fr ? d->xaf + q * fx + (PRE / 16) * fchunk : nullptr;  // ctx_t: xa columns PRE..
     SGemmArgs g{};
     g.B = B;
     g.step = st_cur;
     g.done = d->done;
     g.out_par = -1;
+    g.ntf = d->ntf;
     // 1) prenet layer 2 -> xa_cur[b][0:256]   (common_layers.py:77-83; dropout off in eval)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{d->pre1, PRE, PRE};
+        a.seg[0] = Seg{d->pre1, PRE, PRE, fr ? d->pre1f : nullptr};
         a.nseg = 1;
         a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
         a.out = xa_cur; a.ldo = XA;
+        a.outf = xaf_cur; a.outf_k0 = 0;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     }
     // 2) attention LSTM: x = [prenet_t | ctx_{t-1}], h = h_att_{t-1}   (tacotron2.py:195-197)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{xa_cur, XA, XA};
-        a.seg[1] = Seg{h_att_prev, HATT, HATT};
+        a.seg[0] = Seg{xa_cur, XA, XA, xaf_cur};
+        a.seg[1] = Seg{h_att_prev, HATT, HATT, hattf_prev};
         a.nseg = 2;
         a.W = d->W_att; a.K = XA + HATT; a.N = 4 * HATT; a.bias = d->b_att;
         a.out = h_att_cur; a.ldo = HATT;
+        a.outf = hattf_cur; a.outf_k0 = 0;
         a.cell = d->c_att; a.ldc = HATT;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_ATT_LSTM, s));
@@ -175,6 +228,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
         a.nidx = d->nidx; a.tail = d->tail;
         a.ctx = ctx_cur;  // kernel writes ctx[b*XA + d]
+        a.ctxf = fr ? d->xaf + q * fx : nullptr; a.ctxf_k0 = PRE; a.ntf = d->ntf;
         a.align_hist = d->align_hist; a.align_ldb = (int64_t)d->hist_cap * Lmax; a.Lalign = Lmax;
         a.hist_cap = d->hist_cap;
         a.step = st_cur; a.done = d->done;
@@ -184,12 +238,13 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     // 5) decoder LSTM: x = [h_att_t | ctx_t], h = h_dec_{t-1}   (tacotron2.py:206-208)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{h_att_cur, HATT, HATT};
-        a.seg[1] = Seg{ctx_cur, XA, ENC};
-        a.seg[2] = Seg{h_dec_prev, HDEC, HDEC};
+        a.seg[0] = Seg{h_att_cur, HATT, HATT, hattf_cur};
+        a.seg[1] = Seg{ctx_cur, XA, ENC, ctxf_cur};
+        a.seg[2] = Seg{h_dec_prev, HDEC, HDEC, hdecf_prev};
         a.nseg = 3;
         a.W = d->W_dec; a.K = HATT + ENC + HDEC; a.N = 4 * HDEC; a.bias = d->b_dec;
         a.out = h_dec_cur; a.ldo = HDEC;
+        a.outf = hdecf_cur; a.outf_k0 = 0;
         a.cell = d->c_dec; a.ldc = HDEC;
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_DEC_LSTM, s));
@@ -198,13 +253,14 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     //    prenet L1 of the next step; stop = sigmoid(stopnet([h_dec; mel])) + stop rule (:219-277)
     {
         SGemmArgs a = g;
-        a.seg[0] = Seg{h_dec_cur, HDEC, HDEC};
-        a.seg[1] = Seg{ctx_cur, XA, ENC};
+        a.seg[0] = Seg{h_dec_cur, HDEC, HDEC, hdecf_cur};
+        a.seg[1] = Seg{ctx_cur, XA, ENC, ctxf_cur};
         a.nseg = 2;
         a.W = d->W_melf; a.K = HDEC + ENC; a.N = nmel + PRE + 1; a.bias = d->b_melf;
         a.hist = d->mel_hist; a.ldh = (int64_t)d->hist_cap * nmel; a.hist_cap = d->hist_cap;
         MelFused& m = a.mf;
         m.nmel = nmel; m.pre1 = d->pre1; m.ldp = PRE;
+        m.pre1f = fr ? d->pre1f : nullptr;
         m.stop_hist = d->stop_hist; m.stop_ldb = d->hist_cap;
         m.lens = d->lens; m.tail = d->tail; m.flag1 = d->flag1; m.count = d->count;
         m.done = d->done; m.n_steps = d->n_steps;
@@ -246,6 +302,7 @@ tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s, int* slot = n
     a.nseg = 1;
     a.W = d->W_pre1; a.K = d->nmel; a.N = PRE; a.act = ACT_RELU;
     a.out = d->pre1; a.ldo = PRE;
+    if (frag_on(d, B)) { a.outf = d->pre1f; a.outf_k0 = 0; a.ntf = d->ntf; }
     TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
     return TTS_OK;
 }
@@ -432,6 +489,14 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->mem, (size_t)Bc * nmel));
     CK(dmalloc(d, &d->pre1, (size_t)Bc * PRE));
     CK(dmalloc(d, &d->q, (size_t)Bc * ADIM));
+    if (Bc > 16) {
+        d->ntf = (Bc + 15) / 16;
+        const size_t rows = (size_t)d->ntf * 16;
+        CK(dmalloc(d, &d->xaf, 2 * rows * XA));
+        CK(dmalloc(d, &d->hattf, 2 * rows * HATT));
+        CK(dmalloc(d, &d->hdecf, 2 * rows * HDEC));
+        CK(dmalloc(d, &d->pre1f, rows * PRE));
+    }
     CK(dmalloc(d, &d->epart, (size_t)Bc * QE_TILES * Lc));
     CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
@@ -511,6 +576,7 @@ tts_status tts_decoder_run_teacher(tts_decoder* d, const float* enc, const int32
     ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
     ia.step = d->state; ia.n_active = d->state + 1;
     TTS_HIP(launch_decoder_init(ia, s));
+    if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
     // step t: memory = go frame (t = 0) or teacher row t-1 -> prenet layer 1 (reference weights, no
     // fold) -> the inference step with the stop rule off (its fused launch's prenet-1 output is
     // overwritten by the next step's teacher frame)
@@ -596,6 +662,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ia.keep = 1;
     }
     TTS_HIP(launch_decoder_init(ia, s));
+    if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
     if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
     int run = 0;  // steps enqueued; the next step has parity run & 1
     d->last_resident = 0;

@@ -19,6 +19,10 @@ struct Seg {
     const float* p;
     int ld;   // row stride (floats)
     int len;  // multiple of 16
+    // fragment-order mirror of the same values (common.h: frag_idx with SGemmArgs::ntf m-tiles),
+    // already offset to the segment's first chunk; when every segment has one the launch reads
+    // the mirrors (sgemm_launch: the batched 4-wave kernel)
+    const float* pf = nullptr;
 };
 
 enum Epi { EPI_LINEAR = 0, EPI_LSTM = 1, EPI_MEL_FUSED = 2, EPI_ENC_LSTM = 3, EPI_GRU = 4 };
@@ -85,6 +89,7 @@ struct MelFused {
     int* n_steps;
     int* state_next;  // int2 {t+1, n_active} read by the next step (other parity slot)
     int* stop_acc;    // zero at rest: the row groups' active counts meet here (grid.y > 1)
+    float* pre1f;     // fragment mirror of pre1 (SGemmArgs::ntf m-tiles) or null
     int max_steps;
     int rule;  // 0: Tacotron2 stop rule (layers/tacotron2.py:267-277); 1: Tacotron (layers/tacotron.py:464-469);
                // 2: teacher forcing (Decoder.forward, layers/tacotron2.py:227-247): no rule, stop logits
@@ -103,6 +108,11 @@ struct SGemmArgs {
     int ldo;
     float* out2;  // optional plain copy of the output rows
     int ldo2;
+    // optional fragment-order mirror of the output (frag_idx(b, outf_k0 + column, ntf)); ntf is
+    // also the m-tile count of the input mirrors (Seg::pf)
+    float* outf;
+    int outf_k0;
+    int ntf;
     float* hist;  // optional history: hist[b*ldh + step*N + n] for active rows, step < hist_cap
     int64_t ldh;
     int hist_cap;

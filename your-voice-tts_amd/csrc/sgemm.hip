@@ -19,12 +19,16 @@ constexpr int PRE_DIM = 256;  // prenet width (layers/tacotron2.py:108)
 __device__ const int kOneActive[2] = {0, 1};  // {step 0, 1 active} for launches without step state
 
 // Activation addressing of one lane: segments p0 | p1 | p2 of the concatenated row (wave-uniform
-// bases shifted by each segment's first k, row strides, first chunk past segments 0 and 1) and
-// the lane's rows (one per m-tile) and k offset.
+// bases shifted by each segment's first chunk, row strides, first chunk past segments 0 and 1,
+// floats per chunk) and the lane's rows (one per m-tile) and offset.  Element (m-tile mt, chunk
+// c) of the lane = p_s + c * cs + xk + row[mt] * ld_s.  Row-major activations: cs = 16, xk = the
+// lane's k offset, row = the batch row.  Fragment mirrors (Seg::pf): cs = ntf * 256, ld = 1,
+// xk = 4 * lane, row = 256 * m-tile.
 template <int NT>
 struct XAddr {
     const float *p0 = nullptr, *p1 = nullptr, *p2 = nullptr;
     int ld0 = 0, ld1 = 0, ld2 = 0, cb0 = 0, cb1 = 0;
+    int cs = 16;
     int row[NT];
     int xk = 0;
 };
@@ -47,9 +51,9 @@ __device__ __forceinline__ void sg_load(const float4* __restrict__ Wp, const XAd
         } else {
             wv[u] = Wp[(size_t)c * 64];
         }
-        // wave-uniform segment: scalar base + c*16 and row stride, per-lane row and k
+        // wave-uniform segment: scalar base + c * cs and row stride, per-lane row and offset
         const bool s0 = c < xa.cb0, s1 = c < xa.cb1;
-        const float* base = (s0 ? xa.p0 : (s1 ? xa.p1 : xa.p2)) + c * 16 + xa.xk;
+        const float* base = (s0 ? xa.p0 : (s1 ? xa.p1 : xa.p2)) + c * xa.cs + xa.xk;
         const int ld = s0 ? xa.ld0 : (s1 ? xa.ld1 : xa.ld2);
 #pragma unroll
         for (int mt = 0; mt < NT; ++mt) xv[u][mt] = *reinterpret_cast<const float4*>(base + xa.row[mt] * ld);
@@ -102,9 +106,11 @@ __device__ __forceinline__ void sg_mfma(int c0, int cend, const float4 (&wv)[UP]
 }
 
 // ROLE only names the instantiation (distinct kernel names in rocprof traces per decoder stage).
-// MT = m-tiles of 16 batch rows on the MFMA path; MT = 0 is the batch-1 VALU path.
-template <int MT, int EPI, int ROLE>
-__global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
+// MT = m-tiles of 16 batch rows on the MFMA path; MT = 0 is the batch-1 VALU path.  FRAG: the
+// activations come from fragment mirrors (Seg::pf) and the workgroup is 4 waves, one per SIMD
+// (sgemm_frag_kernel); otherwise 16 waves read row-major activations (sgemm_kernel).
+template <int MT, int EPI, int ROLE, bool FRAG>
+__device__ __forceinline__ void sgemm_body(const SGemmArgs& a) {
     constexpr bool VALU = MT == 0;
     constexpr int NT = VALU ? 1 : MT;
     // Latency structure (batch-1 decode: every launch is one dependent link of the step chain):
@@ -188,21 +194,23 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
     const int xk = (lane >> 4) * 4;
     XAddr<NT> xa;
     int kstart = 0;
+    const int fcs = FRAG ? a.ntf * 256 : 16;  // floats per chunk
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
         // the encoder LSTM reads one segment: its direction's previous hidden state
         const Seg& g = a.seg[EPI == EPI_ENC_LSTM ? (s == 0 ? dir : 2) : s];
         const bool live = EPI == EPI_ENC_LSTM ? s == 0 : s < a.nseg;
-        const float* base = live ? g.p - kstart : nullptr;
-        const int ld = live ? g.ld : 0;
+        const float* base = live ? (FRAG ? g.pf : g.p) - (kstart >> 4) * fcs : nullptr;
+        const int ld = live ? (FRAG ? 1 : g.ld) : 0;
         kstart += live ? g.len : 0;
         if (s == 0) { xa.p0 = base; xa.ld0 = ld; xa.cb0 = kstart >> 4; }
         if (s == 1) { xa.p1 = base; xa.ld1 = ld; xa.cb1 = kstart >> 4; }
         if (s == 2) { xa.p2 = base; xa.ld2 = ld; }
     }
+    xa.cs = fcs;
 #pragma unroll
-    for (int mt = 0; mt < NT; ++mt) xa.row[mt] = min(m0 + mt * 16 + xrow, a.B - 1);
-    xa.xk = xk;
+    for (int mt = 0; mt < NT; ++mt) xa.row[mt] = FRAG ? ((m0 >> 4) + mt) * 256 : min(m0 + mt * 16 + xrow, a.B - 1);
+    xa.xk = FRAG ? 4 * lane : xk;
 
     floatx4 acc[2][NT];  // MFMA accumulators (see sg_mfma)
 #pragma unroll
@@ -215,7 +223,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
         // runs its MFMAs (one memory round trip exposed per wave, not one per stage).  At batch
         // <= 16 one stage of 4 covers most of a wave's chunks; at 64 a wave owns 10 chunks of
         // the widest GEMM, 5 stages of 2.
-        constexpr int UP = NT == 1 ? 4 : 2;
+        constexpr int UP = (NT == 1 && !FRAG) ? 4 : 2;
         float4 wA[UP], xA[UP][NT], wB[UP], xB[UP][NT];
         if (cbeg < cend) sg_load<UP, NT, ROLE>(Wp, xa, cbeg, cend, wA, xA);
         for (int c0 = cbeg; c0 < cend; c0 += 2 * UP) {
@@ -306,6 +314,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                 else if (a.act == ACT_SIGMOID) v = sigmoidf_(v);
                 if (out) out[(int64_t)b * a.ldo + n] = v;
                 if (a.out2) a.out2[(int64_t)b * a.ldo2 + n] = v;
+                if (a.outf) a.outf[frag_idx(b, a.outf_k0 + n, a.ntf)] = v;
                 if (track && !pre_done) a.hist[(int64_t)b * a.ldh + (int64_t)step * a.N + n] = v;
             }
         }
@@ -338,7 +347,9 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
                     // n_steps are garbage the host masks out (tts_decoder_run zero-fills them)
                     if (track) a.hist[(int64_t)b * a.ldh + (int64_t)step * m.nmel + n] = v;
                 } else {
-                    m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
+                    const float pv = fmaxf(v, 0.f);  // prenet layer 1 of step t+1
+                    m.pre1[(int64_t)b * m.ldp + (n - m.nmel)] = pv;
+                    if (m.pre1f) m.pre1f[frag_idx(b, n - m.nmel, a.ntf)] = pv;
                 }
             }
         }
@@ -416,6 +427,7 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             const float n = tanhf((fin[bl][8 + u] + pre_bias[2]) + r * (fin[bl][12 + u] + pre_bias[3]));
             const float h = (pre_cell - n) * z + n;
             out[(int64_t)b * a.ldo + unit] = h;
+            if (a.outf) a.outf[frag_idx(b, a.outf_k0 + unit, a.ntf)] = h;
             if (a.gru.dout) a.gru.dout[(int64_t)b * a.gru.ldd + unit] = h + pre_res;
         }
     } else {
@@ -431,9 +443,25 @@ __global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
             const float go = fin[bl][12 + u] + pre_bias[3];
             const float c2 = sigmoidf_(gf) * pre_cell + sigmoidf_(gi) * tanhf(gg);
             a.cell[(int64_t)b * a.ldc + unit] = c2;
-            out[(int64_t)b * a.ldo + unit] = sigmoidf_(go) * tanhf(c2);
+            const float h = sigmoidf_(go) * tanhf(c2);
+            out[(int64_t)b * a.ldo + unit] = h;
+            if (a.outf) a.outf[frag_idx(b, a.outf_k0 + unit, a.ntf)] = h;
         }
     }
+}
+
+template <int MT, int EPI, int ROLE>
+__global__ __launch_bounds__(1024) void sgemm_kernel(const SGemmArgs a) {
+    sgemm_body<MT, EPI, ROLE, false>(a);
+}
+
+// Batched launches over fragment mirrors: 4 waves, one per SIMD, each with its own MFMA pipe and
+// up to 256 VGPRs.  16 waves per CU interleave load and MFMA phases in lockstep (measured: a
+// B=64 dec_lstm launch 26 us with row-major activations and 16 waves, 22.7 with mirrors and 16
+// waves, 12.5 with mirrors and 4 waves; MFMA alone 10.8; tools/microbench/sgemm_b64.hip).
+template <int MT, int EPI, int ROLE>
+__global__ __launch_bounds__(256) void sgemm_frag_kernel(const SGemmArgs a) {
+    sgemm_body<MT, EPI, ROLE, true>(a);
 }
 
 __global__ void sgemm_pack_kernel(const float* A, int K1, const float* Bm, int K2, int N, int rowmap, int H,
@@ -525,6 +553,23 @@ static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
     const int ntiles = (a.N + 15) / 16;
     const dim3 grid(ntiles), block(MAX_WAVES * 64);
     const int mt = (a.B + 15) / 16;
+    bool frag = a.B > 1 && a.nseg >= 1 && EPI != EPI_ENC_LSTM;
+    for (int i = 0; i < a.nseg; ++i) frag = frag && a.seg[i].pf != nullptr;
+    if (frag) {
+        // 256 threads: the element-per-thread epilogues need B * 16 <= 256 for the linear and
+        // fused-mel tiles (row groups of 16) and B * 4 <= 256 for the gate tiles
+        if (a.ntf < mt) return hipErrorInvalidValue;
+        const dim3 fb(256);
+        if (EPI == EPI_LINEAR || EPI == EPI_MEL_FUSED || ntiles < split_below())
+            hipLaunchKernelGGL((sgemm_frag_kernel<1, EPI, ROLE>), dim3(ntiles, mt), fb, 0, s, a);
+        else if (mt <= 1)
+            hipLaunchKernelGGL((sgemm_frag_kernel<1, EPI, ROLE>), grid, fb, 0, s, a);
+        else if (mt <= 2)
+            hipLaunchKernelGGL((sgemm_frag_kernel<2, EPI, ROLE>), grid, fb, 0, s, a);
+        else
+            hipLaunchKernelGGL((sgemm_frag_kernel<4, EPI, ROLE>), grid, fb, 0, s, a);
+        return hipGetLastError();
+    }
     if (a.B == 1)
         hipLaunchKernelGGL((sgemm_kernel<0, EPI, ROLE>), grid, block, 0, s, a);
     else if (mt <= 1)
