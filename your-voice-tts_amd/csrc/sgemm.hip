@@ -464,6 +464,13 @@ __global__ __launch_bounds__(256) void sgemm_frag_kernel(const SGemmArgs a) {
     sgemm_body<MT, EPI, ROLE, true>(a);
 }
 
+// Narrow GEMMs over fragment mirrors (one 16-row group per workgroup, <= 88 workgroups at B=64):
+// most CUs are idle, so the K split over 16 waves shortens each wave's dependent load chain.
+template <int EPI, int ROLE>
+__global__ __launch_bounds__(1024) void sgemm_frag16_kernel(const SGemmArgs a) {
+    sgemm_body<1, EPI, ROLE, true>(a);
+}
+
 __global__ void sgemm_pack_kernel(const float* A, int K1, const float* Bm, int K2, int N, int rowmap, int H,
                                   float* packed, size_t total) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -561,7 +568,7 @@ static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
         if (a.ntf < mt) return hipErrorInvalidValue;
         const dim3 fb(256);
         if (EPI == EPI_LINEAR || EPI == EPI_MEL_FUSED || ntiles < split_below())
-            hipLaunchKernelGGL((sgemm_frag_kernel<1, EPI, ROLE>), dim3(ntiles, mt), fb, 0, s, a);
+            hipLaunchKernelGGL((sgemm_frag16_kernel<EPI, ROLE>), dim3(ntiles, mt), block, 0, s, a);
         else if (mt <= 1)
             hipLaunchKernelGGL((sgemm_frag_kernel<1, EPI, ROLE>), grid, fb, 0, s, a);
         else if (mt <= 2)
