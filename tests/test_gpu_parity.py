@@ -365,3 +365,42 @@ def test_tacotron2_forward_ragged_batch_teacher_forcing():
     al = align[1, :, :7].cpu().numpy()
     np.testing.assert_array_equal(al.argmax(1), ref["align"].argmax(1))
     assert np.abs(stop[1].cpu().numpy() - ref["stop"]).max() < 1e-3
+
+
+@pytest.mark.gpu
+def test_tacotron2_forward_batch20_teacher_forcing_mirrors():
+    """Above 16 sentences the decoder GEMMs read fragment-order mirrors of their inputs
+    (csrc/sgemm.h: Seg::pf), kept beside the row-major state by every producer; under teacher
+    forcing the prenet runs on the teacher frame at every step and must keep the pre1 mirror in
+    step.  The fixture sentence and a shorter one inside a ragged batch of 20, against the
+    reference fixture and the oracle's forward (models/tacotron2.py:47-60)."""
+    z = golden("tf_fwdmask_L12")
+    fl = golden_flags(z)
+    m = _model(fl)
+    w = weights_mod()
+    T, B = 20, 20
+    rng = np.random.Generator(np.random.PCG64(90))
+    text = torch.zeros(B, 12, dtype=torch.long)
+    mels = np.zeros((B, T, 80), np.float32)
+    lens = []
+    ids2 = w.synthetic_ids(7, 88)
+    teacher2 = np.random.Generator(np.random.PCG64(89)).uniform(0, 1, size=(T, 80)).astype(np.float32)
+    for b in range(B):
+        if b == 0:
+            ids, mels[b] = z["ids"], z["teacher"][:T]
+        elif b == 1:
+            ids, mels[b] = ids2, teacher2
+        else:
+            ids = w.synthetic_ids(int(rng.integers(2, 13)), 100 + b)
+            mels[b] = rng.uniform(0, 1, size=(T, 80)).astype(np.float32)
+        text[b, :len(ids)] = torch.from_numpy(ids)
+        lens.append(len(ids))
+    mel, mel_post, align, stop = m.forward(text, torch.tensor(lens), torch.from_numpy(mels))
+    assert tuple(mel.shape) == (B, T, 80)
+    assert rel_rms(mel[0].cpu().numpy(), z["mel"].T[:T]) < MEL_RTOL
+    np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"][:T].argmax(1))
+    ref = Tacotron2Oracle(w.tacotron2_weights(0), dtype=np.float32, **fl).forward(ids2, teacher2)
+    assert rel_rms(mel[1].cpu().numpy(), ref["mel"]) < MEL_RTOL
+    assert rel_rms(mel_post[1].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
+    np.testing.assert_array_equal(align[1, :, :7].cpu().numpy().argmax(1), ref["align"].argmax(1))
+    assert np.abs(stop[1].cpu().numpy() - ref["stop"]).max() < 1e-3
