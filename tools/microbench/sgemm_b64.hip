@@ -114,6 +114,39 @@ __global__ __launch_bounds__(WAVES * 64) void k(const float* __restrict__ W, con
     }
 }
 
+// rewrites the activation buffer from every CU (what the previous step launch does in the decoder)
+__global__ void producer(float* X, int n, float v) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) X[i] = v;
+}
+
+template <int V, int WAVES = NW, int UP = 2, int ST = 2>
+static float run_prod(hipStream_t s, const float* W, float* X, float* out, bool gemm) {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    const int n = 200;
+    (void)hipStreamBeginCapture(s, hipStreamCaptureModeGlobal);
+    for (int i = 0; i < n; ++i) {
+        hipLaunchKernelGGL(producer, dim3(256), dim3(256), 0, s, X, B * K, (float)i);
+        if (gemm) hipLaunchKernelGGL((k<V, WAVES, UP, ST>), dim3(N / 16), dim3(WAVES * 64), 0, s, W, X, out);
+    }
+    (void)hipStreamEndCapture(s, &g);
+    (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    for (int w = 0; w < 2; ++w) (void)hipGraphLaunch(ge, s);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, s);
+    const int reps = 5;
+    for (int r = 0; r < reps; ++r) (void)hipGraphLaunch(ge, s);
+    (void)hipEventRecord(b, s);
+    (void)hipEventSynchronize(b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    return 1000.f * ms / (reps * n);
+}
+
 template <int V, int WAVES = NW, int UP = 2, int ST = 2>
 static float run(hipStream_t s, const float* W, const float* X, float* out) {
     hipGraph_t g;
@@ -149,16 +182,12 @@ int main() {
     CK(hipMemset(W, 0, (size_t)N * K * 4));
     CK(hipMemset(X, 0, (size_t)B * K * 4 + 4096));
     printf("dec_lstm shape K=%d N=%d B=%d, %d WGs x %d waves (us per launch, dependent chain)\n", K, N, B, N / 16, NW);
-    printf("  current: rows, 16 waves, 2x2   %7.2f\n", run<15>(s, W, X, out));
-    printf("  frag, 4 waves, 3 stages of 4   %7.2f\n", run<31, 4, 4, 3>(s, W, X, out));
-    printf("  rows, 4 waves, 3 stages of 4   %7.2f\n", run<15, 4, 4, 3>(s, W, X, out));
-    printf("  frag, 4 waves, 2 stages of 4   %7.2f\n", run<31, 4, 4, 2>(s, W, X, out));
-    printf("  rows, 4 waves, 2 stages of 4   %7.2f\n", run<15, 4, 4, 2>(s, W, X, out));
-    printf("  frag, 4 waves, 3 stages of 2   %7.2f\n", run<31, 4, 2, 3>(s, W, X, out));
-    printf("  rows, 4 waves, 3 stages of 2   %7.2f\n", run<15, 4, 2, 3>(s, W, X, out));
     printf("  frag, 4 waves, 2 stages of 2   %7.2f\n", run<31, 4, 2, 2>(s, W, X, out));
-    printf("  frag, 4 waves, MFMA only       %7.2f\n", run<12 + 16, 4, 4, 3>(s, W, X, out));
-    printf("  frag, 4 waves, loads only      %7.2f\n", run<27, 4, 4, 3>(s, W, X, out));
-    printf("  rows, 4 waves, loads only      %7.2f\n", run<11, 4, 4, 3>(s, W, X, out));
+    const float p0 = run_prod<31, 4, 2, 2>(s, W, X, out, false);
+    const float p1 = run_prod<31, 4, 2, 2>(s, W, X, out, true);
+    printf("  producer alone                 %7.2f\n", p0);
+    printf("  producer + frag gemm           %7.2f  (gemm after a fresh X: %.2f)\n", p1, p1 - p0);
+    const float p2 = run_prod<15>(s, W, X, out, true);
+    printf("  producer + rows gemm (16 w)    %7.2f  (gemm after a fresh X: %.2f)\n", p2, p2 - p0);
     return 0;
 }

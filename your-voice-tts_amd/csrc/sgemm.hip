@@ -37,7 +37,7 @@ struct XAddr {
 // [c0, c0 + UP).  Chunks past cend load chunk cend-1 again (callers skip their FMAs): every load
 // is unconditional, so the wait before a stage's MFMAs counts exactly the next stage's loads
 // (a load under a branch makes the compiler wait for everything).  Requires cend > c0.
-template <int UP, int NT, int ROLE>
+template <int UP, int NT, int ROLE, bool FRAG = false>
 __device__ __forceinline__ void sg_load(const float4* __restrict__ Wp, const XAddr<NT> xa, int c0, int cend,
                                         float4 (&wv)[UP], float4 (&xv)[UP][NT]) {
 #pragma unroll
@@ -54,54 +54,42 @@ __device__ __forceinline__ void sg_load(const float4* __restrict__ Wp, const XAd
         // wave-uniform segment: scalar base + c * cs and row stride, per-lane row and offset
         const bool s0 = c < xa.cb0, s1 = c < xa.cb1;
         const float* base = (s0 ? xa.p0 : (s1 ? xa.p1 : xa.p2)) + c * xa.cs + xa.xk;
-        const int ld = s0 ? xa.ld0 : (s1 ? xa.ld1 : xa.ld2);
+        if (FRAG) {
+            // uniform chunk base + a 32-bit per-lane offset: the load's scalar-base form, no
+            // per-load 64-bit address arithmetic
+            const float* cbase = (s0 ? xa.p0 : (s1 ? xa.p1 : xa.p2)) + c * xa.cs;
 #pragma unroll
-        for (int mt = 0; mt < NT; ++mt) xv[u][mt] = *reinterpret_cast<const float4*>(base + xa.row[mt] * ld);
+            for (int mt = 0; mt < NT; ++mt)
+                xv[u][mt] = *reinterpret_cast<const float4*>(cbase + (unsigned)(xa.row[mt] + xa.xk));
+        } else {
+            const int ld = s0 ? xa.ld0 : (s1 ? xa.ld1 : xa.ld2);
+#pragma unroll
+            for (int mt = 0; mt < NT; ++mt) xv[u][mt] = *reinterpret_cast<const float4*>(base + xa.row[mt] * ld);
+        }
     }
 }
 
 // The MFMAs of one stage; chunk u accumulates into chain u & 1 at NT == 1 (two independent
 // chains hide the MFMA latency), into the m-tile's one chain otherwise (NT chains interleave).
+// Padding chunks (past cend: sg_load re-loaded chunk cend-1) multiply a zeroed weight fragment:
+// no branch around an MFMA, so the accumulators need no copies between loop blocks (copies that
+// otherwise force a full memory wait ahead of the next stage's loads).
 template <int UP, int NT>
 __device__ __forceinline__ void sg_mfma(int c0, int cend, const float4 (&wv)[UP], const float4 (&xv)[UP][NT],
                                         floatx4 (&acc)[2][NT]) {
-    if (NT == 1) {
-        static_assert(NT != 1 || UP % 2 == 0, "NT == 1 pairs chunks");
-#pragma unroll
-        for (int u = 0; u < UP; u += 2) {
-            floatx4& a0 = acc[0][0];
-            floatx4& a1 = acc[1][0];
-            if (c0 + u + 1 < cend) {  // wave-uniform
-                a0 = mfma16x16x4(xv[u][0].x, wv[u].x, a0);
-                a1 = mfma16x16x4(xv[u + 1][0].x, wv[u + 1].x, a1);
-                a0 = mfma16x16x4(xv[u][0].y, wv[u].y, a0);
-                a1 = mfma16x16x4(xv[u + 1][0].y, wv[u + 1].y, a1);
-                a0 = mfma16x16x4(xv[u][0].z, wv[u].z, a0);
-                a1 = mfma16x16x4(xv[u + 1][0].z, wv[u + 1].z, a1);
-                a0 = mfma16x16x4(xv[u][0].w, wv[u].w, a0);
-                a1 = mfma16x16x4(xv[u + 1][0].w, wv[u + 1].w, a1);
-            } else if (c0 + u < cend) {
-                a0 = mfma16x16x4(xv[u][0].x, wv[u].x, a0);
-                a0 = mfma16x16x4(xv[u][0].y, wv[u].y, a0);
-                a0 = mfma16x16x4(xv[u][0].z, wv[u].z, a0);
-                a0 = mfma16x16x4(xv[u][0].w, wv[u].w, a0);
-            }
-        }
-        return;
-    }
 #pragma unroll
     for (int u = 0; u < UP; ++u) {
-        if (c0 + u < cend) {  // wave-uniform: no MFMAs on the padding of the last stage
-            floatx4* ac = acc[0];
+        const bool live = c0 + u < cend;  // wave-uniform
+        const float4 w = live ? wv[u] : float4{0.f, 0.f, 0.f, 0.f};
+        const int ch = NT == 1 ? (u & 1) : 0;
 #pragma unroll
-            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].x, wv[u].x, ac[mt]);
+        for (int mt = 0; mt < NT; ++mt) acc[ch][mt] = mfma16x16x4(xv[u][mt].x, w.x, acc[ch][mt]);
 #pragma unroll
-            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].y, wv[u].y, ac[mt]);
+        for (int mt = 0; mt < NT; ++mt) acc[ch][mt] = mfma16x16x4(xv[u][mt].y, w.y, acc[ch][mt]);
 #pragma unroll
-            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].z, wv[u].z, ac[mt]);
+        for (int mt = 0; mt < NT; ++mt) acc[ch][mt] = mfma16x16x4(xv[u][mt].z, w.z, acc[ch][mt]);
 #pragma unroll
-            for (int mt = 0; mt < NT; ++mt) ac[mt] = mfma16x16x4(xv[u][mt].w, wv[u].w, ac[mt]);
-        }
+        for (int mt = 0; mt < NT; ++mt) acc[ch][mt] = mfma16x16x4(xv[u][mt].w, w.w, acc[ch][mt]);
     }
 }
 
@@ -119,7 +107,10 @@ __device__ __forceinline__ void sgemm_body(const SGemmArgs& a) {
     // (A scalar load of the step state would be waited on at once, before the weight loads
     // issue.)  The "all sentences done" exit is taken after the MFMAs: it only costs steps past
     // the end.
-    const int* sp = a.step ? a.step : kOneActive;
+    // a global-address-space load: through a generic pointer this would be a FLAT load, which
+    // counts in both vmcnt and lgkmcnt and makes every later memory wait of the main loop a full one
+    typedef const __attribute__((address_space(1))) int* gint_p;
+    const gint_p sp = (gint_p)(a.step ? a.step : kOneActive);
     int st_x = sp[0];
     int st_y = sp[1];
     const int ntile = blockIdx.x;
@@ -225,14 +216,24 @@ __device__ __forceinline__ void sgemm_body(const SGemmArgs& a) {
         // the widest GEMM, 5 stages of 2.
         constexpr int UP = (NT == 1 && !FRAG) ? 4 : 2;
         float4 wA[UP], xA[UP][NT], wB[UP], xB[UP][NT];
-        if (cbeg < cend) sg_load<UP, NT, ROLE>(Wp, xa, cbeg, cend, wA, xA);
-        for (int c0 = cbeg; c0 < cend; c0 += 2 * UP) {
-            sg_load<UP, NT, ROLE>(Wp, xa, c0 + UP, cend, wB, xB);
+        // (the scheduling barriers keep each stage's loads issued ahead of the previous stage's
+        // MFMAs: left alone the scheduler sinks them below, which serialises load and MFMA time)
+        // Stage pairs without an exit in between (a mid-loop exit makes the register allocator
+        // rotate the accumulators through copies at the back edge); an odd last stage runs after
+        // the loop on the loads its last iteration issued.
+        const int nst = (cend - cbeg + UP - 1) / UP;
+        if (nst > 0) sg_load<UP, NT, ROLE, FRAG>(Wp, xa, cbeg, cend, wA, xA);
+        int st = 0;
+        for (; st + 1 < nst; st += 2) {
+            const int c0 = cbeg + st * UP;
+            sg_load<UP, NT, ROLE, FRAG>(Wp, xa, c0 + UP, cend, wB, xB);
+            __builtin_amdgcn_sched_barrier(0);
             sg_mfma<UP, NT>(c0, cend, wA, xA, acc);
-            if (c0 + UP >= cend) break;
-            sg_load<UP, NT, ROLE>(Wp, xa, c0 + 2 * UP, cend, wA, xA);
+            sg_load<UP, NT, ROLE, FRAG>(Wp, xa, c0 + 2 * UP, cend, wA, xA);
+            __builtin_amdgcn_sched_barrier(0);
             sg_mfma<UP, NT>(c0 + UP, cend, wB, xB, acc);
         }
+        if (st < nst) sg_mfma<UP, NT>(cbeg + st * UP, cend, wA, xA, acc);
     }
     // VALU path (batch 1): U chunks of loads (U KiB of weights per wave) in flight before the
     // first FMA; one round covers every decoder shape (<= 10 chunks per wave at 16 waves, K <= 2560)
