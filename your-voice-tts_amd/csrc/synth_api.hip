@@ -5,10 +5,10 @@
 // host round trips between them: one H2D of the ids, the decoder's stop-step readback (the
 // sentence length is decided on the device) and the stages' own completion waits.  The stages
 // run in pipeline mode (common.h) and the call returns once Griffin-Lim is enqueued: the
-// waveform is ready when the caller's stream reaches it.  Griffin-Lim runs on a second stream of
-// this handle, so call k+1's encoder + decoder (which read only host inputs and this handle's
-// buffers) overlap call k's Griffin-Lim on the device; the stage buffers Griffin-Lim reads
-// (mel_post, its compacted copy) alternate per call.
+// waveform is ready when the caller's stream reaches it.  Above 256 frames Griffin-Lim runs on a
+// second stream of this handle, so call k+1's encoder + decoder (which read only host inputs and
+// this handle's buffers) need not wait for call k's Griffin-Lim; the stage buffers Griffin-Lim
+// reads (mel_post, its compacted copy) alternate per call.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -234,10 +234,19 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         TTS_HIP(hipMemcpy2DAsync(s->spec[par], Fmax * row, post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, ss));
         spec = s->spec[par];
     }
-    hipStream_t gs = s->gl_stream;
-    TTS_HIP(hipEventRecord(s->ev_post, ss));
+    // Small jobs (<= 256 frames: the persistent Griffin-Lim, whose spinning grid must not share the
+    // device with the next call's resident launches anyway) stay on the front stream: no
+    // cross-queue hand-offs on the latency-bound batch-1 path.  Larger ones move to gl_stream,
+    // so the next call's encoder + decoder need not wait for them.
+    int frames_total = 0;
+    for (int b = 0; b < B; ++b) frames_total += h_frames[b];
+    const bool same = frames_total <= 256;
+    hipStream_t gs = same ? ss : s->gl_stream;
     TTS_HIP(hipEventRecord(s->ev_in, cs));
-    TTS_HIP(hipStreamWaitEvent(gs, s->ev_post, 0));
+    if (!same) {
+        TTS_HIP(hipEventRecord(s->ev_post, ss));
+        TTS_HIP(hipStreamWaitEvent(gs, s->ev_post, 0));
+    }
     TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
     // shorter sentences leave their waveform tail unwritten: zero it
     if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
@@ -245,7 +254,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, gs))) return st;
     int path = 0;
     if ((st = tts_gl_last_path(s->g, &path))) return st;
-    s->gl_spins = path == TTS_GL_PATH_PERSISTENT;
+    s->gl_spins = !same && path == TTS_GL_PATH_PERSISTENT;
     TTS_HIP(hipEventRecord(s->ev_out, gs));
     TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
     return TTS_OK;
