@@ -46,6 +46,8 @@ tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, 
 hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args, size_t smem, hipStream_t s,
                              bool* launched);
 // the CU count launch_persistent plans with (device CUs, capped by TTS_CU_CAP)
+// rows [B][K] (row stride ld) -> their fragment-order mirror (frag_idx, ntf m-tiles)
+hipError_t frag_mirror(const float* src, int64_t ld, int B, int K, float* dst, int ntf, hipStream_t s);
 int usable_cus();
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));

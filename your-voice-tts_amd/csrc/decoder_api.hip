@@ -119,13 +119,6 @@ bool frag_on(const tts_decoder* d, int B) {
     return d->xaf && B > 16 && !off;
 }
 
-__global__ void frag_mirror_kernel(const float* src, int64_t ld, int B, int K, float* dst, int ntf) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B * K) return;
-    const int b = i / K, k = i % K;
-    dst[frag_idx(b, k, ntf)] = src[(int64_t)b * ld + k];
-}
-
 // Mirrors of the state a run starts from (after launch_decoder_init): both parities of xa, h_att
 // and h_dec (pre1 is mirrored by the prenet launch that writes it).
 tts_status enqueue_frag_sync(tts_decoder* d, int B, hipStream_t s) {
@@ -136,11 +129,7 @@ tts_status enqueue_frag_sync(tts_decoder* d, int B, hipStream_t s) {
             {d->xa + p * xps, XA, XA, d->xaf + p * fx},
             {d->h_att + p * hps, HATT, HATT, d->hattf + p * fh},
             {d->h_dec + p * hps, HDEC, HDEC, d->hdecf + p * fh}};
-        for (auto& j : jobs) {
-            const int n = B * j.K;
-            hipLaunchKernelGGL(frag_mirror_kernel, dim3((n + 255) / 256), dim3(256), 0, s, j.src, j.ld, B, j.K, j.dst, d->ntf);
-            TTS_HIP(hipGetLastError());
-        }
+        for (auto& j : jobs) TTS_HIP(frag_mirror(j.src, j.ld, B, j.K, j.dst, d->ntf, s));
     }
     return TTS_OK;
 }

@@ -83,6 +83,19 @@ hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args,
     return e;
 }
 
+__global__ void frag_mirror_kernel(const float* src, int64_t ld, int B, int K, float* dst, int ntf) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * K) return;
+    const int b = i / K, k = i % K;
+    dst[frag_idx(b, k, ntf)] = src[(int64_t)b * ld + k];
+}
+
+hipError_t frag_mirror(const float* src, int64_t ld, int B, int K, float* dst, int ntf, hipStream_t s) {
+    const int n = B * K;
+    hipLaunchKernelGGL(frag_mirror_kernel, dim3((n + 255) / 256), dim3(256), 0, s, src, ld, B, K, dst, ntf);
+    return hipGetLastError();
+}
+
 }  // namespace tts
 
 extern "C" {

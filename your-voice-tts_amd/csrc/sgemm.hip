@@ -561,6 +561,8 @@ static hipError_t launch_role(const SGemmArgs& a, hipStream_t s) {
     const int ntiles = (a.N + 15) / 16;
     const dim3 grid(ntiles), block(MAX_WAVES * 64);
     const int mt = (a.B + 15) / 16;
+    // (the encoder LSTM, whose K = 256 steps are launch-latency bound, stays row-major: mirrors
+    // of its h measured no faster)
     bool frag = a.B > 1 && a.nseg >= 1 && EPI != EPI_ENC_LSTM;
     for (int i = 0; i < a.nseg; ++i) frag = frag && a.seg[i].pf != nullptr;
     if (frag) {
