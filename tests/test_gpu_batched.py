@@ -190,3 +190,35 @@ def test_tacotron2_synthesis_both_modes(audio_cfg, truncated):
     np.random.seed(5)
     ref = AudioOracle(**a).inv_mel_spectrogram(z["mel_post"].T)
     assert wav.shape == ref.shape and rel_rms(wav, ref) < 1e-4
+
+
+def test_griffin_lim_wave_kernel_ragged_vs_oracle(audio_cfg, monkeypatch):
+    """The one-wave-per-frame iteration kernel (gl_iter_wave_kernel, the batched default) on a
+    ragged batch whose B * Fmax keeps the unfused loop: sentences of 2, 3 and 5 frames (every
+    frame's STFT input reflected at both ends), mid-length and long ones; each sentence vs the
+    oracle at 60 iterations (1e-4) and vs the 256-thread block kernel (TTS_GL_WAVE=0) on the same
+    phases."""
+    audio = load_pkg("audio")
+    o = AudioOracle(**audio_cfg)
+    rng = np.random.Generator(np.random.PCG64(11))
+    Fs = [2, 3, 5, 150, 33, 220, 64, 7]
+    Fmax = max(Fs)
+    assert len(Fs) * Fmax > 1024
+    mel = np.zeros((len(Fs), Fmax, 80), np.float32)
+    pu = np.zeros((len(Fs), 1025, Fmax))
+    for b, F in enumerate(Fs):
+        mel[b, :F] = rng.uniform(0, 1, size=(F, 80))
+        pu[b, :, :F] = rng.uniform(0, 1, size=(1025, F))
+    mel_d = torch.from_numpy(mel).cuda()
+    ap = audio.AudioProcessor(**audio_cfg)
+    wav = ap.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    assert ap.last_gl_path() == "unfused"
+    monkeypatch.setenv("TTS_GL_WAVE", "0")
+    ap_block = audio.AudioProcessor(**audio_cfg)
+    wav_block = ap_block.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    for b, F in enumerate(Fs):
+        n = ap.hop_length * (F - 1)
+        ref = o.inv_mel_spectrogram(mel[b, :F].T, pu[b, :, :F])
+        assert rel_rms(wav[b, :n], ref) < WAV_RTOL, (b, F)
+        assert rel_rms(wav[b, :n], wav_block[b, :n]) < WAV_RTOL, (b, F)
+        assert np.all(wav[b, n:] == 0)

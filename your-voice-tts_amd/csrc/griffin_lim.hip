@@ -390,6 +390,7 @@ struct IterArgs {
     unsigned long long seed;
     unsigned* zero_flags;   // initial iSTFT only: the persistent loop's tag words to clear, or null
     int* zero_status;       // ... and its status word
+    const double2* wt;      // gl_iter_wave_kernel: [32][64] pass twiddles
 };
 
 __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned long long idx) {
@@ -531,6 +532,267 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
         const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
         if (n >= 0 && n < g.win) out[n] = wo[i] * (zv * (1.0 / NH));
     }
+}
+
+// ---------------------------------------------------------------- GL iteration, one wave per frame
+// The batched form of gl_iter_kernel<false, false> (same inputs: the previous iteration's float32
+// signal; same output: the windowed float64 frame), with each frame's whole iteration on ONE
+// wave: the 1024-point complex FFT as radix 16 x 16 x 4 with 16 points per lane in registers and
+// two wave-local LDS transposes per FFT, so no pass waits on a workgroup barrier and every
+// butterfly's operands stay in VGPRs.  Index map (lane L, register r):
+//   pass 1:  z[L + 64 r]                     radix-16 over r, x W1024^(L k2)
+//   pass 2:  lane p1 + 4 k2, register p2     radix-16 over p2, x W64^(p1 q2)
+//   pass 3:  lane r3 + 4 k2, register 4j+p1  radix-4 over p1
+//   output:  lane r3 + 4 k2, register 4j+q1 holds Z[256 q1 + 64 j + 16 r3 + k2]
+// The real-FFT split, the phase step and the inverse pre-split run per bin pair (k, 1024 - k) in
+// the lane that owns k in the pass-1 layout of the inverse FFT; the partner's pre-split value moves
+// to its owner lane (64 - L) through LDS.  LDS slots are XOR-swizzled so every exchange is free of
+// bank conflicts (ds_write_b128 8-lane groups, ds_read_b128 16-lane groups).
+// Twiddles: wt[k2][L] = W1024^(L k2) and wt[16 + q2][L] = W64^((L & 3) q2) (host-built, f64).
+constexpr int WV_SLOTS = NH + 1;  // LDS complex slots per wave (the Nyquist bin at slot 1024)
+
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return double2{a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return double2{a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ double2 cmulf(double2 a, double2 w) {  // a * w
+    return double2{fma(a.x, w.x, -(a.y * w.y)), fma(a.x, w.y, a.y * w.x)};
+}
+__device__ __forceinline__ double2 cmulcf(double2 a, double2 w) {  // a * conj(w)
+    return double2{fma(a.x, w.x, a.y * w.y), fma(a.y, w.x, -(a.x * w.y))};
+}
+template <bool INV>
+__device__ __forceinline__ double2 rotq(double2 a) {  // a * (-i) forward, a * (+i) inverse
+    return INV ? double2{-a.y, a.x} : double2{a.y, -a.x};
+}
+template <bool INV>
+__device__ __forceinline__ void dft4(double2& a0, double2& a1, double2& a2, double2& a3) {
+    const double2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = rotq<INV>(csub(a1, a3));
+    a0 = cadd(t0, t2);
+    a1 = cadd(t1, t3);
+    a2 = csub(t0, t2);
+    a3 = csub(t1, t3);
+}
+// a * W16^E (E in 1..9; the inverse uses conj(W16^E))
+template <int E, bool INV>
+__device__ __forceinline__ double2 tw16(double2 a) {
+    constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173, C2 = 0.70710678118654752440;
+    if constexpr (E == 4) return rotq<INV>(a);
+    if constexpr (E == 2) {  // (1 - i) / sqrt 2
+        return INV ? double2{C2 * (a.x - a.y), C2 * (a.x + a.y)} : double2{C2 * (a.x + a.y), C2 * (a.y - a.x)};
+    }
+    if constexpr (E == 6) {  // (-1 - i) / sqrt 2
+        return INV ? double2{-C2 * (a.x + a.y), C2 * (a.x - a.y)} : double2{C2 * (a.y - a.x), -C2 * (a.x + a.y)};
+    }
+    constexpr double wr = E == 1 ? C1 : E == 3 ? S1 : -C1;  // E = 1, 3, 9
+    constexpr double wi = E == 1 ? -S1 : E == 3 ? -C1 : S1;
+    return INV ? cmulcf(a, double2{wr, wi}) : cmulf(a, double2{wr, wi});
+}
+// in-register 16-point DFT: v[n] -> v[k] (natural order), as 4 x 4 with W16 twiddles
+template <bool INV>
+__device__ __forceinline__ void dft16(double2 (&v)[16]) {
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) dft4<INV>(v[n1], v[n1 + 4], v[n1 + 8], v[n1 + 12]);  // k2 at v[n1 + 4 k2]
+    v[5] = tw16<1, INV>(v[5]);
+    v[9] = tw16<2, INV>(v[9]);
+    v[13] = tw16<3, INV>(v[13]);
+    v[6] = tw16<2, INV>(v[6]);
+    v[10] = tw16<4, INV>(v[10]);
+    v[14] = tw16<6, INV>(v[14]);
+    v[7] = tw16<3, INV>(v[7]);
+    v[11] = tw16<6, INV>(v[11]);
+    v[15] = tw16<9, INV>(v[15]);
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) dft4<INV>(v[4 * k2], v[4 * k2 + 1], v[4 * k2 + 2], v[4 * k2 + 3]);  // X[4 k1 + k2] at v[4 k2 + k1]
+    double2 o[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) o[4 * k1 + k2] = v[4 * k2 + k1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = o[i];
+}
+__device__ __forceinline__ int wv_a1(int k2, int n1) { return k2 * 64 + (n1 ^ (4 * (k2 & 3))); }
+__device__ __forceinline__ int wv_a2(int k2, int p1, int q2) { return k2 * 64 + ((4 * q2) ^ (4 * (k2 & 1))) + (p1 ^ (k2 & 3)); }
+__device__ __forceinline__ int wv_sig(int k) { return k ^ (((k >> 4) & 3) << 1); }
+
+// 1024-point complex FFT of one wave (forward: e^{-i}, inverse: e^{+i}, unnormalised).
+// In: v[r] = z[L + 64 r].  Out: v[4 j + q1] = Z[256 q1 + 64 j + 16 (L & 3) + (L >> 2)].
+// Ends with the pass-3 reads of `lds` complete in registers; the caller may rewrite `lds` only
+// after values that depend on every read (any pass-3 output does).
+template <bool INV>
+__device__ __forceinline__ void wave_fft1024(double2 (&v)[16], double2* lds, __amdgpu_buffer_rsrc_t wt, int L) {
+    dft16<INV>(v);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) {
+        const double2 w = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(wt, 16 * L, 1024 * k2, 0));
+        v[k2] = INV ? cmulcf(v[k2], w) : cmulf(v[k2], w);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) lds[wv_a1(k2, L)] = v[k2];
+    __syncthreads();  // one wave per workgroup: orders the lanes' LDS writes before the reads
+    const int p1 = L & 3, K2 = L >> 2;
+#pragma unroll
+    for (int p2 = 0; p2 < 16; ++p2) v[p2] = lds[wv_a1(K2, p1 + 4 * p2)];
+    dft16<INV>(v);
+#pragma unroll
+    for (int q2 = 1; q2 < 16; ++q2) {
+        const double2 w = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(wt, 16 * L, 1024 * (16 + q2), 0));
+        v[q2] = INV ? cmulcf(v[q2], w) : cmulf(v[q2], w);
+    }
+#pragma unroll
+    for (int q2 = 0; q2 < 16; ++q2) lds[wv_a2(K2, p1, q2)] = v[q2];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) v[4 * j + pp] = lds[wv_a2(K2, pp, 4 * j + p1)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dft4<INV>(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    __syncthreads();  // a pass-3 output depends on its own 4 reads only: no later LDS write may pass them
+}
+
+// STFT value X (rounded to complex64, librosa stft dtype) -> |S| X / |X| (angle(0) = 0)
+__device__ __forceinline__ double2 unit_phase(double2 X, double s) {
+    const double xre = (double)(float)X.x, xim = (double)(float)X.y;
+    const double m2 = xre * xre + xim * xim;
+    const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
+    return m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
+}
+// inverse real-FFT pre-split: z'[k] = E + i O, E = (X[k] + conj X[N-k]) / 2, O = (X[k] - conj X[N-k]) / 2 * conj(t)
+__device__ __forceinline__ double2 inv_presplit(double2 xk, double2 xm, double2 t) {
+    const double2 E = double2{0.5 * (xk.x + xm.x), 0.5 * (xk.y - xm.y)};
+    const double2 D = double2{0.5 * (xk.x - xm.x), 0.5 * (xk.y + xm.y)};
+    const double2 O = cmulcf(D, t);
+    return double2{E.x - O.y, E.y + O.x};
+}
+
+// buffer-resource access (SGPR base + 32-bit lane offset; out-of-range loads read 0, stores drop)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_f32(__amdgpu_buffer_rsrc_t r, int voff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+}
+__device__ __forceinline__ double buf_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+__device__ __forceinline__ double2 buf_c64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, int voff) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
+}
+
+__global__ __launch_bounds__(64) void gl_iter_wave_kernel(const IterArgs a) {
+    const int b = blockIdx.y;
+    const int f = xcd_remap(blockIdx.x, gridDim.x);
+    const int Fb = a.F[b];
+    if (f >= Fb) return;
+    const Geo g = a.g;
+    const int L = threadIdx.x;
+    __shared__ __align__(16) double2 lds[WV_SLOTS];
+    const auto rS = buf_rsrc(a.S + ((int64_t)b * a.Fmax + f) * NB, NB * 8);
+    const auto rW = buf_rsrc(a.c.win, NFFT * 8);
+    const auto rT = buf_rsrc(a.c.tw, NFFT * 16);
+    const auto rP = buf_rsrc(a.wt, 32 * 64 * 16);
+    // ---- STFT input: z[L + 64 r] = x[2 (L + 64 r)] + i x[2 (L + 64 r) + 1], x = window * y_pad (the
+    // window table is zero outside its support, where the range-checked loads may read anything)
+    const int N = g.hop * (Fb - 1);
+    const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax, (unsigned)N * 4);
+    const int base = f * g.hop - NFFT / 2;
+    double2 v[16];
+    float y0[16], y1[16];
+    if (base + g.woff >= 0 && base + g.woff + g.win <= N) {  // the support needs no reflection
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int s = 2 * (L + 64 * r);
+            y0[r] = buf_f32(rY, (base + s) * 4);
+            y1[r] = buf_f32(rY, (base + s + 1) * 4);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int s = 2 * (L + 64 * r);
+            y0[r] = buf_f32(rY, reflect_idx(base + s, N) * 4);
+            y1[r] = buf_f32(rY, reflect_idx(base + s + 1, N) * 4);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const double2 w = buf_c64(rW, 16 * L, 1024 * r);
+        v[r] = double2{w.x * (double)y0[r], w.y * (double)y1[r]};
+    }
+    wave_fft1024<false>(v, lds, rP, L);
+    // ---- Z to LDS in natural (swizzled) order
+    const int r3 = L & 3, K2 = L >> 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q1 = 0; q1 < 4; ++q1) lds[wv_sig(256 * q1 + 64 * j + 16 * r3 + K2)] = v[4 * j + q1];
+    __syncthreads();
+    // ---- bin pairs (k, 1024 - k), k = L + 64 m, m < 8; plus k = 512 (lane 0)
+    double2 zk[8], zm[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        zk[m] = lds[wv_sig(L + 64 * m)];
+        zm[m] = lds[wv_sig((NH - L - 64 * m) & (NH - 1))];
+    }
+    const double2 z512 = lds[wv_sig(512)];
+    double sa[8], sb[8];
+    double2 tk[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        sa[m] = buf_f64(rS, 8 * L, 512 * m);
+        sb[m] = buf_f64(rS, 8 * (NH - L - 64 * m), 0);
+        tk[m] = buf_c64(rT, 16 * L, 1024 * m);
+    }
+    const double s512 = buf_f64(rS, 0, 4096);
+    const double2 t512 = buf_c64(rT, 0, 8192);
+    __syncthreads();  // every lane's Z reads are done before the exchange below rewrites lds
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const double2 zc = cconj(zm[m]);
+        const double2 E = double2{0.5 * (zk[m].x + zc.x), 0.5 * (zk[m].y + zc.y)};
+        const double2 O = double2{0.5 * (zk[m].y - zc.y), -0.5 * (zk[m].x - zc.x)};
+        const double2 tO = cmulf(O, tk[m]);
+        double2 xk = unit_phase(cadd(E, tO), sa[m]);         // X[k]
+        double2 xm = unit_phase(cconj(csub(E, tO)), sb[m]);  // X[1024 - k]
+        const bool k0 = (L | m) == 0;
+        if (k0) {  // istft: .real of the Hermitian extension at DC and Nyquist
+            xk.y = 0.0;
+            xm.y = 0.0;
+        }
+        v[m] = inv_presplit(xk, xm, tk[m]);
+        // the partner bin 1024 - k belongs to lane (64 - L) & 63, register 15 - m (16 - m on lane 0)
+        const double2 vm = inv_presplit(xm, xk, double2{-tk[m].x, tk[m].y});
+        const int R = L == 0 ? 16 - m : 15 - m;
+        if (!k0) lds[(R - 8) * 64 + ((64 - L) & 63)] = vm;
+    }
+    if (L == 0) {  // k = 512 pairs with itself
+        const double2 zc = cconj(z512);
+        const double2 E = double2{0.5 * (z512.x + zc.x), 0.5 * (z512.y + zc.y)};
+        const double2 O = double2{0.5 * (z512.y - zc.y), -0.5 * (z512.x - zc.x)};
+        const double2 x = unit_phase(cadd(E, cmulf(O, t512)), s512);
+        lds[0] = inv_presplit(x, x, t512);  // slot (lane 0, register 8)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int R = 8; R < 16; ++R) v[R] = lds[(R - 8) * 64 + L];
+    // ---- inverse FFT; z'[n] -> real samples 2n, 2n + 1; window the support and store float64
+    // (the frame's store range is its support: stores outside it are dropped by the range check)
+    wave_fft1024<true>(v, lds, rP, L);
+    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.win * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q1 = 0; q1 < 4; ++q1) {
+            const int s = 2 * (256 * q1 + 64 * j + 16 * r3 + K2);
+            const double2 w = buf_c64(rW, 16 * (16 * r3 + K2), 16 * (256 * q1 + 64 * j));
+            const double2 z = v[4 * j + q1];
+            buf_st_f64(w.x * (z.x * (1.0 / NH)), rO, (s - g.woff) * 8);
+            buf_st_f64(w.y * (z.y * (1.0 / NH)), rO, (s + 1 - g.woff) * 8);
+        }
 }
 
 // ---------------------------------------------------------------- persistent GL loop (small batches)
@@ -961,6 +1223,8 @@ struct tts_gl {
     int* NS = nullptr;  // mel analysis: samples per sentence
     int NS_cap = 0;
     double2* tw = nullptr;
+    double2* wt = nullptr;  // gl_iter_wave_kernel pass twiddles [32][64]
+    bool wave = true;       // batched iterations on gl_iter_wave_kernel (TTS_GL_WAVE=0: gl_iter_kernel)
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
     double *S = nullptr, *frames = nullptr;
@@ -997,7 +1261,7 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr})
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
     for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done})
@@ -1047,6 +1311,20 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if ((e = hipMemcpy(g->win2, win2.data(), NFFT * 8, hipMemcpyHostToDevice)) != hipSuccess) return fail(e, "copy");
     if ((e = hipMemcpy(g->tw, tw.data(), NFFT * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "copy");
+    {
+        // wt[k2][L] = W1024^(L k2), wt[16 + q2][L] = W64^((L & 3) q2)
+        std::vector<double2> wt(32 * 64);
+        for (int r = 0; r < 16; ++r)
+            for (int L = 0; L < 64; ++L) {
+                const double a1 = 2.0 * M_PI * (double)(L * r) / 1024.0, a2 = 2.0 * M_PI * (double)((L & 3) * r) / 64.0;
+                wt[r * 64 + L] = double2{std::cos(a1), -std::sin(a1)};
+                wt[(16 + r) * 64 + L] = double2{std::cos(a2), -std::sin(a2)};
+            }
+        if ((e = hipMalloc(&g->wt, wt.size() * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
+        if ((e = hipMemcpy(g->wt, wt.data(), wt.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
+            return fail(e, "copy");
+        g->wave = !getenv_off("TTS_GL_WAVE");
+    }
     if (inv_mel_basis) {
         const size_t n = (size_t)NB * cfg->num_mels;
         if ((e = hipMalloc(&g->pinv, n * 8)) != hipSuccess) return fail(e, "hipMalloc");
@@ -1191,6 +1469,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.y = g->y;
     ia.Nmax = Nmax;
     ia.next = fr0;
+    ia.wt = g->wt;
     if (persistent) {
         if ((size_t)B * Fmax > g->flags_n) {
             if (g->flags) TTS_HIP(hipFree(g->flags));
@@ -1287,7 +1566,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                     FinArgs o = fa;
                     o.frames = g->frames + (i & 1) * fstride;
                     hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, o);
-                    hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+                    if (g->wave)
+                        hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
+                    else
+                        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
                 }
             }
             hipError_t ce = hipGetLastError();
@@ -1368,6 +1650,8 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
         TTS_HIP(hipEventRecord(ev[1], s));
         if (g->last_fused)
             hipLaunchKernelGGL((gl_iter_kernel<false, true>), grid, block, 0, s, a);
+        else if (g->wave)
+            hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
         TTS_HIP(hipGetLastError());
