@@ -390,7 +390,9 @@ struct IterArgs {
     unsigned long long seed;
     unsigned* zero_flags;   // initial iSTFT only: the persistent loop's tag words to clear, or null
     int* zero_status;       // ... and its status word
-    const double2* wt;      // gl_iter_wave_kernel: [32][64] pass twiddles
+    const double2* wt;      // gl_iter_wave_kernel: [16][4] pass-2 twiddles
+    const double2* winc;    // gl_iter_wave_kernel: [4][64] window rotation bases (see tts_gl_create)
+    double2 wrot;           // ... and the rotation per register step, e^{2 pi i 128 / win}
 };
 
 __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned long long idx) {
@@ -551,6 +553,17 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
 // Twiddles: wt[k2][L] = W1024^(L k2) and wt[16 + q2][L] = W64^((L & 3) q2) (host-built, f64).
 constexpr int WV_SLOTS = NH + 1;  // LDS complex slots per wave (the Nyquist bin at slot 1024)
 
+// W32^m = e^{-i pi m / 16}, m < 8 (the split twiddle steps of the bin-pair loop)
+__device__ constexpr double kW32[8][2] = {
+    {1.00000000000000000000, -0.00000000000000000000},
+    {0.98078528040323043058, -0.19509032201612824808},
+    {0.92387953251128673848, -0.38268343236508978178},
+    {0.83146961230254523567, -0.55557023301960217765},
+    {0.70710678118654757274, -0.70710678118654746172},
+    {0.55557023301960228867, -0.83146961230254523567},
+    {0.38268343236508983729, -0.92387953251128673848},
+    {0.19509032201612833135, -0.98078528040323043058}};
+
 __device__ __forceinline__ double2 cadd(double2 a, double2 b) { return double2{a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ double2 csub(double2 a, double2 b) { return double2{a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ double2 cmulf(double2 a, double2 w) {  // a * w
@@ -610,57 +623,99 @@ __device__ __forceinline__ void dft16(double2 (&v)[16]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = o[i];
 }
-__device__ __forceinline__ int wv_a1(int k2, int n1) { return k2 * 64 + (n1 ^ (4 * (k2 & 3))); }
-__device__ __forceinline__ int wv_a2(int k2, int p1, int q2) { return k2 * 64 + ((4 * q2) ^ (4 * (k2 & 1))) + (p1 ^ (k2 & 3)); }
-__device__ __forceinline__ int wv_sig(int k) { return k ^ (((k >> 4) & 3) << 1); }
+// LDS slots (8-byte words; every exchange moves real parts, then imaginary parts, through one
+// 1025-word buffer).  Bank rules: ds_write_b64 in 16-lane contiguous groups over 32 banks,
+// ds_read_b64 in 32-lane halves over 64 banks; these swizzles keep every exchange conflict-free.
+__device__ __forceinline__ int wv_a1(int k2, int n1) { return k2 * 64 + (n1 ^ (4 * (k2 & 7))); }
+__device__ __forceinline__ int wv_a2(int k2, int p1, int q2) { return k2 * 64 + 4 * (q2 ^ (k2 & 7)) + (p1 ^ (k2 & 3)); }
+__device__ __forceinline__ int wv_sig(int k) { return k ^ (((k >> 4) & 3) << 2); }
+
+// All-to-all of one wave's 16 complex registers through `lds`: real parts, then imaginary parts.
+// Each round overwrites only registers whose value has already been stored (the real parts are
+// read back into the real halves after every lane stored them), so 8 KB of LDS suffice.
+template <class WS, class RS>
+__device__ __forceinline__ void wave_xchg(double2 (&v)[16], double* lds, WS wslot, RS rslot) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds[wslot(r)] = v[r].x;
+    __syncthreads();  // one wave per workgroup: orders the lanes' LDS writes before the reads
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r].x = lds[rslot(r)];
+    __syncthreads();  // the imaginary stores below do not depend on these reads
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds[wslot(r)] = v[r].y;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r].y = lds[rslot(r)];
+}
 
 // 1024-point complex FFT of one wave (forward: e^{-i}, inverse: e^{+i}, unnormalised).
 // In: v[r] = z[L + 64 r].  Out: v[4 j + q1] = Z[256 q1 + 64 j + 16 (L & 3) + (L >> 2)].
-// Ends with the pass-3 reads of `lds` complete in registers; the caller may rewrite `lds` only
-// after values that depend on every read (any pass-3 output does).
+// Twiddles: pass 1 multiplies register k2 by w^k2, w = W1024^L (one load), the powers built by a
+// product tree (depth <= 4, a few ulp); pass 2 reads W64^(p1 q2) from the wave's 64-entry LDS
+// table t2[q2][p1] (4 distinct addresses per read).  The vector-memory path was the bound.
+// Ends after a barrier that follows the last LDS reads.
 template <bool INV>
-__device__ __forceinline__ void wave_fft1024(double2 (&v)[16], double2* lds, __amdgpu_buffer_rsrc_t wt, int L) {
+__device__ __forceinline__ void wave_fft1024(double2 (&v)[16], double* lds, const double2* t2, __amdgpu_buffer_rsrc_t tw,
+                                             int lane) {
+    // the lane index is laundered per call: otherwise the inverse FFT reuses the forward's loads
+    // and LDS addresses, which then stay live (and spill) across the spectrum step
+    int L = lane;
+    asm volatile("" : "+v"(L));
+    const double2 w1 = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(tw, 32 * L, 0, 0));
     dft16<INV>(v);
-#pragma unroll
-    for (int k2 = 1; k2 < 16; ++k2) {
-        const double2 w = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(wt, 16 * L, 1024 * k2, 0));
-        v[k2] = INV ? cmulcf(v[k2], w) : cmulf(v[k2], w);
+    {
+        auto mul = [&](double2 a, double2 w) { return INV ? cmulcf(a, w) : cmulf(a, w); };
+        const double2 w2 = cmulf(w1, w1), w4 = cmulf(w2, w2), w8 = cmulf(w4, w4);
+        const double2 w3 = cmulf(w2, w1), w12 = cmulf(w8, w4);
+        v[1] = mul(v[1], w1);
+        v[2] = mul(v[2], w2);
+        v[3] = mul(v[3], w3);
+        v[4] = mul(v[4], w4);
+        v[5] = mul(v[5], cmulf(w4, w1));
+        v[6] = mul(v[6], cmulf(w4, w2));
+        v[7] = mul(v[7], cmulf(w4, w3));
+        v[8] = mul(v[8], w8);
+        v[9] = mul(v[9], cmulf(w8, w1));
+        v[10] = mul(v[10], cmulf(w8, w2));
+        v[11] = mul(v[11], cmulf(w8, w3));
+        v[12] = mul(v[12], w12);
+        v[13] = mul(v[13], cmulf(w12, w1));
+        v[14] = mul(v[14], cmulf(w12, w2));
+        v[15] = mul(v[15], cmulf(w12, w3));
     }
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) lds[wv_a1(k2, L)] = v[k2];
-    __syncthreads();  // one wave per workgroup: orders the lanes' LDS writes before the reads
     const int p1 = L & 3, K2 = L >> 2;
-#pragma unroll
-    for (int p2 = 0; p2 < 16; ++p2) v[p2] = lds[wv_a1(K2, p1 + 4 * p2)];
+    wave_xchg(v, lds, [&](int k2) { return wv_a1(k2, L); }, [&](int p2) { return wv_a1(K2, p1 + 4 * p2); });
     dft16<INV>(v);
 #pragma unroll
     for (int q2 = 1; q2 < 16; ++q2) {
-        const double2 w = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(wt, 16 * L, 1024 * (16 + q2), 0));
+        const double2 w = t2[q2 * 4 + p1];
         v[q2] = INV ? cmulcf(v[q2], w) : cmulf(v[q2], w);
     }
-#pragma unroll
-    for (int q2 = 0; q2 < 16; ++q2) lds[wv_a2(K2, p1, q2)] = v[q2];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) v[4 * j + pp] = lds[wv_a2(K2, pp, 4 * j + p1)];
+    __syncthreads();  // the previous exchange's last reads are done before this one's stores
+    wave_xchg(v, lds, [&](int q2) { return wv_a2(K2, p1, q2); },
+              [&](int r) { return wv_a2(K2, r & 3, 4 * (r >> 2) + p1); });
 #pragma unroll
     for (int j = 0; j < 4; ++j) dft4<INV>(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
-    __syncthreads();  // a pass-3 output depends on its own 4 reads only: no later LDS write may pass them
+    __syncthreads();
 }
 
-// STFT value X (rounded to complex64, librosa stft dtype) -> |S| X / |X| (angle(0) = 0)
+// STFT value X (rounded to complex64, librosa stft dtype) -> |S| X / |X| (angle(0) = 0).  The
+// reference's unit phase is itself complex64 (np.exp(1j * np.angle(X)) on a complex64 X), so the
+// hardware reciprocal square root plus one Newton step (relative error far below float32's) is
+// ample; X may carry any power-of-two scale (the result does not).  |X|^2 of two floats is
+// within fp64 range, so no operand scaling is needed.
 __device__ __forceinline__ double2 unit_phase(double2 X, double s) {
     const double xre = (double)(float)X.x, xim = (double)(float)X.y;
-    const double m2 = xre * xre + xim * xim;
-    const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
-    return m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
+    const double m2 = fma(xre, xre, xim * xim);
+    double r = __builtin_amdgcn_rsq(m2);
+    r = fma(0.5 * r, fma(-m2 * r, r, 1.0), r);
+    return m2 > 0.0 ? double2{s * (xre * r), s * (xim * r)} : double2{s, 0.0};
 }
-// inverse real-FFT pre-split: z'[k] = E + i O, E = (X[k] + conj X[N-k]) / 2, O = (X[k] - conj X[N-k]) / 2 * conj(t)
-__device__ __forceinline__ double2 inv_presplit(double2 xk, double2 xm, double2 t) {
-    const double2 E = double2{0.5 * (xk.x + xm.x), 0.5 * (xk.y - xm.y)};
-    const double2 D = double2{0.5 * (xk.x - xm.x), 0.5 * (xk.y + xm.y)};
+// inverse real-FFT pre-split, times 2: z'[k] = E + i O, 2E = X[k] + conj X[N-k],
+// 2O = (X[k] - conj X[N-k]) * conj(t) (the factor 1/2 is folded into the output scale)
+__device__ __forceinline__ double2 inv_presplit2(double2 xk, double2 xm, double2 t) {
+    const double2 E = double2{xk.x + xm.x, xk.y - xm.y};
+    const double2 D = double2{xk.x - xm.x, xk.y + xm.y};
     const double2 O = cmulcf(D, t);
     return double2{E.x - O.y, E.y + O.x};
 }
@@ -684,114 +739,180 @@ __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, i
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
 }
 
-__global__ __launch_bounds__(64) void gl_iter_wave_kernel(const IterArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void gl_iter_wave_kernel(const IterArgs a) {
     const int b = blockIdx.y;
     const int f = xcd_remap(blockIdx.x, gridDim.x);
     const int Fb = a.F[b];
     if (f >= Fb) return;
     const Geo g = a.g;
     const int L = threadIdx.x;
-    __shared__ __align__(16) double2 lds[WV_SLOTS];
+    __shared__ double lds[WV_SLOTS];
+    __shared__ double2 t2[64];  // W64^(p1 q2) at [q2][p1]
     const auto rS = buf_rsrc(a.S + ((int64_t)b * a.Fmax + f) * NB, NB * 8);
-    const auto rW = buf_rsrc(a.c.win, NFFT * 8);
+    const auto rC = buf_rsrc(a.winc, 4 * 64 * 16);
     const auto rT = buf_rsrc(a.c.tw, NFFT * 16);
-    const auto rP = buf_rsrc(a.wt, 32 * 64 * 16);
-    // ---- STFT input: z[L + 64 r] = x[2 (L + 64 r)] + i x[2 (L + 64 r) + 1], x = window * y_pad (the
-    // window table is zero outside its support, where the range-checked loads may read anything)
+    const auto rP = buf_rsrc(a.wt, 64 * 16);
+    // ---- STFT input: z[L + 64 r] = x[2 (L + 64 r)] + i x[2 (L + 64 r) + 1], x = window * y_pad.
+    // The periodic Hann at sample s is 1/2 - 1/2 Re c(s), c(s) = e^{2 pi i (s - woff) / win}; the
+    // lane's samples step by 128 per register, so c = c0 R^r (one base load per parity, the
+    // rotation R uniform: a few ulp, instead of 16 window-table loads).  Outside the support the
+    // sample is exactly 0: the support-sized y range reads 0 there, or (reflected frames) a select.
     const int N = g.hop * (Fb - 1);
-    const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax, (unsigned)N * 4);
     const int base = f * g.hop - NFFT / 2;
+    const double2 R = a.wrot;
     double2 v[16];
     float y0[16], y1[16];
-    if (base + g.woff >= 0 && base + g.woff + g.win <= N) {  // the support needs no reflection
+    const bool interior = base + g.woff >= 0 && base + g.woff + g.win <= N;
+    if (interior) {  // the support needs no reflection
+        const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax + base + g.woff, (unsigned)g.win * 4);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int s = 2 * (L + 64 * r);
-            y0[r] = buf_f32(rY, (base + s) * 4);
-            y1[r] = buf_f32(rY, (base + s + 1) * 4);
+            const int s = 2 * (L + 64 * r) - g.woff;
+            y0[r] = buf_f32(rY, s * 4);
+            y1[r] = buf_f32(rY, (s + 1) * 4);
         }
     } else {
+        const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax, (unsigned)N * 4);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int s = 2 * (L + 64 * r);
-            y0[r] = buf_f32(rY, reflect_idx(base + s, N) * 4);
-            y1[r] = buf_f32(rY, reflect_idx(base + s + 1, N) * 4);
+            const bool i0 = s >= g.woff && s < g.woff + g.win, i1 = s + 1 >= g.woff && s + 1 < g.woff + g.win;
+            y0[r] = i0 ? buf_f32(rY, reflect_idx(base + s, N) * 4) : 0.f;
+            y1[r] = i1 ? buf_f32(rY, reflect_idx(base + s + 1, N) * 4) : 0.f;
         }
     }
+    {
+        double2 c0 = buf_c64(rC, 16 * L, 0), c1 = buf_c64(rC, 16 * L, 1024);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const double2 w = buf_c64(rW, 16 * L, 1024 * r);
-        v[r] = double2{w.x * (double)y0[r], w.y * (double)y1[r]};
+        for (int r = 0; r < 16; ++r) {
+            v[r] = double2{fma(-0.5, c0.x, 0.5) * (double)y0[r], fma(-0.5, c1.x, 0.5) * (double)y1[r]};
+            if (r < 15) {
+                c0 = cmulf(c0, R);
+                c1 = cmulf(c1, R);
+            }
+        }
     }
-    wave_fft1024<false>(v, lds, rP, L);
-    // ---- Z to LDS in natural (swizzled) order
+    t2[L] = buf_c64(rP, 16 * L, 0);  // first LDS use: ordered before the reads by the FFT's barriers
+    wave_fft1024<false>(v, lds, t2, rT, L);
+    // ---- Z to LDS in natural (swizzled) order, real parts then imaginary parts; bin pairs
+    // (k, 1024 - k), k = L + 64 m, m < 8, plus k = 512.  sig() only permutes bits 2-3 by bits 4-5,
+    // so every address below is one per-lane base plus a multiple of 64 slots: Z[k] at zb + 64 m,
+    // Z[1024 - k] at mb + 64 (15 - m) (for lane 0, m = 0 that is the spare slot 1024: Z[0] is taken
+    // from its own Z[k] read, and the partner store that pair does not have lands there).  Every
+    // LDS store is unconditional: a divergent store makes the compiler branch around the partner's
+    // computation and spill.
     const int r3 = L & 3, K2 = L >> 2;
+    const int wb = wv_sig(16 * r3 + K2);              // this lane's output Z[256 q1 + 64 j + wb']
+    const int zb = wv_sig(L);                         // Z[L + 64 m]
+    const int mb = wv_sig((64 - L) & 63) + (L == 0 ? 64 : 0);
+    double zkr[8], zmr[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int q1 = 0; q1 < 4; ++q1) lds[wv_sig(256 * q1 + 64 * j + 16 * r3 + K2)] = v[4 * j + q1];
+        for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].x;
     __syncthreads();
-    // ---- bin pairs (k, 1024 - k), k = L + 64 m, m < 8; plus k = 512 (lane 0)
-    double2 zk[8], zm[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        zk[m] = lds[wv_sig(L + 64 * m)];
-        zm[m] = lds[wv_sig((NH - L - 64 * m) & (NH - 1))];
+        zkr[m] = lds[zb + 64 * m];
+        zmr[m] = lds[mb + 64 * (15 - m)];
     }
-    const double2 z512 = lds[wv_sig(512)];
-    double sa[8], sb[8];
-    double2 tk[8];
+    if (L == 0) zmr[0] = zkr[0];
+    const double z512r = lds[512];  // sig(512) = 512
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].y;
+    __syncthreads();
+    const double z512i = lds[512];
+    // One pair at a time (its imaginary parts, |S| and split twiddle read one pair ahead).  The
+    // partner bin's pre-split value goes to lane (64 - L) & 63, register 15 - m (16 - m on lane 0),
+    // i.e. to the slot of Z[1024 - k]: a slot only this lane reads (512 is read by one instruction
+    // of all lanes and rewritten by lane 0 only), so it is stored in place with no barrier; its
+    // real part at once, its imaginary part after the next barrier.
+    double vmy[8];
+    double zki = lds[zb], zmi = lds[mb + 64 * 15];
+    if (L == 0) zmi = zki;
+    double sa = buf_f64(rS, 8 * L, 0), sb = buf_f64(rS, 8 * (NH - L), 0);
+    // split twiddles t[k] = W2048^(L + 64 m) = W2048^L x W32^m (compile-time W32^m)
+    const double2 tL = buf_c64(rT, 16 * L, 0);
+    double2 tk = tL;
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
-        sa[m] = buf_f64(rS, 8 * L, 512 * m);
-        sb[m] = buf_f64(rS, 8 * (NH - L - 64 * m), 0);
-        tk[m] = buf_c64(rT, 16 * L, 1024 * m);
-    }
-    const double s512 = buf_f64(rS, 0, 4096);
-    const double2 t512 = buf_c64(rT, 0, 8192);
-    __syncthreads();  // every lane's Z reads are done before the exchange below rewrites lds
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        const double2 zc = cconj(zm[m]);
-        const double2 E = double2{0.5 * (zk[m].x + zc.x), 0.5 * (zk[m].y + zc.y)};
-        const double2 O = double2{0.5 * (zk[m].y - zc.y), -0.5 * (zk[m].x - zc.x)};
-        const double2 tO = cmulf(O, tk[m]);
-        double2 xk = unit_phase(cadd(E, tO), sa[m]);         // X[k]
-        double2 xm = unit_phase(cconj(csub(E, tO)), sb[m]);  // X[1024 - k]
-        const bool k0 = (L | m) == 0;
-        if (k0) {  // istft: .real of the Hermitian extension at DC and Nyquist
+        __builtin_amdgcn_sched_barrier(0);
+        const int k = L + 64 * m;
+        double zki_n = 0.0, zmi_n = 0.0, sa_n, sb_n = 0.0;
+        double2 tk_n = double2{0.0, 0.0};
+        if (m < 7) {
+            zki_n = lds[zb + 64 * (m + 1)];
+            zmi_n = lds[mb + 64 * (14 - m)];
+            sa_n = buf_f64(rS, 8 * L, 512 * (m + 1));
+            sb_n = buf_f64(rS, 8 * (NH - k - 64), 0);
+            tk_n = cmulf(tL, double2{kW32[m + 1][0], kW32[m + 1][1]});
+        } else {
+            sa_n = buf_f64(rS, 0, 4096);  // k = 512
+            tk_n = buf_c64(rT, 0, 8192);  // k = 512
+        }
+        // 2E = Z[k] + conj Z[N-k], 2O = -i (Z[k] - conj Z[N-k]): X[k] = E + t O up to the factor 2
+        const double2 E = double2{zkr[m] + zmr[m], zki - zmi};
+        const double2 O = double2{zki + zmi, zmr[m] - zkr[m]};
+        const double2 tO = cmulf(O, tk);
+        double2 xk = unit_phase(cadd(E, tO), sa);         // X[k]
+        double2 xm = unit_phase(cconj(csub(E, tO)), sb);  // X[1024 - k]
+        if ((L | m) == 0) {  // istft: .real of the Hermitian extension at DC and Nyquist
             xk.y = 0.0;
             xm.y = 0.0;
         }
-        v[m] = inv_presplit(xk, xm, tk[m]);
-        // the partner bin 1024 - k belongs to lane (64 - L) & 63, register 15 - m (16 - m on lane 0)
-        const double2 vm = inv_presplit(xm, xk, double2{-tk[m].x, tk[m].y});
-        const int R = L == 0 ? 16 - m : 15 - m;
-        if (!k0) lds[(R - 8) * 64 + ((64 - L) & 63)] = vm;
+        v[m] = inv_presplit2(xk, xm, tk);
+        const double2 vm = inv_presplit2(xm, xk, double2{-tk.x, tk.y});
+        lds[mb + 64 * (15 - m)] = vm.x;
+        vmy[m] = vm.y;
+        zki = zki_n;
+        zmi = zmi_n;
+        sa = sa_n;
+        sb = sb_n;
+        tk = tk_n;
     }
-    if (L == 0) {  // k = 512 pairs with itself
-        const double2 zc = cconj(z512);
-        const double2 E = double2{0.5 * (z512.x + zc.x), 0.5 * (z512.y + zc.y)};
-        const double2 O = double2{0.5 * (z512.y - zc.y), -0.5 * (z512.x - zc.x)};
-        const double2 x = unit_phase(cadd(E, cmulf(O, t512)), s512);
-        lds[0] = inv_presplit(x, x, t512);  // slot (lane 0, register 8)
+    __builtin_amdgcn_sched_barrier(0);
+    double2 v512;
+    {  // k = 512 pairs with itself: 2E = (2 Re Z, 0), 2O = (2 Im Z, 0)
+        const double2 x = unit_phase(double2{2.0 * z512r + 2.0 * z512i * tk.x, 2.0 * z512i * tk.y}, sa);
+        v512 = inv_presplit2(x, x, tk);
     }
+    lds[512] = v512.x;  // the same value from every lane
     __syncthreads();
 #pragma unroll
-    for (int R = 8; R < 16; ++R) v[R] = lds[(R - 8) * 64 + L];
+    for (int R = 8; R < 16; ++R) v[R].x = lds[zb + 64 * R];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+        lds[mb + 64 * (15 - m)] = vmy[m];
+    lds[512] = v512.y;
+    __syncthreads();
+#pragma unroll
+    for (int R = 8; R < 16; ++R) v[R].y = lds[zb + 64 * R];
+    __syncthreads();
     // ---- inverse FFT; z'[n] -> real samples 2n, 2n + 1; window the support and store float64
     // (the frame's store range is its support: stores outside it are dropped by the range check)
-    wave_fft1024<true>(v, lds, rP, L);
+    wave_fft1024<true>(v, lds, t2, rT, L);
+    // (samples 2 (16 r3 + K2) + 128 (j + 4 q1): the window by the same rotation, stores outside the
+    // support dropped by the frame's range)
     const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.win * 8);
+    __builtin_amdgcn_sched_barrier(0);
+    double2 c0 = buf_c64(rC, 16 * L, 2048), c1 = buf_c64(rC, 16 * L, 3072);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int q1 = 0; q1 < 4; ++q1)
 #pragma unroll
-        for (int q1 = 0; q1 < 4; ++q1) {
+        for (int j = 0; j < 4; ++j) {
             const int s = 2 * (256 * q1 + 64 * j + 16 * r3 + K2);
-            const double2 w = buf_c64(rW, 16 * (16 * r3 + K2), 16 * (256 * q1 + 64 * j));
             const double2 z = v[4 * j + q1];
-            buf_st_f64(w.x * (z.x * (1.0 / NH)), rO, (s - g.woff) * 8);
-            buf_st_f64(w.y * (z.y * (1.0 / NH)), rO, (s + 1 - g.woff) * 8);
+            // (1/2 of the pre-split) x 1/NH: one exact power-of-two scale
+            buf_st_f64(fma(-0.5, c0.x, 0.5) * (z.x * (0.5 / NH)), rO, (s - g.woff) * 8);
+            buf_st_f64(fma(-0.5, c1.x, 0.5) * (z.y * (0.5 / NH)), rO, (s + 1 - g.woff) * 8);
+            if (j + 4 * q1 < 15) {
+                c0 = cmulf(c0, R);
+                c1 = cmulf(c1, R);
+            }
         }
 }
 
@@ -1223,7 +1344,9 @@ struct tts_gl {
     int* NS = nullptr;  // mel analysis: samples per sentence
     int NS_cap = 0;
     double2* tw = nullptr;
-    double2* wt = nullptr;  // gl_iter_wave_kernel pass twiddles [32][64]
+    double2* wt = nullptr;  // gl_iter_wave_kernel pass-2 twiddles [16][4]
+    double2* winc = nullptr;  // gl_iter_wave_kernel window rotation bases [4][64]
+    double2 wrot{};
     bool wave = true;       // batched iterations on gl_iter_wave_kernel (TTS_GL_WAVE=0: gl_iter_kernel)
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
@@ -1261,7 +1384,7 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt})
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt, (void*)g->winc})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
     for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done})
@@ -1312,16 +1435,31 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if ((e = hipMemcpy(g->tw, tw.data(), NFFT * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
         return fail(e, "copy");
     {
-        // wt[k2][L] = W1024^(L k2), wt[16 + q2][L] = W64^((L & 3) q2)
-        std::vector<double2> wt(32 * 64);
-        for (int r = 0; r < 16; ++r)
-            for (int L = 0; L < 64; ++L) {
-                const double a1 = 2.0 * M_PI * (double)(L * r) / 1024.0, a2 = 2.0 * M_PI * (double)((L & 3) * r) / 64.0;
-                wt[r * 64 + L] = double2{std::cos(a1), -std::sin(a1)};
-                wt[(16 + r) * 64 + L] = double2{std::cos(a2), -std::sin(a2)};
+        // wt[q2][p1] = W64^(p1 q2): the pass-2 twiddles of gl_iter_wave_kernel
+        std::vector<double2> wt(64);
+        for (int q2 = 0; q2 < 16; ++q2)
+            for (int p1 = 0; p1 < 4; ++p1) {
+                const double a2 = 2.0 * M_PI * (double)(p1 * q2) / 64.0;
+                wt[q2 * 4 + p1] = double2{std::cos(a2), -std::sin(a2)};
             }
         if ((e = hipMalloc(&g->wt, wt.size() * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
         if ((e = hipMemcpy(g->wt, wt.data(), wt.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
+            return fail(e, "copy");
+        // window rotation bases: c(s) = e^{2 pi i (s - woff) / win} at the first sample of each lane,
+        // input order (s = 2 L + e) and output order (s = 2 (16 (L & 3) + (L >> 2)) + e), e = 0, 1
+        std::vector<double2> wc(4 * 64);
+        for (int L = 0; L < 64; ++L)
+            for (int e = 0; e < 2; ++e) {
+                const int si = 2 * L + e, so = 2 * (16 * (L & 3) + (L >> 2)) + e;
+                const double ai = 2.0 * M_PI * (double)(si - g->g.woff) / cfg->win_length;
+                const double ao = 2.0 * M_PI * (double)(so - g->g.woff) / cfg->win_length;
+                wc[e * 64 + L] = double2{std::cos(ai), std::sin(ai)};
+                wc[(2 + e) * 64 + L] = double2{std::cos(ao), std::sin(ao)};
+            }
+        const double ar = 2.0 * M_PI * 128.0 / cfg->win_length;
+        g->wrot = double2{std::cos(ar), std::sin(ar)};
+        if ((e = hipMalloc(&g->winc, wc.size() * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
+        if ((e = hipMemcpy(g->winc, wc.data(), wc.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e, "copy");
         g->wave = !getenv_off("TTS_GL_WAVE");
     }
@@ -1470,6 +1608,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.Nmax = Nmax;
     ia.next = fr0;
     ia.wt = g->wt;
+    ia.winc = g->winc;
+    ia.wrot = g->wrot;
     if (persistent) {
         if ((size_t)B * Fmax > g->flags_n) {
             if (g->flags) TTS_HIP(hipFree(g->flags));
