@@ -391,8 +391,8 @@ struct IterArgs {
     unsigned* zero_flags;   // initial iSTFT only: the persistent loop's tag words to clear, or null
     int* zero_status;       // ... and its status word
     const double2* wt;      // gl_iter_wave_kernel: [16][4] pass-2 twiddles
-    const double2* winc;    // gl_iter_wave_kernel: [4][64] window rotation bases (see tts_gl_create)
-    double2 wrot;           // ... and the rotation per register step, e^{2 pi i 128 / win}
+    const double2* winc;    // gl_iter_wave_kernel: [4][64] window cosine seeds (see tts_gl_create)
+    double wrot;            // ... and the recurrence factor 2 cos(2 pi 128 / win)
 };
 
 __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned long long idx) {
@@ -753,13 +753,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const auto rT = buf_rsrc(a.c.tw, NFFT * 16);
     const auto rP = buf_rsrc(a.wt, 64 * 16);
     // ---- STFT input: z[L + 64 r] = x[2 (L + 64 r)] + i x[2 (L + 64 r) + 1], x = window * y_pad.
-    // The periodic Hann at sample s is 1/2 - 1/2 Re c(s), c(s) = e^{2 pi i (s - woff) / win}; the
-    // lane's samples step by 128 per register, so c = c0 R^r (one base load per parity, the
-    // rotation R uniform: a few ulp, instead of 16 window-table loads).  Outside the support the
-    // sample is exactly 0: the support-sized y range reads 0 there, or (reflected frames) a select.
+    // The periodic Hann at sample s is 1/2 - 1/2 c(s), c(s) = cos(2 pi (s - woff) / win); the lane's
+    // samples step by 128 per register, so c follows the Chebyshev recurrence
+    // c_{r+1} = 2 cos(theta) c_r - c_{r-1} (one fma per sample from two seeds per parity, a few
+    // ulp over 16 steps, instead of 16 window-table loads).  Outside the support the sample is
+    // exactly 0: the support-sized y range reads 0 there, or (reflected frames) a select.
     const int N = g.hop * (Fb - 1);
     const int base = f * g.hop - NFFT / 2;
-    const double2 R = a.wrot;
+    const double K = a.wrot;
     double2 v[16];
     float y0[16], y1[16];
     const bool interior = base + g.woff >= 0 && base + g.woff + g.win <= N;
@@ -782,14 +783,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         }
     }
     {
-        double2 c0 = buf_c64(rC, 16 * L, 0), c1 = buf_c64(rC, 16 * L, 1024);
+        const double2 s0 = buf_c64(rC, 16 * L, 0), s1 = buf_c64(rC, 16 * L, 1024);  // (c_0, c_1) per parity
+        double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            v[r] = double2{fma(-0.5, c0.x, 0.5) * (double)y0[r], fma(-0.5, c1.x, 0.5) * (double)y1[r]};
-            if (r < 15) {
-                c0 = cmulf(c0, R);
-                c1 = cmulf(c1, R);
-            }
+            v[r] = double2{fma(-0.5, a0, 0.5) * (double)y0[r], fma(-0.5, b0, 0.5) * (double)y1[r]};
+            const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
+            a0 = a1;
+            a1 = a2;
+            b0 = b1;
+            b1 = b2;
         }
     }
     t2[L] = buf_c64(rP, 16 * L, 0);  // first LDS use: ordered before the reads by the FFT's barriers
@@ -899,7 +902,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // support dropped by the frame's range)
     const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.win * 8);
     __builtin_amdgcn_sched_barrier(0);
-    double2 c0 = buf_c64(rC, 16 * L, 2048), c1 = buf_c64(rC, 16 * L, 3072);
+    const double2 s0 = buf_c64(rC, 16 * L, 2048), s1 = buf_c64(rC, 16 * L, 3072);
+    double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
 #pragma unroll
     for (int q1 = 0; q1 < 4; ++q1)
 #pragma unroll
@@ -907,12 +911,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             const int s = 2 * (256 * q1 + 64 * j + 16 * r3 + K2);
             const double2 z = v[4 * j + q1];
             // (1/2 of the pre-split) x 1/NH: one exact power-of-two scale
-            buf_st_f64(fma(-0.5, c0.x, 0.5) * (z.x * (0.5 / NH)), rO, (s - g.woff) * 8);
-            buf_st_f64(fma(-0.5, c1.x, 0.5) * (z.y * (0.5 / NH)), rO, (s + 1 - g.woff) * 8);
-            if (j + 4 * q1 < 15) {
-                c0 = cmulf(c0, R);
-                c1 = cmulf(c1, R);
-            }
+            buf_st_f64(fma(-0.5, a0, 0.5) * (z.x * (0.5 / NH)), rO, (s - g.woff) * 8);
+            buf_st_f64(fma(-0.5, b0, 0.5) * (z.y * (0.5 / NH)), rO, (s + 1 - g.woff) * 8);
+            const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
+            a0 = a1;
+            a1 = a2;
+            b0 = b1;
+            b1 = b2;
         }
 }
 
@@ -1346,7 +1351,7 @@ struct tts_gl {
     double2* tw = nullptr;
     double2* wt = nullptr;  // gl_iter_wave_kernel pass-2 twiddles [16][4]
     double2* winc = nullptr;  // gl_iter_wave_kernel window rotation bases [4][64]
-    double2 wrot{};
+    double wrot = 0.0;
     bool wave = true;       // batched iterations on gl_iter_wave_kernel (TTS_GL_WAVE=0: gl_iter_kernel)
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
@@ -1445,19 +1450,19 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
         if ((e = hipMalloc(&g->wt, wt.size() * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
         if ((e = hipMemcpy(g->wt, wt.data(), wt.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e, "copy");
-        // window rotation bases: c(s) = e^{2 pi i (s - woff) / win} at the first sample of each lane,
-        // input order (s = 2 L + e) and output order (s = 2 (16 (L & 3) + (L >> 2)) + e), e = 0, 1
+        // window cosine seeds (c_0, c_1), c_r = cos(2 pi (s + 128 r - woff) / win), at the first sample
+        // of each lane: input order (s = 2 L + e), output order (s = 2 (16 (L & 3) + (L >> 2)) + e)
         std::vector<double2> wc(4 * 64);
         for (int L = 0; L < 64; ++L)
             for (int e = 0; e < 2; ++e) {
                 const int si = 2 * L + e, so = 2 * (16 * (L & 3) + (L >> 2)) + e;
                 const double ai = 2.0 * M_PI * (double)(si - g->g.woff) / cfg->win_length;
                 const double ao = 2.0 * M_PI * (double)(so - g->g.woff) / cfg->win_length;
-                wc[e * 64 + L] = double2{std::cos(ai), std::sin(ai)};
-                wc[(2 + e) * 64 + L] = double2{std::cos(ao), std::sin(ao)};
+                const double ar = 2.0 * M_PI * 128.0 / cfg->win_length;
+                wc[e * 64 + L] = double2{std::cos(ai), std::cos(ai + ar)};
+                wc[(2 + e) * 64 + L] = double2{std::cos(ao), std::cos(ao + ar)};
             }
-        const double ar = 2.0 * M_PI * 128.0 / cfg->win_length;
-        g->wrot = double2{std::cos(ar), std::sin(ar)};
+        g->wrot = 2.0 * std::cos(2.0 * M_PI * 128.0 / cfg->win_length);
         if ((e = hipMalloc(&g->winc, wc.size() * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
         if ((e = hipMemcpy(g->winc, wc.data(), wc.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e, "copy");
