@@ -501,8 +501,10 @@ def main():
             flops = GL_FLOPS_PER_FRAME_ITER * frames_total * (1 if dom == "gl_iter" else args.iters)
             tf = flops / (kdom["mean_ms"] * 1e-3) / 1e12
             roofline["diagnostics"] = dict(
-                limiter="fp64 VALU issue + LDS passes of the per-frame Stockham FFTs (workgroup barriers); "
-                        "HBM traffic is the fp64 |S| row and the fp64 windowed frames written and overlap-added",
+                limiter="batched: one wave per frame (gl_iter_wave_kernel), fp64 VALU (~65% busy) and the "
+                        "vector-memory return path (TD ~74% busy); small batches: the persistent loop's "
+                        "per-iteration neighbour hand-offs. HBM traffic is the fp64 |S| row and the fp64 "
+                        "windowed frames written and overlap-added",
                 fp64_flops_per_launch=flops, fp64_tflops=tf, fp64_vector_frac=tf / FP64_VECTOR_PEAK_TF,
                 traffic_gbs=(traffic / (kdom["mean_ms"] * 1e-3) / 1e9) if traffic else None)
         if dom == "resident_decoder":

@@ -27,7 +27,7 @@ LABELS = [
     (r"sgemm_kernel<\d+, 1, 3>", "dec_lstm"),
     (r"sgemm_kernel<\d+, 2, 5>", "mel_fused"),
     (r"sgemm_kernel<\d+, 3, 6>", "enc_lstm"),
-    (r"gl_iter_kernel<false", "gl_iter_frames"),
+    (r"gl_iter_kernel<false|gl_iter_wave_kernel", "gl_iter_frames"),
     (r"gl_iter_kernel<true", "gl_iter_init"),
     (r"gl_persistent_kernel", "gl_persistent"),
     (r"encoder_resident_kernel", "enc_lstm_resident"),
