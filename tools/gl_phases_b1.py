@@ -1,0 +1,12 @@
+import os, sys
+import numpy as np, torch
+sys.path.insert(0, "tests")
+from conftest import load_pkg
+audio = load_pkg("audio"); cfg = load_pkg("generic_utils").default_config("config_tacotron2.json")
+rng = np.random.Generator(np.random.PCG64(2))
+mel = torch.from_numpy(rng.uniform(0, 1, size=(1, 222, 80)).astype(np.float32)).cuda()
+ap = audio.AudioProcessor(**cfg.audio)
+for k in range(3):
+    ap.griffin_lim_batch(mel, [222], seed=3)
+torch.cuda.synchronize()
+print(ap.last_gl_path(), ap.last_gl_timing())
