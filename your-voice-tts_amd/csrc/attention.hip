@@ -157,6 +157,7 @@ __host__ __device__ static inline int red_stride(int Lcap) { return Lcap > ATT_T
 size_t attention_smem_bytes(int Lcap, int location) {
     size_t f = 2 * ADIM + 3 * (size_t)Lcap + ATT_WAVES * (size_t)red_stride(Lcap) + 4 * ATT_WAVES;
     if (location) f += 2 * ((size_t)Lcap + 32) + (size_t)NLOC * Lcap + ADIM * NLOC;
+    f += ATT_THREADS;  // attention_kernel's fused-query partials
     return f * sizeof(float);
 }
 
@@ -216,8 +217,25 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     const float u = a.forward_attn ? a.u[b] : 0.f;
     const float vb = a.v_b[0];
     float qv = 0.f;
-    if (tid < ADIM) qv = a.q[(int64_t)b * ADIM + tid];
-    else if (tid < 2 * ADIM) qv = a.v[tid - ADIM];
+    if (tid < ADIM && !a.wqT) qv = a.q[(int64_t)b * ADIM + tid];
+    else if (tid >= ADIM && tid < 2 * ADIM) qv = a.v[tid - ADIM];
+    // fused query_layer (common_layers.py:179; TacotronGST): thread (d = tid % 128, slice
+    // ks = tid / 128) sums k in [ks * KS, (ks + 1) * KS) of W_q[d][k] h_att[k] (coalesced rows of
+    // the transposed weight, h_att a broadcast read); the 8 partials meet in LDS in slice order
+    constexpr int QSL = ATT_THREADS / ADIM, KS = HATT_ / QSL;
+    float qpart = 0.f;
+    if (a.wqT) {
+        const int d = tid & (ADIM - 1), ks = tid / ADIM;
+        const float* w = a.wqT + (int64_t)ks * KS * ADIM + d;
+        const float* h = a.h_att + (int64_t)b * HATT_ + ks * KS;
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < KS; k += 2) {
+            s0 = fmaf(w[(int64_t)k * ADIM], h[k], s0);
+            s1 = fmaf(w[(int64_t)(k + 1) * ADIM], h[k + 1], s1);
+        }
+        qpart = s0 + s1;
+    }
     const float aold_j = (a.forward_attn && in) ? a.alpha[row + j] : 0.f;
     const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
     const int d0 = wave * DPW;
@@ -252,6 +270,20 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     float* locf = cat + 2 * (Lc + 32);
     float* wd = locf + NLOC * Lc;
 
+    if (a.wqT) {
+        // the partials go through their own scratch at the end of the allocation; slice sums in
+        // order 0..7
+        float* qsc = a.location_attn ? wd + ADIM * NLOC : cat;
+        qsc[tid] = qpart;
+        __syncthreads();
+        if (tid < ADIM) {
+            float sq = 0.f;
+#pragma unroll
+            for (int k = 0; k < QSL; ++k) sq += qsc[k * ADIM + tid];
+            qv = sq;
+        }
+        __syncthreads();
+    }
     if (tid < ADIM) q[tid] = qv;
     else if (tid < 2 * ADIM) vv[tid - ADIM] = qv;
     if (a.forward_attn && in) aold[j] = aold_j;
@@ -620,6 +652,19 @@ hipError_t launch_query_energy(const QEArgs& a, int B, hipStream_t s) {
 
 static size_t attention_fm_smem_bytes(int Lcap) {
     return ((size_t)Lcap + 2 * ATT_WAVES) * sizeof(float);
+}
+
+__global__ void transpose_f32_kernel(const float* src, int rows, int cols, float* dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)rows * cols) return;
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    dst[(int64_t)c * rows + r] = src[i];
+}
+
+hipError_t transpose_f32(const float* src, int rows, int cols, float* dst, hipStream_t s) {
+    const int64_t n = (int64_t)rows * cols;
+    hipLaunchKernelGGL(transpose_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, cols, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {

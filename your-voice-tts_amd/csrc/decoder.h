@@ -31,7 +31,9 @@ struct AttnArgs {
     const float* loc_conv; // [32][2][31]
     const float* loc_dense;// [128][32]
     // inputs
-    const float* q;        // [B][128] processed query
+    const float* q;        // [B][128] processed query (unused when wqT is set)
+    const float* wqT;      // attention_kernel: [HATT_][128] query_layer weight, transposed, or null:
+                           // then the kernel computes the processed query itself from h_att
     const float* Pt;       // [B][128][Lcap] processed inputs, transposed
     const float* enc;      // [B][Lcap][enc_dim]
     const int* lens;       // [B]
@@ -104,6 +106,7 @@ hipError_t launch_zero_tail(float* dst, int64_t ldb, const int* n_steps, int wid
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, hipStream_t s,
                                  int enc_dim = ENC);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
+hipError_t transpose_f32(const float* src, int rows, int cols, float* dst, hipStream_t s);  // dst[c][r] = src[r][c]
 size_t attention_smem_bytes(int Lcap, int location);
 hipError_t attention_prepare(int Lcap, int location);  // raise the dynamic-LDS limit once
 

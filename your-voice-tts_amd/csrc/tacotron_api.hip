@@ -82,6 +82,8 @@ struct tts_tacotron {
     float *W_go = nullptr, *b_go = nullptr;    // prenet L1 alone (step 0)
     float *W_p1s = nullptr, *b_p1s = nullptr;  // [prenet L1 | stopnet] over [mel out | decoder out]
     float *W_p2 = nullptr, *b_p2 = nullptr, *W_att = nullptr, *b_att = nullptr, *W_q = nullptr;
+    float* W_qT = nullptr;  // query_layer weight transposed [256][128]: the attention launch computes the query
+    bool fused_query = true;  // TTS_GST_FUSED_QUERY=0: the separate query GEMM launch (A/B)
     float *W_proj = nullptr, *b_proj = nullptr, *W_g[2] = {}, *b_g[2] = {}, *W_mel = nullptr, *b_mel = nullptr;
     float *v = nullptr, *v_b = nullptr, *ta_w = nullptr, *ta_b = nullptr, *loc_conv = nullptr, *loc_dense = nullptr;
     float *W_in = nullptr, *att_init = nullptr, *dec_init = nullptr, *mem_init = nullptr;
@@ -461,14 +463,18 @@ tts_status enqueue_step(tts_tacotron* t, int B, int Lmax, int max_steps, int p, 
         MARK();
         TTS_HIP(sgemm_launch(a, ROLE_T_ATT_GRU, s));
     }
-    {  // 3) processed query = query_layer(h_att_t) (common_layers.py:179)
-        SGemmArgs a = g;
-        a.seg[0] = Seg{h_att_cur, T_DEC, T_DEC};
-        a.nseg = 1;
-        a.W = t->W_q; a.K = T_DEC; a.N = ADIM;
-        a.out = t->q; a.ldo = ADIM;
+    {  // 3) processed query = query_layer(h_att_t) (common_layers.py:179): inside the attention
+        // launch (fused_query) or its own GEMM; the profiling mark stays so the per-kernel events
+        // keep their order (the fused query's time is in the attention interval)
         MARK();
-        TTS_HIP(sgemm_launch(a, ROLE_T_QUERY, s));
+        if (!t->fused_query) {
+            SGemmArgs a = g;
+            a.seg[0] = Seg{h_att_cur, T_DEC, T_DEC};
+            a.nseg = 1;
+            a.W = t->W_q; a.K = T_DEC; a.N = ADIM;
+            a.out = t->q; a.ldo = ADIM;
+            TTS_HIP(sgemm_launch(a, ROLE_T_QUERY, s));
+        }
     }
     {  // 4) attention (energies, norm, forward attention, context -> ctx_t), :371
         const tts_tacotron_config& c = t->cfg;
@@ -479,6 +485,7 @@ tts_status enqueue_step(tts_tacotron* t, int B, int Lmax, int max_steps, int p, 
         a.v = t->v; a.v_b = t->v_b; a.ta_w = t->ta_w; a.ta_b = t->ta_b;
         a.loc_conv = t->loc_conv; a.loc_dense = t->loc_dense;
         a.q = t->q; a.Pt = t->Pt; a.enc = t->denc; a.lens = t->lens;
+        a.wqT = t->fused_query ? t->W_qT : nullptr;
         a.h_att = h_att_cur;
         a.epart = t->epart;
         a.alpha = t->alpha; a.att_w = t->att_w; a.att_cum = t->att_cum; a.u = t->u; a.win_idx = t->win_idx;
@@ -707,6 +714,12 @@ tts_status create_weights(tts_tacotron* t, const WeightMap& wm, hipStream_t s) {
         GET(vw, "decoder.attention_layer.v.linear_layer.weight", ADIM);
         GET(vb, "decoder.attention_layer.v.linear_layer.bias", 1);
         CK(pack_linear(t, wq, ADIM, T_DEC, &t->W_q, s));
+        CK(talloc(t, &t->W_qT, (size_t)ADIM * T_DEC));
+        TTS_HIP(transpose_f32(wq, ADIM, T_DEC, t->W_qT, s));
+        {
+            const char* fq = getenv("TTS_GST_FUSED_QUERY");
+            t->fused_query = !(fq && fq[0] == '0');
+        }
         CK(copy_w(t, &t->W_in, win, ADIM * T_DEC, s));
         CK(copy_w(t, &t->v, vw, ADIM, s));
         CK(copy_w(t, &t->v_b, vb, 1, s));
