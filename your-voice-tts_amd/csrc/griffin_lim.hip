@@ -1170,8 +1170,11 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     // a persistent loop whose hand-off wait timed out left frames unwritten: never hand out a
     // plausible-looking waveform for it (the run's error status is raised when it is collected)
     const bool bad = a.status && *a.status != 0;
-    a.y[(int64_t)b * a.Nmax + p] =
-        bad ? __builtin_nanf("") : ola_sample(a.frames + (int64_t)b * a.Fmax * a.g.winp, p + NFFT / 2, Fb, a.g, a.c.win2);
+    // (contributor loads issued together when the geometry allows it: bitwise the same sum)
+    const double* fr = a.frames + (int64_t)b * a.Fmax * a.g.winp;
+    const float yv = (a.g.win + a.g.hop - 1) / a.g.hop <= OLA_MAX ? ola_sample_unrolled(fr, p + NFFT / 2, Fb, a.g, a.c.win2)
+                                                                  : ola_sample(fr, p + NFFT / 2, Fb, a.g, a.c.win2);
+    a.y[(int64_t)b * a.Nmax + p] = bad ? __builtin_nanf("") : yv;
 }
 
 // y[n] = x[n] + c*y[n-1] in float64 (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136).
