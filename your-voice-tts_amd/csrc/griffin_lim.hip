@@ -41,7 +41,9 @@ constexpr int SCAN_PER = 8;  // samples per thread per scan tile
 constexpr int SCAN_CHUNK = 4096;  // de-emphasis output samples per workgroup
 
 struct Geo {
-    int hop, win, woff, winp;  // woff = (NFFT - win) / 2, winp = win rounded up to 4
+    int hop, win, woff, winp;  // woff = (NFFT - win) / 2, winp = win + (woff - fb) rounded up to 4
+    int fb;                    // a frame slot holds samples [fb, fb + winp): fb = woff rounded down to
+                               // even, so sample pairs (2n, 2n+1) are 16-byte aligned
 };
 
 struct GLConst {
@@ -244,7 +246,7 @@ __device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q
     float y = 0.f, wss = 0.f;
     for (int i = ilo; i <= ihi; ++i) {
         const int o = q - i * g.hop;  // offset inside frame i (0..2047)
-        y = (float)((double)y + fr[(int64_t)i * g.winp + (o - g.woff)]);
+        y = (float)((double)y + fr[(int64_t)i * g.winp + (o - g.fb)]);
         wss = (float)((double)wss + win2[o]);
     }
     return wss > 1.17549435e-38f ? y / wss : y;
@@ -266,7 +268,7 @@ __device__ __forceinline__ float ola_sample_unrolled(const double* __restrict__ 
         const int i = ilo + k;
         const int o = q - i * g.hop;
         const bool ok = i <= ihi;
-        fv[k] = ok ? fr[(int64_t)i * g.winp + (o - g.woff)] : 0.0;
+        fv[k] = ok ? fr[(int64_t)i * g.winp + (o - g.fb)] : 0.0;
         wv[k] = ok ? win2[o] : 0.0;
     }
     float y = 0.f, wss = 0.f;
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i) - g.woff;
         const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-        if (n >= 0 && n < g.win) out[n] = wo[i] * (zv * (1.0 / NH));
+        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = wo[i] * (zv * (1.0 / NH));
     }
 }
 
@@ -898,9 +900,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // ---- inverse FFT; z'[n] -> real samples 2n, 2n + 1; window the support and store float64
     // (the frame's store range is its support: stores outside it are dropped by the range check)
     wave_fft1024<true>(v, lds, t2, rT, L);
-    // (samples 2 (16 r3 + K2) + 128 (j + 4 q1): the window by the same rotation, stores outside the
-    // support dropped by the frame's range)
-    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.win * 8);
+    // (samples 2 (16 r3 + K2) + 128 (j + 4 q1): the window by the same recurrence; each sample pair
+    // is one 16-byte store into the frame slot [fb, fb + winp), pairs outside the slot dropped by its
+    // range; the slot's one or two samples outside the support are never read)
+    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.winp * 8);
     __builtin_amdgcn_sched_barrier(0);
     const double2 s0 = buf_c64(rC, 16 * L, 2048), s1 = buf_c64(rC, 16 * L, 3072);
     double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
@@ -911,8 +914,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             const int s = 2 * (256 * q1 + 64 * j + 16 * r3 + K2);
             const double2 z = v[4 * j + q1];
             // (1/2 of the pre-split) x 1/NH: one exact power-of-two scale
-            buf_st_f64(fma(-0.5, a0, 0.5) * (z.x * (0.5 / NH)), rO, (s - g.woff) * 8);
-            buf_st_f64(fma(-0.5, b0, 0.5) * (z.y * (0.5 / NH)), rO, (s + 1 - g.woff) * 8);
+            const double2 o2 = double2{fma(-0.5, a0, 0.5) * (z.x * (0.5 / NH)), fma(-0.5, b0, 0.5) * (z.y * (0.5 / NH))};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o2), rO, (s - g.fb) * 8, 0, 0);
             const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
             a0 = a1;
             a1 = a2;
@@ -1009,7 +1012,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const int fi = ilo + k;
             const int o = q - fi * g.hop;
             const bool ok = any && fi <= ihi;
-            off[i][k] = ok ? fi * g.winp + (o - g.woff) : -1;
+            off[i][k] = ok ? fi * g.winp + (o - g.fb) : -1;
             wss = (float)((double)wss + (ok ? a.c.win2[o] : 0.0));
             if (ok) { flo = min(flo, fi); fhi = max(fhi, fi); }
         }
@@ -1132,7 +1135,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const int n = edge_sample(tid, i) - g.woff;
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
             if (n >= 0 && n < g.win)
-                __hip_atomic_store((gu64_t*)(dst + n),
+                __hip_atomic_store((gu64_t*)(dst + n + g.woff - g.fb),
                                    (unsigned long long)__double_as_longlong(wo[i] * (zv * (1.0 / NH))),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1413,7 +1416,8 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     g->g.hop = cfg->hop_length;
     g->g.win = cfg->win_length;
     g->g.woff = (NFFT - cfg->win_length) / 2;  // librosa util.pad_center
-    g->g.winp = (cfg->win_length + 3) / 4 * 4;
+    g->g.fb = g->g.woff & ~1;
+    g->g.winp = (cfg->win_length + (g->g.woff - g->g.fb) + 3) / 4 * 4;
     (void)stream;
     std::vector<double> win(NFFT, 0.0), win2(NFFT, 0.0);
     for (int n = 0; n < cfg->win_length; ++n) {
