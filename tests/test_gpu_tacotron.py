@@ -219,3 +219,29 @@ def test_style_wav_synthesis_vs_oracle(tmp_path):
     o = TacotronOracle(weights_mod().tacotron_gst_weights(0), dtype=np.float32, **fl)
     ref = o.encoder(ids, None, ref_mel.astype(np.float32).reshape(-1, 80))
     assert rel_rms(enc[0].cpu().numpy(), ref) < RTOL
+
+
+def test_fused_query_matches_separate_query_launch(monkeypatch):
+    """The TacotronGST step computes query_layer(h_att) inside the attention launch (transposed
+    weight, 8 k-slices summed in a fixed order); TTS_GST_FUSED_QUERY=0 keeps the separate GEMM
+    launch.  Both on a B=8 config-5-shaped batch (speakers, style mel): identical step counts and
+    stop decisions, spectrograms within 1e-5 relative RMS (fp32 summation order only)."""
+    w = weights_mod()
+    gu = load_pkg("generic_utils")
+    cfg = gu.default_config("config_tacotron_gst.json")
+    lens = w.synthetic_lengths(8, 4)
+    ids = [w.synthetic_ids(int(L), 300 + b) for b, L in enumerate(lens)]
+    style = torch.from_numpy(np.random.Generator(np.random.PCG64(8)).uniform(0, 1, size=(8, 200, 80)).astype(np.float32))
+    spk = [b % 4 for b in range(8)]
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TTS_GST_FUSED_QUERY", fused)
+        m = gu.setup_model(130, 4, cfg).cuda().eval()
+        m.decoder.max_decoder_steps = 120
+        outs.append(m.inference_batch(ids, speaker_ids=spk, style_mel=style))
+    a, b = outs
+    assert a["steps"] == b["steps"] and a["frames"] == b["frames"]
+    for b_ in range(8):
+        T = a["frames"][b_]
+        assert rel_rms(a["linear"][b_, :T].cpu().numpy(), b["linear"][b_, :T].cpu().numpy()) < 1e-5
+        assert rel_rms(a["mel"][b_, :T].cpu().numpy(), b["mel"][b_, :T].cpu().numpy()) < 1e-5
