@@ -19,13 +19,13 @@ import sys
 from collections import defaultdict
 
 LABELS = [
-    (r"sgemm_kernel<\d+, 0, 0>", "prenet2"),
-    (r"sgemm_kernel<\d+, 1, 1>", "att_lstm"),
+    (r"sgemm_kernel<\d+, 0, 0>|sgemm_frag16_kernel<0, 0>", "prenet2"),
+    (r"sgemm(?:_frag)?_kernel<\d+, 1, 1>", "att_lstm"),
     (r"sgemm_kernel<\d+, 0, 2>", "query"),
     (r"query_energy_kernel", "query"),
     (r"attention_kernel|attention_fm_kernel", "attention"),
-    (r"sgemm_kernel<\d+, 1, 3>", "dec_lstm"),
-    (r"sgemm_kernel<\d+, 2, 5>", "mel_fused"),
+    (r"sgemm(?:_frag)?_kernel<\d+, 1, 3>", "dec_lstm"),
+    (r"sgemm_kernel<\d+, 2, 5>|sgemm_frag16_kernel<2, 5>", "mel_fused"),
     (r"sgemm_kernel<\d+, 3, 6>", "enc_lstm"),
     (r"gl_iter_kernel<false|gl_iter_wave_kernel", "gl_iter_frames"),
     (r"gl_iter_kernel<true", "gl_iter_init"),
