@@ -222,3 +222,30 @@ def test_griffin_lim_wave_kernel_ragged_vs_oracle(audio_cfg, monkeypatch):
         assert rel_rms(wav[b, :n], ref) < WAV_RTOL, (b, F)
         assert rel_rms(wav[b, :n], wav_block[b, :n]) < WAV_RTOL, (b, F)
         assert np.all(wav[b, n:] == 0)
+
+
+def test_overlap_add_launch_bitwise_vs_in_kernel_gather(audio_cfg, monkeypatch):
+    """gl_ola_kernel takes the window sum-square of samples with every contributor present from a
+    per-(u mod hop) table summed on the host; the fused block kernel sums win^2 per sample itself
+    (ola_sample_unrolled). With the block kernel on both sides (TTS_GL_WAVE=0) the unfused loop
+    (overlap-add launch + iteration launch) and the forced in-kernel gather (TTS_GL_FUSED=1) must
+    give bitwise the same waveform on a ragged batch, edges and reflected short sentences included."""
+    audio = load_pkg("audio")
+    rng = np.random.Generator(np.random.PCG64(12))
+    Fs = [2, 4, 6, 300, 41, 290, 9, 130]
+    Fmax = max(Fs)
+    mel = np.zeros((len(Fs), Fmax, 80), np.float32)
+    pu = np.zeros((len(Fs), 1025, Fmax))
+    for b, F in enumerate(Fs):
+        mel[b, :F] = rng.uniform(0, 1, size=(F, 80))
+        pu[b, :, :F] = rng.uniform(0, 1, size=(1025, F))
+    mel_d = torch.from_numpy(mel).cuda()
+    monkeypatch.setenv("TTS_GL_WAVE", "0")
+    ap = audio.AudioProcessor(**audio_cfg)
+    wav = ap.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    assert ap.last_gl_path() == "unfused"
+    monkeypatch.setenv("TTS_GL_FUSED", "1")
+    ap_f = audio.AudioProcessor(**audio_cfg)
+    wav_f = ap_f.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    assert ap_f.last_gl_path() == "fused"
+    assert np.array_equal(wav, wav_f)

@@ -1162,6 +1162,8 @@ struct FinArgs {
     float* y;  // [B][Nmax]
     int64_t Nmax;
     const int* status;  // the persistent loop's status word, or null: nonzero poisons the signal (NaN)
+    const float* wssp;  // [hop] float32 window sum-square of a sample whose every contributing frame
+                        // exists, by (q - woff) mod hop (summed on the host in ola_sample's order)
 };
 
 __global__ void gl_ola_kernel(const FinArgs a) {
@@ -1173,10 +1175,38 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     // a persistent loop whose hand-off wait timed out left frames unwritten: never hand out a
     // plausible-looking waveform for it (the run's error status is raised when it is collected)
     const bool bad = a.status && *a.status != 0;
-    // (contributor loads issued together when the geometry allows it: bitwise the same sum)
+    // (contributor loads issued together when the geometry allows it: bitwise the same sum; the
+    // window sum-square from the periodic table where no contributor is clipped, as ola_sample
+    // would sum it, else summed here)
     const double* fr = a.frames + (int64_t)b * a.Fmax * a.g.winp;
-    const float yv = (a.g.win + a.g.hop - 1) / a.g.hop <= OLA_MAX ? ola_sample_unrolled(fr, p + NFFT / 2, Fb, a.g, a.c.win2)
-                                                                  : ola_sample(fr, p + NFFT / 2, Fb, a.g, a.c.win2);
+    const Geo& g = a.g;
+    const int q = p + NFFT / 2;
+    float yv;
+    if ((g.win + g.hop - 1) / g.hop <= OLA_MAX && q >= g.woff) {
+        const int u = q - g.woff;
+        const int ihu = u / g.hop;
+        int ilo = u - g.win + 1;
+        const bool full = ilo >= 1 && ihu <= Fb - 1;
+        ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
+        const int ihi = ihu > Fb - 1 ? Fb - 1 : ihu;
+        double fv[OLA_MAX];
+#pragma unroll
+        for (int k = 0; k < OLA_MAX; ++k) {
+            const int i = ilo + k;
+            fv[k] = i <= ihi ? fr[(int64_t)i * g.winp + (q - i * g.hop - g.fb)] : 0.0;
+        }
+        float y = 0.f, wss = 0.f;
+#pragma unroll
+        for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + fv[k]);
+        if (full) {
+            wss = a.wssp[u - ihu * g.hop];
+        } else {
+            for (int i = ilo; i <= ihi; ++i) wss = (float)((double)wss + a.c.win2[q - i * g.hop]);
+        }
+        yv = wss > 1.17549435e-38f ? y / wss : y;
+    } else {
+        yv = ola_sample(fr, q, Fb, g, a.c.win2);
+    }
     a.y[(int64_t)b * a.Nmax + p] = bad ? __builtin_nanf("") : yv;
 }
 
@@ -1357,6 +1387,7 @@ struct tts_gl {
     double2* tw = nullptr;
     double2* wt = nullptr;  // gl_iter_wave_kernel pass-2 twiddles [16][4]
     double2* winc = nullptr;  // gl_iter_wave_kernel window rotation bases [4][64]
+    float* wssp = nullptr;    // gl_ola_kernel periodic window sum-square [hop]
     double wrot = 0.0;
     bool wave = true;       // batched iterations on gl_iter_wave_kernel (TTS_GL_WAVE=0: gl_iter_kernel)
     // workspace
@@ -1395,7 +1426,8 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt, (void*)g->winc})
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt, (void*)g->winc,
+                    (void*)g->wssp})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
     for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done})
@@ -1474,6 +1506,21 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
         if ((e = hipMemcpy(g->winc, wc.data(), wc.size() * sizeof(double2), hipMemcpyHostToDevice)) != hipSuccess)
             return fail(e, "copy");
         g->wave = !getenv_off("TTS_GL_WAVE");
+        // window sum-square of a sample q (u = q - woff) with every contributor present: frames
+        // i = ceil((u - win + 1) / hop) .. floor(u / hop) in index order, float32 additions of the
+        // float64 win^2 as ola_sample makes them; depends on u mod hop only
+        const int hop = cfg->hop_length, wl = cfg->win_length;
+        std::vector<float> wp(hop);
+        for (int r = 0; r < hop; ++r) {
+            const int u = r + hop * (wl / hop + 1);
+            const int ilo = (u - wl + 1 + hop - 1) / hop, ihi = u / hop;
+            float w = 0.f;
+            for (int i = ilo; i <= ihi; ++i) w = (float)((double)w + win2[g->g.woff + u - i * hop]);
+            wp[r] = w;
+        }
+        if ((e = hipMalloc(&g->wssp, hop * sizeof(float))) != hipSuccess) return fail(e, "hipMalloc");
+        if ((e = hipMemcpy(g->wssp, wp.data(), hop * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+            return fail(e, "copy");
     }
     if (inv_mel_basis) {
         const size_t n = (size_t)NB * cfg->num_mels;
@@ -1648,6 +1695,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     fa.c = ia.c;
     fa.y = g->y;
     fa.Nmax = Nmax;
+    fa.wssp = g->wssp;
     const dim3 ogrid((Nmax + 255) / 256, B), oblock(256);
     bool persistent_ran = false;
     if (persistent) {
