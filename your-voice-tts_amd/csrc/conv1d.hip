@@ -8,8 +8,8 @@
 // then each wave issues v_mfma_f32_16x16x4_f32 on its (BM/WM) x (64/WN) sub-tile.  For KW <= 5
 // one accumulator set per tap keeps the fp32 fma chains short (Cin long instead of KW*Cin); the
 // long CBHG bank slabs (KW 8 / 16) accumulate every tap into one set (register budget).  Two tile
-// shapes: BM=64 (2x2 waves of 32x32) for large batches, BM=16 (1x4 waves of 16x16) so that a single
-// sentence still spreads over >= 100 workgroups.
+// shapes: BM=64 (2x2 waves of 32x32) for large batches (BM=32, 2x2 waves of 16x32, for the KW=5
+// convs), BM=16 (1x4 waves of 16x16) so that a single sentence still spreads over >= 100 workgroups.
 #include "conv1d.h"
 
 namespace tts {
@@ -290,6 +290,12 @@ hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
     if (frames_hint <= 4096) {
         const dim3 grid(((Tt + 15) / 16) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4>), grid, block, 0, s, a);
+    } else if (KW == 5) {
+        // the Tacotron2 encoder / postnet convs (sentences of 60-1000 frames): 32-frame tiles halve
+        // the last tile's padding rows; measured -0.3 ms per configs[2] batch (the KW 1 / 3 / 8 / 16
+        // CBHG launches of configs[4] measured slower with them and keep 64)
+        const dim3 grid(((Tt + 31) / 32) * (a.co_pad / CONV_BN) * B);
+        hipLaunchKernelGGL((conv_kernel<KW, 32, 2, 2>), grid, block, 0, s, a);
     } else {
         const dim3 grid(((Tt + 63) / 64) * (a.co_pad / CONV_BN) * B);
         hipLaunchKernelGGL((conv_kernel<KW, 64, 2, 2>), grid, block, 0, s, a);
