@@ -120,24 +120,38 @@ def build(args, device):
     return cfg, model, ap
 
 
-def make_job(args, world, rank, max_steps):
+def make_job(args, world, rank, max_steps, model=None, batch=None, lengths=None, seed=None):
     """The whole job's sentences (world x batch) and this rank's LPT share (sharding.py)."""
-    n = world * args.batch
-    if args.model == "gst":
+    model = args.model if model is None else model
+    batch = args.batch if batch is None else batch
+    lengths = args.lengths if lengths is None else lengths
+    n = world * batch
+    if model == "gst":
         # configs[4]: L ~ U{60..160} (seed 4); every sentence costs up to the 500-step cap
         lens = weights.synthetic_lengths(n, 4)
         ids = [weights.synthetic_ids(int(L), 200 + b) for b, L in enumerate(lens)]
-        mine = sharding.lpt_partition([len(x) for x in ids], world, capacity=args.batch)[rank]
+        mine = sharding.lpt_partition([len(x) for x in ids], world, capacity=batch)[rank]
         return ids, mine
-    if args.lengths == "fixed":
+    if lengths == "fixed":
         ids = [weights.synthetic_ids(args.L, 1) for _ in range(n)]  # configs[1]: L=100, seed 1
     else:
         # configs[2] (B=64, seed 2) on one GPU; configs[3] (B=512 over 8 GPUs, seed 3) otherwise
-        lens = weights.synthetic_lengths(n, 2 if world == 1 else 3)
+        if seed is None:
+            seed = 2 if world == 1 else 3
+        lens = weights.synthetic_lengths(n, seed)
         ids = [weights.synthetic_ids(int(L), 100 + b) for b, L in enumerate(lens)]
     costs = [sharding.sentence_cost(len(x), max_steps) for x in ids]
-    mine = sharding.lpt_partition(costs, world, capacity=args.batch)[rank]
+    mine = sharding.lpt_partition(costs, world, capacity=batch)[rank]
     return ids, mine
+
+
+CONFIGS3_WORLD = 8  # BASELINE configs[3]: 512 sentences over 8 GPUs, 64 per rank
+
+
+def configs3_share(args, max_steps):
+    """Rank 0's LPT share of the configs[3] job (512 seed-3 sentences over 8 ranks, 64 each): the
+    per-rank workload of the driver's 8-GPU run, which the N=1 line times on one GPU too."""
+    return make_job(args, CONFIGS3_WORLD, 0, max_steps, model="tacotron2", batch=64, lengths="uniform", seed=3)
 
 
 _STYLE = {}
@@ -169,6 +183,14 @@ def run_step(model, ap, ids, mine, world, seed):
         rows = [wav[k, :ap.hop_length * (T - 1)] for k, T in enumerate(out["frames"])]
         sharding.gather_waveforms(rows, mine, len(ids))
     return out["frames"], wav
+
+
+def collect_status(model):
+    """The timed loop pipelines tts_synth_run (sync=False): the LAST call's Griffin-Lim status is
+    only collected by tts_synth_sync (a device synchronize does not read it).  Raise if it failed,
+    so a timed-out persistent loop can never hide inside a published measurement."""
+    if hasattr(model, "synth_sync"):
+        model.synth_sync()
 
 
 def _cpu_model():
@@ -325,25 +347,75 @@ def proxy_main(args, world, rank):
     all_ids, mine = make_job(args, world, rank, 1000)
     hop = 275
 
-    def step(seed):
-        frames = [sharding.sentence_cost(len(all_ids[i]), 1000) for i in mine]
-        rows = [torch.from_numpy(np.random.Generator(np.random.PCG64(i)).standard_normal(hop * (T - 1)))
-                for i, T in zip(mine, frames)]
-        if world > 1:
-            sharding.gather_waveforms(rows, mine, len(all_ids))
-        return frames
+    def make_step(ids, share, w):
+        def step(seed):
+            frames = [sharding.sentence_cost(len(ids[i]), 1000) for i in share]
+            rows = [torch.from_numpy(np.random.Generator(np.random.PCG64(i)).standard_normal(hop * (T - 1)))
+                    for i, T in zip(share, frames)]
+            if w > 1:
+                sharding.gather_waveforms(rows, share, len(ids))
+            return frames
+        return step
 
-    tm = timed_region(step, args, world, cpu, hop, 22050)
+    ref = single_rank_reference(make_step(all_ids, mine, 1), args, world, rank, cpu, hop, 22050)
+    tm = timed_region(make_step(all_ids, mine, world), args, world, cpu, hop, 22050)
+    share = None
+    if world == 1 and args.model != "gst":
+        ids8, mine8 = configs3_share(args, 1000)
+        share = share_record(timed_region(make_step(ids8, mine8, 1), args, 1, cpu, hop, 22050), len(mine8))
     if rank == 0:
-        print(json.dumps({"metric": "proxy (launcher rehearsal, not a measurement)", "value": tm["value"],
-                          "unit": "mel-frames/s", "n_gpus": world,
-                          "world_size_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": tm["ms_per_step"], "proxy": True,
-                          "config": {"sentences_per_gpu": args.batch, "sentences_total": len(all_ids),
-                                     "frames_per_step": tm["frames_per_step"], "lengths": args.lengths}}))
+        rec = {"metric": "proxy (launcher rehearsal, not a measurement)", "value": tm["value"],
+               "unit": "mel-frames/s", "n_gpus": world,
+               "world_size_seen": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": tm["ms_per_step"], "proxy": True,
+               "config": {"sentences_per_gpu": args.batch, "sentences_total": len(all_ids),
+                          "frames_per_step": tm["frames_per_step"], "lengths": args.lengths}}
+        rec.update(scaling_keys(tm, ref, world, share))
+        print(json.dumps(rec))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def single_rank_reference(step, args, world, rank, device, hop, sr):
+    """N > 1: rank 0 times its own share ALONE (the same synthesis, no gather) while every other rank
+    waits at a barrier, before the collective timed region: the single-GPU point of this very
+    per-rank workload, so the line carries its own weak-scaling reference.  None at N = 1 or on
+    ranks > 0."""
+    if world == 1:
+        return None
+    dist.barrier()
+    ref = None
+    if rank == 0:
+        ref = timed_region(step, args, 1, device, hop, sr)
+    dist.barrier()
+    return ref
+
+
+def share_record(tm, n_sentences=None):
+    d = dict(value=tm["value"], unit="mel-frames/s", ms_per_step=tm["ms_per_step"],
+             frames_per_step=tm["frames_per_step"], rtf=tm["rtf"])
+    if n_sentences is not None:
+        d["sentences"] = n_sentences
+    return d
+
+
+def scaling_keys(tm, ref, world, share):
+    """Keys that make the 1/2/4/8-GPU records comparable: at N > 1
+    ``scaling_ref_1rank`` (rank 0's share timed alone on one GPU) and ``efficiency`` =
+    value / (N x scaling_ref_1rank); at N = 1 ``configs3_share_1rank`` (rank 0's share of the
+    8-GPU configs[3] job on this one GPU), beside the configs[1] headline."""
+    out = {}
+    if ref is not None:
+        r = share_record(ref)
+        r["note"] = "rank 0's share of this job, timed alone on one GPU before the collective region (no gather)"
+        out["scaling_ref_1rank"] = r
+        out["efficiency"] = tm["value"] / (world * ref["value"])
+    if share is not None:
+        share["note"] = ("rank 0's LPT share of configs[3] (512 seed-3 sentences over 8 GPUs) on this one GPU: "
+                         "the per-rank workload of the N=8 line")
+        out["configs3_share_1rank"] = share
+    return out
 
 
 def _free_port():
@@ -379,6 +451,8 @@ def parse_args(argv=None):
     ap_.add_argument("--iters", type=int, default=60)
     ap_.add_argument("--no-cpu-baseline", action="store_true")
     ap_.add_argument("--no-profile", action="store_true")
+    ap_.add_argument("--no-share", action="store_true",
+                     help="N=1: skip the configs[3]-share region (configs3_share_1rank)")
     ap_.add_argument("--model", choices=["tacotron2", "gst"], default="tacotron2")
     ap_.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                      help="gloo + --proxy: CPU rehearsal of the launcher / partition / gather (no GPU)")
@@ -414,8 +488,14 @@ def main():
     all_ids, mine = make_job(args, world, rank, model.decoder.max_decoder_steps)
     ids = [all_ids[i] for i in mine]
 
+    # N > 1: rank 0's share alone first (same synthesis, no gather; the other ranks wait)
+    ref = single_rank_reference(lambda seed: run_step(model, ap, all_ids, mine, 1, seed=seed)[0], args, world, rank,
+                                device, ap.hop_length, ap.sample_rate)
+    if ref is not None:
+        collect_status(model)
     timing = timed_region(lambda seed: run_step(model, ap, all_ids, mine, world, seed=seed)[0], args, world, device,
                           ap.hop_length, ap.sample_rate)
+    collect_status(model)
     elapsed, frames_per_step, ms_per_step, value, rtf = (timing[k] for k in ("elapsed", "frames_per_step",
                                                                            "ms_per_step", "value", "rtf"))
 
@@ -520,9 +600,23 @@ def main():
                 fp32_compute_frac=flops / (dec_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF,
                 device_wide_edges_us_per_step=edges, handoff_floor_us_per_step=sum(edges.values()),
                 us_per_step=us, handoff_share_of_step=sum(edges.values()) / us)
+    # the headline workload's paths, before any other region runs on the same handles
+    paths = dict(decoder=("resident" if model.last_timing.get("resident") else "multi-launch") if not gst
+                 else "multi-launch",
+                 encoder_bilstm=("resident" if model.last_timing.get("encoder_resident") else "per-step")
+                 if not gst else "per-step",
+                 griffin_lim=ap.last_gl_path())
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+    share = None
+    if world == 1 and not gst and not args.no_share:
+        # the driver's N=8 line runs configs[3]'s 64-sentence share per rank: time that same share
+        # here on one GPU (after the headline and its profile, which keep their batch-1 handles)
+        ids8, mine8 = configs3_share(args, model.decoder.max_decoder_steps)
+        share = share_record(timed_region(lambda seed: run_step(model, ap, ids8, mine8, 1, seed=seed)[0], args, 1,
+                                          device, ap.hop_length, ap.sample_rate), len(mine8))
+        collect_status(model)
 
     if gst:
         workload = (f"configs[4]: TacotronGST batch={args.batch} per GPU, L ~ U{{60..160}}, style mel [B,200,80], "
@@ -536,11 +630,6 @@ def main():
         workload = f"configs[2]: Tacotron2 batch=64, L ~ U{{60..160}} (seed 2), GL {args.iters} iters"
     else:
         workload = f"Tacotron2 batch={args.batch} per GPU, {args.lengths} lengths"
-    paths = dict(decoder=("resident" if model.last_timing.get("resident") else "multi-launch") if not gst
-                 else "multi-launch",
-                 encoder_bilstm=("resident" if model.last_timing.get("encoder_resident") else "per-step")
-                 if not gst else "per-step",
-                 griffin_lim=ap.last_gl_path())
     rec = {
         "metric": ("mel-frames/sec + RTF, TacotronGST + 60-iter Griffin-Lim (configs[4])" if gst else
                    "mel-frames/sec + RTF, Tacotron2 + 60-iter Griffin-Lim, LJSpeech"),
@@ -571,6 +660,7 @@ def main():
         "paths_rank0": paths,
         "kernels_rank0": kernels,
     }
+    rec.update(scaling_keys(timing, ref, world, share))
     print(json.dumps(rec))
     if world > 1:
         dist.barrier()

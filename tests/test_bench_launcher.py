@@ -37,6 +37,15 @@ def test_launcher_spawns_n_ranks_with_configs3_default(n):
     w = load_pkg("weights")
     lens = w.synthetic_lengths(64 * n, 3)
     assert rec["config"]["frames_per_step"] == sum(2 * int(L) + 22 for L in lens)
+    # the line carries its own single-GPU point of the same per-rank workload (rank 0's share)
+    sh = load_pkg("sharding")
+    costs = [2 * int(L) + 22 for L in lens]
+    share0 = sh.lpt_partition(costs, n, capacity=64)[0]
+    ref = rec["scaling_ref_1rank"]
+    assert ref["frames_per_step"] == sum(costs[i] for i in share0)
+    assert ref["value"] > 0 and ref["ms_per_step"] > 0
+    assert abs(rec["efficiency"] - rec["value"] / (n * ref["value"])) < 1e-9 * rec["efficiency"]
+    assert "configs3_share_1rank" not in rec
 
 
 def test_launcher_single_rank_default_is_configs1():
@@ -44,6 +53,15 @@ def test_launcher_single_rank_default_is_configs1():
     assert rec["n_gpus"] == 1 and rec["world_size_seen"] == 1
     assert rec["config"]["sentences_per_gpu"] == 1 and rec["config"]["lengths"] == "fixed"
     assert rec["config"]["frames_per_step"] == 222  # L = 100 -> 2L + 22
+    # ... plus the N=8 line's per-rank workload on this one GPU: rank 0's share of configs[3]
+    from conftest import load_pkg
+    sh = load_pkg("sharding")
+    lens = load_pkg("weights").synthetic_lengths(512, 3)
+    costs = [2 * int(L) + 22 for L in lens]
+    share0 = sh.lpt_partition(costs, 8, capacity=64)[0]
+    share = rec["configs3_share_1rank"]
+    assert share["sentences"] == 64 and share["frames_per_step"] == sum(costs[i] for i in share0)
+    assert "scaling_ref_1rank" not in rec and "efficiency" not in rec
 
 
 def test_world_size_mismatch_is_refused():

@@ -137,6 +137,40 @@ def test_config4_gst_batch32_linear_unfused_griffin_lim_vs_oracle():
         assert np.all(wav[b, nb:] == 0)
 
 
+def test_config4_gst_batch32_full_cap_linear_griffin_lim_vs_oracle():
+    """configs[4] exactly as benched: TacotronGST B=32 at the real 500-step cap (r=5: up to 2505
+    frames, the length where the bench spends 88% of its Griffin-Lim frames, beyond anything the
+    60-step test reaches), linear GL 60 iterations with device phases (seed 17).  The longest
+    sentence's waveform vs the oracle's inv_spectrogram of the GPU linear output on the restated
+    device phases at 1e-4; every sentence finite and zero past its own length."""
+    w = weights_mod()
+    gu = load_pkg("generic_utils")
+    audio = load_pkg("audio")
+    cfg = gu.default_config("config_tacotron_gst.json")
+    m = gu.setup_model(130, 4, cfg, max_batch=32, max_len=256).cuda().eval()
+    assert m.decoder.max_decoder_steps == 500  # layers/tacotron.py:278
+    lens = w.synthetic_lengths(32, 4)
+    ids = [w.synthetic_ids(int(L), 200 + b) for b, L in enumerate(lens)]
+    rng = np.random.Generator(np.random.PCG64(4))
+    style = torch.from_numpy(rng.uniform(0, 1, size=(32, 200, 80)).astype(np.float32)).cuda()
+    out = m.inference_batch(ids, speaker_ids=[b % 4 for b in range(32)], style_mel=style)
+    frames = out["frames"]
+    assert max(frames) > 2048
+    ap = audio.AudioProcessor(**cfg.audio)
+    wav = ap.griffin_lim_batch(out["linear"], frames, mode=audio._native.TTS_GL_FROM_LINEAR, seed=17)
+    assert ap.last_gl_path() == "unfused" and ap.last_gl_timing()["gl_iterations"] == 2 * 60
+    wav = wav.cpu().numpy()
+    assert np.isfinite(wav).all()
+    for b, T in enumerate(frames):
+        assert np.all(wav[b, ap.hop_length * (T - 1):] == 0), b
+    b = int(np.argmax(frames))
+    T = frames[b]
+    lin = out["linear"][b, :T].cpu().numpy()
+    ref = AudioOracle(**cfg.audio).inv_spectrogram(lin.T, device_phase_u(17, b, T))
+    nb = ap.hop_length * (T - 1)
+    assert rel_rms(wav[b, :nb], ref) < WAV_RTOL, (b, T)
+
+
 def test_synthesizer_tts_vs_oracle_chain(audio_cfg):
     """Synthesizer.tts (server/synthesizer.py:128-162) on a 3-sentence text with the reference's
     numpy phases: split, drop len < 3, per-sentence Tacotron2 (cap 3000) + GL in order, 10 000-zero

@@ -116,3 +116,24 @@ def test_synthesize_native_timeout_surfaces(audio_cfg):
             m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
         wav, _ = m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
         assert torch.isfinite(wav).all()
+
+
+def test_resident_decoder_timeout_reruns_multilaunch():
+    """Fault injection: every hand-off wait of the resident decoder times out at once
+    (TTS_DEC_WAIT_TICKS=1), as when a workgroup cannot become resident beside another stream's work.
+    The call must not fail: the sentence re-runs from its initial state on the multi-launch path,
+    bitwise that path's output; the next call on a normal handle is resident again."""
+    z = golden("t2_fwdmask_L100")
+    L = len(z["ids"])
+    enc = _t2().encode(torch.from_numpy(z["ids"]).view(1, -1).cuda(), [L])  # one encoder output for all
+    with _env(TTS_RESIDENT=0):
+        want = _t2().inference_batch(None, enc=enc, lens=[L])
+    with _env(TTS_DEC_WAIT_TICKS=1):
+        m = _t2()
+        got = m.inference_batch(None, enc=enc, lens=[L])
+        assert not m.last_timing["resident"], "no timeout was injected"
+    for k in ("mel", "mel_post", "align", "stop"):
+        assert torch.equal(got[k], want[k]), k
+    m2 = _t2()
+    again = m2.inference_batch(None, enc=enc, lens=[L])
+    assert m2.last_timing["resident"] and again["frames"] == want["frames"] == [z["mel"].shape[0]]

@@ -321,6 +321,58 @@ def test_synthesize_native_back_to_back(audio_cfg):
         assert torch.equal(wav, ref), k
 
 
+def test_synthesize_native_pipelined_cross_stream(audio_cfg):
+    """sync=False back to back across the cross-stream path: jobs above 256 frames run Griffin-Lim on
+    the synth handle's second stream while the next call's encoder / decoder / postnet run (batch-1
+    ones on the resident decoder), the stage buffers alternate by call parity; small jobs in between
+    take the same-stream persistent Griffin-Lim.  Every waveform, cloned on the caller's stream right
+    after its call, is bitwise inference_batch + griffin_lim_batch at the same seed."""
+    w = weights_mod()
+    z = {c: golden(c)["ids"] for c in ("t2_fwdmask_L100", "t2_fwdmask_L12", "t2_fwdmask_L40")}
+    z["L150"] = w.synthetic_ids(150, 7)
+    z["L140"] = w.synthetic_ids(140, 8)
+    m = _model(golden_flags(golden("t2_fwdmask_L100")))
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
+    seq = [["L150"], ["L140"], ["t2_fwdmask_L100"] * 3, ["t2_fwdmask_L12"], ["L150", "t2_fwdmask_L40"],
+           ["L140"], ["t2_fwdmask_L12"]]
+    outs = []
+    for k, cases in enumerate(seq):
+        wav, frames = m.synthesize_native([z[c] for c in cases], ap, seed=50 + k, sync=False)
+        outs.append((wav.clone(), frames))
+    m.synth_sync()
+    assert sum(outs[0][1]) > 256 and sum(outs[2][1]) > 256 and sum(outs[3][1]) <= 256
+    for k, cases in enumerate(seq):
+        ids = [z[c] for c in cases]
+        out = m.inference_batch(ids)
+        ref = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=50 + k)
+        wav, frames = outs[k]
+        assert frames == out["frames"], k
+        assert torch.equal(wav, ref), k
+
+
+@pytest.mark.parametrize("cap", [30, 31, 33, 40, 60])
+def test_synthesize_native_stop_near_cap(audio_cfg, cap):
+    """The stop rule fires within 20 steps of max_decoder_steps (the `elif` cap of
+    layers/tacotron2.py:271-277 is skipped once every stop flag is set, so the decoder may run up to
+    max_steps + 20 steps): tts_synth_run's waveform buffer holds those frames, the frame count is the
+    oracle's at the same cap, and the waveform is bitwise the staged path."""
+    z = golden("t2_nomask_L12")
+    fl = dict(golden_flags(z), max_decoder_steps=cap)
+    m = _model(fl)
+    ap = load_pkg("audio").AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 4})
+    o = Tacotron2Oracle(weights_mod().tacotron2_weights(0), dtype=np.float32, **fl)
+    T = o.inference(z["ids"])["mel"].shape[0]
+    wav, frames = m.synthesize_native([z["ids"]], ap, seed=3)
+    assert frames == [T]
+    out = m.inference_batch([z["ids"]])
+    ref = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=3)
+    assert out["frames"] == [T] and torch.equal(wav, ref)
+    # every flag is set from step 30 on: a cap of 30 ends the loop there, any later cap lets the
+    # stop count run to 51 frames (31 + 20: the widest overshoot at cap 31)
+    assert T == (30 if cap == 30 else 51)
+
+
 TF_CASES = ["tf_fwdmask_L12", "tf_loc_softmax_L20", "tf_win_fwdmask_L16"]
 
 

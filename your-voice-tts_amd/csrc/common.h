@@ -30,24 +30,28 @@ tts_status hip_fail(hipError_t e, const char* what, const char* file, int line);
 // completion checks that would block the host (encoder placement status, Griffin-Lim timing and
 // status) pending for the pipeline to collect at its next synchronisation point.
 void encoder_set_pipeline(tts_encoder* e, bool on);
-// *placement_failed = 1: the resident encoder could not be placed (rerun with per-step launches)
+// *placement_failed = 1: the resident encoder could not be placed, or one of its hand-off waits
+// timed out: the caller reruns the encoder (with per-step launches)
 tts_status encoder_pending_status(tts_encoder* e, int* placement_failed);
 void decoder_set_pipeline(tts_decoder* d, bool on);
 void gl_set_pipeline(tts_gl* g, bool on);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 
 // Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent
-// Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This launches
-// `fn` so that co-residency is GUARANTEED or nothing runs: an occupancy check of the grid against the
-// device's CUs (optionally capped by the TTS_CU_CAP environment variable, which tests use to force
-// the fallback), then hipLaunchCooperativeKernel, whose runtime refuses a grid that cannot be
-// co-resident.  *launched = false (and hipSuccess) when the grid cannot be co-resident: the caller
-// takes its multi-launch path.  TTS_COOP=0 launches plainly after the same check (A/B measurement).
+// Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This checks
+// the grid against the device's occupancy (the kernel's workgroups per CU x CUs, the CU count
+// optionally capped by the TTS_CU_CAP environment variable, which tests use to force the fallback)
+// and, if it fits, launches `fn` with a PLAIN hipLaunchKernel by default: the check does not
+// guarantee co-residency when other work occupies CUs, so correctness rests on the kernels' bounded
+// waits plus their status word (the decoder / encoder then rerun multi-launch, the persistent
+// Griffin-Lim raises with a NaN waveform).  TTS_COOP=1 uses hipLaunchCooperativeKernel instead
+// (≈30 µs more per launch).  *launched = false (and hipSuccess) when the grid cannot fit: nothing
+// ran and the caller takes its multi-launch path.
 hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args, size_t smem, hipStream_t s,
                              bool* launched);
-// the CU count launch_persistent plans with (device CUs, capped by TTS_CU_CAP)
 // rows [B][K] (row stride ld) -> their fragment-order mirror (frag_idx, ntf m-tiles)
 hipError_t frag_mirror(const float* src, int64_t ld, int B, int K, float* dst, int ntf, hipStream_t s);
+// the CU count launch_persistent plans with (device CUs, capped by TTS_CU_CAP)
 int usable_cus();
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));

@@ -74,6 +74,7 @@ struct tts_decoder {
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
     int last_resident = 0;    // the last run used the resident decoder
+    int res_timeouts = 0;     // resident runs that timed out a hand-off and re-ran multi-launch
     ResArgs last_ra{};
     InitArgs last_init{};
 };
@@ -399,6 +400,8 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
             resident_prepare() == hipSuccess) {
             d->resident = true;
             d->res_ticks = (long long)rate_khz * 50;  // 50 ms per hand-off wait
+            // fault injection for the timeout fallback test (TTS_DEC_WAIT_TICKS wall-clock ticks)
+            if (const char* tk = getenv("TTS_DEC_WAIT_TICKS"); tk && tk[0]) d->res_ticks = std::max(1LL, atoll(tk));
         }
     }
     CK(dmalloc(d, &d->W_pre1, sgemm_packed_floats(PRE, nmel)));
@@ -692,6 +695,17 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             d->resident = false;
             TTS_HIP(launch_decoder_init(ia, s));
             if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+        } else if (d->host_flags[0] != 0 && d->host_flags[0] != 100 && !keep) {
+            // a hand-off wait timed out (a workgroup could not become resident beside another
+            // stream's work, e.g. a pipelined Griffin-Lim): every wave drained with the status and
+            // the grid is gone.  Re-run this sentence from its initial state on the multi-launch
+            // path (same results within the resident tests' tolerance); the handle stays resident.
+            // (inference_truncated's carried state may already be overwritten: that case raises.)
+            ++d->res_timeouts;
+            TTS_HIP(launch_decoder_init(ia, s));
+            if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
+            tts_status st = enqueue_prenet_go(d, B, s);
+            if (st) return st;
         } else {
             TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP,
                       d->host_flags[0] == 100 ? "decoder did not stop within max_steps + 20 (internal error)"

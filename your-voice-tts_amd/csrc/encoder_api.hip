@@ -48,6 +48,8 @@ struct tts_encoder {
     int* host_status = nullptr;  // pinned
     bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
     bool status_pending = false;
+    bool skip_resident_once = false;  // a pipelined resident run timed out: its rerun goes per-step
+    int res_timeouts = 0;             // resident runs that timed out a hand-off and re-ran per-step
     std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
     int last_resident = 0;                  // the last run's BiLSTM path (tts_encoder_last_path)
 };
@@ -292,16 +294,24 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
     // initial state (h_0, c_0) of both directions: step 0 reads the parity-1 h slots
     const size_t hs = (size_t)e->Bcap * EH;  // per-direction stride
     const size_t row = (size_t)B * EH * sizeof(float);
-    if (state_in) {  // [h_fwd, h_bwd, c_fwd, c_bwd] x [B][256]
-        for (int d = 0; d < 2; ++d) {
-            TTS_HIP(hipMemcpyAsync(e->h + 2 * hs + d * hs, state_in + (size_t)d * B * EH, row, hipMemcpyDeviceToDevice, s));
-            TTS_HIP(hipMemcpyAsync(e->c + d * hs, state_in + (size_t)(2 + d) * B * EH, row, hipMemcpyDeviceToDevice, s));
+    auto init_state = [&]() -> tts_status {
+        if (state_in) {  // [h_fwd, h_bwd, c_fwd, c_bwd] x [B][256]
+            for (int d = 0; d < 2; ++d) {
+                TTS_HIP(hipMemcpyAsync(e->h + 2 * hs + d * hs, state_in + (size_t)d * B * EH, row,
+                                       hipMemcpyDeviceToDevice, s));
+                TTS_HIP(hipMemcpyAsync(e->c + d * hs, state_in + (size_t)(2 + d) * B * EH, row,
+                                       hipMemcpyDeviceToDevice, s));
+            }
+        } else {
+            TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * hs, s));
+            TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * hs, s));
         }
-    } else {
-        TTS_HIP(hipMemsetAsync(e->h, 0, sizeof(float) * 4 * hs, s));
-        TTS_HIP(hipMemsetAsync(e->c, 0, sizeof(float) * 2 * hs, s));
-    }
-    if (e->resident && B == 1 && lens[0] == Lmax) {
+        return TTS_OK;
+    };
+    if (tts_status st = init_state()) return st;
+    const bool skip_resident = e->skip_resident_once;
+    e->skip_resident_once = false;
+    if (e->resident && !skip_resident && B == 1 && lens[0] == Lmax) {
         auto rit = e->rgraphs.find(Lmax);
         if (rit == e->rgraphs.end()) {
             hipGraph_t g = nullptr;
@@ -336,9 +346,13 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
             TTS_HIP(hipStreamSynchronize(s));
             if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
                 e->resident = false;  // rerun below with the per-step launches (same state, untouched)
+            } else if (e->host_status[0] != 0) {
+                // a hand-off wait timed out (a workgroup could not be placed beside another stream's
+                // work): the grid drained; rerun this call with the per-step launches from the
+                // initial state (state_in is still the caller's), the handle stays resident
+                ++e->res_timeouts;
+                if (tts_status st = init_state()) return st;
             } else {
-                TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP,
-                          "resident encoder: a hand-off wait timed out (internal error)");
                 goto done;
             }
         }
@@ -397,7 +411,11 @@ tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
         *placement_failed = 1;
         return TTS_OK;
     }
-    TTS_CHECK(e->host_status[0] == 0, TTS_ERR_HIP, "resident encoder: a hand-off wait timed out (internal error)");
+    if (e->host_status[0] != 0) {  // a hand-off wait timed out: the caller reruns once per-step
+        ++e->res_timeouts;
+        e->skip_resident_once = true;
+        *placement_failed = 1;
+    }
     return TTS_OK;
 }
 }  // namespace tts

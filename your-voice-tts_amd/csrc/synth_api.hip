@@ -37,9 +37,6 @@ struct tts_synth {
     // waits for Griffin-Lim.
     hipStream_t stream = nullptr, gl_stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_post = nullptr, ev_out = nullptr;
-    // the last Griffin-Lim was the persistent launch (its workgroups wait on each other): the next
-    // call's resident encoder / decoder launches (which do too) must not run beside it
-    bool gl_spins = false;
     // pinned host staging of ids / lens / frames, alternated per call: call k reuses call k-2's
     // buffer, whose copies completed before call k-1's decoder synchronisation and Griffin-Lim
     // collection
@@ -203,8 +200,12 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     const int par = s->calls & 1;
     PipelineScope scope(s);
     // the front stages do not wait for the caller's stream (they read host inputs and write this
-    // handle's buffers only), nor for the previous call's Griffin-Lim unless that one spins
-    if (s->gl_spins) TTS_HIP(hipStreamWaitEvent(ss, s->ev_out, 0));
+    // handle's buffers only), nor for the previous call's Griffin-Lim.  The persistent Griffin-Lim
+    // (whose workgroups wait on each other) only runs on this same stream (<= 256 frames, below),
+    // so it never shares the device with this call's resident launches.  A cross-stream Griffin-Lim
+    // is the non-persistent per-iteration form; if its workgroups keep a resident encoder /
+    // decoder workgroup from being placed, that launch's bounded waits drain it and the stage
+    // re-runs multi-launch (decoder_api.hip, encoder_api.hip): slower, never wrong.
     TTS_HIP(hipMemcpyAsync(s->ids, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
     s->steps.assign(B, 0);
     for (int attempt = 0;; ++attempt) {
@@ -250,11 +251,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
     // shorter sentences leave their waveform tail unwritten: zero it
     if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
-    s->gl_spins = false;
     if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, gs))) return st;
-    int path = 0;
-    if ((st = tts_gl_last_path(s->g, &path))) return st;
-    s->gl_spins = !same && path == TTS_GL_PATH_PERSISTENT;
     TTS_HIP(hipEventRecord(s->ev_out, gs));
     TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
     return TTS_OK;

@@ -173,17 +173,54 @@ def tts(model, vocoder_model, C, VC, text, ap, use_cuda, batched_vocoder, figure
 
 
 class Synthesizer:
-    """server/synthesizer.py:22-162 without file loading: give it a built model, an
-    AudioProcessor, the tts config and an input_adapter (sentence -> ids).  All sentences of a
-    request are synthesised as one GPU batch instead of one after another."""
+    """server/synthesizer.py:29-162.  Built like the reference, from the server config
+    (``Synthesizer(config)`` with tts_path / tts_file / tts_config / use_cuda: ``load_tts`` reads
+    the model config and checkpoint), or from parts: a built model, an AudioProcessor, the tts config
+    and an input_adapter (sentence -> ids).  All sentences of a request are synthesised as one GPU
+    batch instead of one after another."""
 
-    def __init__(self, tts_model, ap, tts_config, input_adapter=None, seed=0):
+    def __init__(self, tts_model, ap=None, tts_config=None, input_adapter=None, seed=0):
+        self.seed = seed
+        self.wavernn = None
+        if ap is None and tts_config is None and isinstance(tts_model, dict) and "tts_path" in tts_model:
+            # server/synthesizer.py:30-38: Synthesizer(config)
+            self.config = tts_model
+            self.use_cuda = self.config.get("use_cuda", True)
+            self.load_tts(self.config["tts_path"], self.config["tts_file"], self.config["tts_config"], self.use_cuda)
+            if self.config.get("wavernn_lib_path"):
+                raise NotImplementedError("WaveRNN (server/synthesizer.py:68-95) is an external repo, not part "
+                                          "of the reference tree: leave wavernn_lib_path empty for Griffin-Lim")
+            return
         self.tts_model = tts_model
         self.ap = ap
         self.tts_config = tts_config
         self.input_adapter = input_adapter
-        self.seed = seed
         self.tts_model.eval()
+        self.tts_model.decoder.max_decoder_steps = 3000  # server/synthesizer.py:66
+
+    def load_tts(self, model_path, model_file, model_config, use_cuda=True):
+        """server/synthesizer.py:40-66: config -> AudioProcessor, the input adapter (phonemes or
+        characters), setup_model, cp['model'] (weights-only load), eval, 3000-step decoder cap.
+        The model always runs on the GPU (no CPU path), whatever use_cuda says."""
+        from . import text as _text
+        from .generic_utils import load_config
+        from .synthesize import load_model
+        tts_config = os.path.join(model_path, model_config)
+        self.model_file = os.path.join(model_path, model_file)
+        print(" > Loading TTS model ...")
+        print(" | > model config: ", tts_config)
+        print(" | > model file: ", model_file)
+        self.tts_config = load_config(tts_config)
+        self.use_phonemes = self.tts_config.use_phonemes
+        self.ap = AudioProcessor(**self.tts_config.audio)
+        c = self.tts_config
+        if self.use_phonemes:
+            self.input_adapter = lambda sen: _text.phoneme_to_sequence(sen, [c.text_cleaner], c.phoneme_language,
+                                                                       c.enable_eos_bos_chars)
+        else:
+            self.input_adapter = lambda sen: _text.text_to_sequence(sen, [c.text_cleaner])
+        self.input_size = _text.num_chars(c)
+        self.tts_model = load_model(c, self.model_file)
         self.tts_model.decoder.max_decoder_steps = 3000  # server/synthesizer.py:66
 
     def split_into_sentences(self, text):

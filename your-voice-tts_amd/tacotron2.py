@@ -365,6 +365,12 @@ class Tacotron2:
         n = ap.hop_length * (max(frames) - 1)
         return self._wav_buf[:B * n].view(B, n), frames
 
+    def synth_sync(self):
+        """Wait for the last synthesize_native call and raise if its Griffin-Lim failed
+        (tts_synth_sync); a no-op before the first call."""
+        if self._synth is not None:
+            _native.check(_native.lib().tts_synth_sync(self._synth[0]), "tts_synth_sync")
+
     def _path_timing(self, lib, hdec):
         """Decoder loop time and the paths the last run took (resident decoder / encoder BiLSTM)."""
         ms, ns, res, enc = ctypes.c_float(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
