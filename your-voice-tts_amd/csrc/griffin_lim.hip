@@ -8,9 +8,13 @@
 // amplifies rounding ~100x over 60 iterations, so this is what keeps the waveform within 1e-4.
 //
 // HBM layout (per call):
-//   S      [B][Fmax][1025] f64    |S|^power, frame-major (one 8.2 KB row per frame)
-//   frames [2][B][Fmax][WINP] f64 windowed inverse-FFT output of every frame, window support only
-//                                 (WIN = 1102 samples; the padded Hann is zero elsewhere)
+//   S      [B][Fmax][1025] f32    |S|^power, frame-major (one 4.1 KB row per frame; computed in
+//                                 float64, stored rounded: the linear path's values are float32
+//                                 already, the mel path's rounding moves the waveform ~1e-6)
+//   frames [2][B][Fmax][WINP] f32 windowed inverse-FFT output of every frame, window support only
+//                                 (WIN = 1102 samples; the padded Hann is zero elsewhere), rounded
+//                                 to float32 once before librosa's float32 overlap-add (round 3:
+//                                 the float64 slots were 2/3 of the batched loop's HBM traffic)
 // One workgroup per (sentence, frame) per iteration does the whole GL iteration for its frame:
 //   overlap-add gather of the previous iteration's frames (<= 5 contributors per sample) with the
 //   window-sum-square normalisation and the STFT's reflect padding -> window -> 2048-point real
@@ -29,6 +33,9 @@
 using namespace tts;
 
 namespace {
+
+typedef float spec_t;   // |S|^power storage
+typedef float frame_t;  // windowed iSTFT frame storage
 
 constexpr int NFFT = 2048;
 constexpr int NB = 1025;  // bins
@@ -236,7 +243,7 @@ __device__ __forceinline__ int reflect_idx(int p, int N) {
 // float32 y[p] of the previous iteration's iSTFT (librosa istft): float64 frame contributions
 // added frame by frame into a float32 accumulator, divided (float32) by the float32 window
 // sum-square where it exceeds float32 tiny.  q = p + n_fft/2 is the untrimmed position.
-__device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q, int F, const Geo& g,
+__device__ __forceinline__ float ola_sample(const frame_t* __restrict__ fr, int q, int F, const Geo& g,
                                             const double* __restrict__ win2) {
     if (q < g.woff) return 0.f;
     int ilo = q - g.woff - g.win + 1;
@@ -246,7 +253,7 @@ __device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q
     float y = 0.f, wss = 0.f;
     for (int i = ilo; i <= ihi; ++i) {
         const int o = q - i * g.hop;  // offset inside frame i (0..2047)
-        y = (float)((double)y + fr[(int64_t)i * g.winp + (o - g.fb)]);
+        y = (float)((double)y + (double)fr[(int64_t)i * g.winp + (o - g.fb)]);
         wss = (float)((double)wss + win2[o]);
     }
     return wss > 1.17549435e-38f ? y / wss : y;
@@ -255,7 +262,7 @@ __device__ __forceinline__ float ola_sample(const double* __restrict__ fr, int q
 // ola_sample with the <= OLA_MAX contributing frames' loads issued together (the sum still runs
 // frame by frame in index order; absent contributors add exact zeros): bitwise equal to it.
 constexpr int OLA_MAX = 5;  // ceil(win / hop) for the reference geometry (1102 / 275)
-__device__ __forceinline__ float ola_sample_unrolled(const double* __restrict__ fr, int q, int F, const Geo& g,
+__device__ __forceinline__ float ola_sample_unrolled(const frame_t* __restrict__ fr, int q, int F, const Geo& g,
                                                      const double* __restrict__ win2) {
     if (q < g.woff) return 0.f;
     int ilo = q - g.woff - g.win + 1;
@@ -268,7 +275,7 @@ __device__ __forceinline__ float ola_sample_unrolled(const double* __restrict__ 
         const int i = ilo + k;
         const int o = q - i * g.hop;
         const bool ok = i <= ihi;
-        fv[k] = ok ? fr[(int64_t)i * g.winp + (o - g.fb)] : 0.0;
+        fv[k] = ok ? (double)fr[(int64_t)i * g.winp + (o - g.fb)] : 0.0;
         wv[k] = ok ? win2[o] : 0.0;
     }
     float y = 0.f, wss = 0.f;
@@ -287,7 +294,7 @@ struct MagArgs {
     int n_in, Fmax;
     const int* F;
     const double* pinv;  // [n_mels][1025]: pinv(mel basis) transposed (lanes read consecutive bins)
-    double* S;
+    spec_t* S;
     float min_db, ref_db, power, max_norm;
     int signal_norm, symmetric, clip;
 };
@@ -318,14 +325,14 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     if (f0 >= Fb) return;
     const int nf = min(MAG_FT, Fb - f0);
     const float* sp = a.spec + ((int64_t)b * a.Fmax + f0) * a.n_in;
-    double* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
+    spec_t* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
     const int tid = threadIdx.x;
     const int k0 = blockIdx.x * MAG_KT;
     if (a.mode == TTS_GL_FROM_LINEAR) {
         // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160)
         for (int i = tid; i < nf * MAG_KT; i += blockDim.x) {
             const int f = i / MAG_KT, k = k0 + i % MAG_KT;
-            if (k < NB) S[(int64_t)f * NB + k] = (double)powf(denorm_to_amp(sp[(int64_t)f * NB + k], a), a.power);
+            if (k < NB) S[(int64_t)f * NB + k] = (spec_t)powf(denorm_to_amp(sp[(int64_t)f * NB + k], a), a.power);
         }
         return;
     }
@@ -371,18 +378,18 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
 #pragma unroll
         for (int i = 0; i < FW; ++i) {
             const int f = wave * FW + i;
-            if (f < nf) S[(int64_t)f * NB + k] = pow(fmax(acc[i], 1e-10), (double)a.power);
+            if (f < nf) S[(int64_t)f * NB + k] = (spec_t)pow(fmax(acc[i], 1e-10), (double)a.power);
         }
     }
 }
 
 // ---------------------------------------------------------------- GL iteration
 struct IterArgs {
-    const double* S;      // [B][Fmax][1025]
+    const spec_t* S;      // [B][Fmax][1025]
     const float* y;       // [B][Nmax] the previous iteration's float32 signal (gl_ola_kernel)
-    const double* prev;   // FUSED: the previous iteration's frames (overlap-added here instead)
+    const frame_t* prev;  // FUSED: the previous iteration's frames (overlap-added here instead)
     int64_t Nmax;
-    double* next;         // frames written by this iteration
+    frame_t* next;        // frames written by this iteration
     const int* F;
     int Fmax;
     int B;
@@ -429,7 +436,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     // X[1024] stays in a register of thread 0, the thread that writes and reads it: 32 KB of LDS
     double2* const X = buf0;
     double2 xnyq = double2{0.0, 0.0};
-    const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     // ---- phase 0: the frame's global operands are issued before anything waits: window, |S|,
     // split twiddles, the input samples (the FFT twiddles follow pass by pass, fft1024_regs_gtw)
     constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;   // bins per thread (5)
@@ -440,7 +447,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
 #pragma unroll
     for (int i = 0; i < PK; ++i) {
         const int k = tid + i * GL_THREADS;
-        sk[i] = k < NB ? Sf[k] : 0.0;
+        sk[i] = k < NB ? (double)Sf[k] : 0.0;
     }
     // the padded Hann at this thread's samples: the analysis window of the STFT input (the first
     // butterfly's register operands) and the synthesis window of the iSTFT output (the last
@@ -462,7 +469,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
             const int n = edge_sample(tid, i);  // the first butterfly's operands stay in registers
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
             if (FUSED) {
-                const double* fb = a.prev + (int64_t)b * a.Fmax * g.winp;
+                const frame_t* fb = a.prev + (int64_t)b * a.Fmax * g.winp;
                 yi[i] = sup ? ola_sample_unrolled(fb, reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2, Fb, g, a.c.win2)
                             : 0.f;
             } else {
@@ -529,12 +536,12 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
     // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft), from
     // the last butterfly's registers
-    double* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
+    frame_t* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i) - g.woff;
         const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = wo[i] * (zv * (1.0 / NH));
+        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = (frame_t)(wo[i] * (zv * (1.0 / NH)));
     }
 }
 
@@ -731,6 +738,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsign
 __device__ __forceinline__ float buf_f32(__amdgpu_buffer_rsrc_t r, int voff) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
 }
+__device__ __forceinline__ float buf_f32s(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
 __device__ __forceinline__ double buf_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
@@ -750,7 +760,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     const int L = threadIdx.x;
     __shared__ double lds[WV_SLOTS];
     __shared__ double2 t2[64];  // W64^(p1 q2) at [q2][p1]
-    const auto rS = buf_rsrc(a.S + ((int64_t)b * a.Fmax + f) * NB, NB * 8);
+    const auto rS = buf_rsrc(a.S + ((int64_t)b * a.Fmax + f) * NB, NB * 4);
     const auto rC = buf_rsrc(a.winc, 4 * 64 * 16);
     const auto rT = buf_rsrc(a.c.tw, NFFT * 16);
     const auto rP = buf_rsrc(a.wt, 64 * 16);
@@ -838,7 +848,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     double vmy[8];
     double zki = lds[zb], zmi = lds[mb + 64 * 15];
     if (L == 0) zmi = zki;
-    double sa = buf_f64(rS, 8 * L, 0), sb = buf_f64(rS, 8 * (NH - L), 0);
+    double sa = buf_f32(rS, 4 * L), sb = buf_f32(rS, 4 * (NH - L));
     // split twiddles t[k] = W2048^(L + 64 m) = W2048^L x W32^m (compile-time W32^m)
     const double2 tL = buf_c64(rT, 16 * L, 0);
     double2 tk = tL;
@@ -851,11 +861,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         if (m < 7) {
             zki_n = lds[zb + 64 * (m + 1)];
             zmi_n = lds[mb + 64 * (14 - m)];
-            sa_n = buf_f64(rS, 8 * L, 512 * (m + 1));
-            sb_n = buf_f64(rS, 8 * (NH - k - 64), 0);
+            sa_n = buf_f32s(rS, 4 * L, 256 * (m + 1));
+            sb_n = buf_f32(rS, 4 * (NH - k - 64));
             tk_n = cmulf(tL, double2{kW32[m + 1][0], kW32[m + 1][1]});
         } else {
-            sa_n = buf_f64(rS, 0, 4096);  // k = 512
+            sa_n = buf_f32s(rS, 0, 2048);  // k = 512
             tk_n = buf_c64(rT, 0, 8192);  // k = 512
         }
         // 2E = Z[k] + conj Z[N-k], 2O = -i (Z[k] - conj Z[N-k]): X[k] = E + t O up to the factor 2
@@ -901,9 +911,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // (the frame's store range is its support: stores outside it are dropped by the range check)
     wave_fft1024<true>(v, lds, t2, rT, L);
     // (samples 2 (16 r3 + K2) + 128 (j + 4 q1): the window by the same recurrence; each sample pair
-    // is one 16-byte store into the frame slot [fb, fb + winp), pairs outside the slot dropped by its
-    // range; the slot's one or two samples outside the support are never read)
-    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.winp * 8);
+    // is one 8-byte store (float32 pair; a wave's 64 pairs are 128 consecutive samples) into the
+    // frame slot [fb, fb + winp), pairs outside the slot dropped by its range; the slot's one or two
+    // samples outside the support are never read)
+    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.winp * 4);
     __builtin_amdgcn_sched_barrier(0);
     const double2 s0 = buf_c64(rC, 16 * L, 2048), s1 = buf_c64(rC, 16 * L, 3072);
     double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
@@ -914,8 +925,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             const int s = 2 * (256 * q1 + 64 * j + 16 * r3 + K2);
             const double2 z = v[4 * j + q1];
             // (1/2 of the pre-split) x 1/NH: one exact power-of-two scale
-            const double2 o2 = double2{fma(-0.5, a0, 0.5) * (z.x * (0.5 / NH)), fma(-0.5, b0, 0.5) * (z.y * (0.5 / NH))};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o2), rO, (s - g.fb) * 8, 0, 0);
+            const float2 o2 = float2{(float)(fma(-0.5, a0, 0.5) * (z.x * (0.5 / NH))),
+                                     (float)(fma(-0.5, b0, 0.5) * (z.y * (0.5 / NH)))};
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o2), rO, (s - g.fb) * 4, 0, 0);
             const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
             a0 = a1;
             a1 = a2;
@@ -940,7 +952,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 // 1e-4..1e-2 rel RMS errors.  Every wait is bounded.
 struct PersArgs {
     IterArgs it;        // S, F, Fmax, B, geometry, constants (y / next / prev unused)
-    double* frames;     // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
+    frame_t* frames;    // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
     int64_t fstride;
     int iters;          // iterations after the initial one
     int it0;            // first iteration index of this launch (parity of the frames it reads)
@@ -972,7 +984,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;
     constexpr int PN = NFFT / GL_THREADS;
     // ---- iteration-invariant operands
-    const double* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     const FftTw ftw = load_fft_tw(a.c.tw);
     double2 tk[PK];
     double sk[PK];
@@ -980,7 +992,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     for (int i = 0; i < PK; ++i) {
         const int k = tid + i * GL_THREADS;
         tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
-        sk[i] = k < NB ? Sf[k] : 0.0;
+        sk[i] = k < NB ? (double)Sf[k] : 0.0;
     }
     double wo[PN];  // synthesis window at this thread's output samples (edge_sample)
 #pragma unroll
@@ -1040,8 +1052,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         tp = tn;                                         \
     }
     for (int it = p.it0; it < p.it0 + p.iters; ++it) {
-        const double* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
-        double* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
+        const frame_t* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
+        frame_t* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
         if (it > p.it0 && wave == 0) {
             // the previous iteration of every contributor frame, one lane per frame: its tag is it
             // or, when that frame already finished this iteration too, it + 1 (never further: the
@@ -1083,8 +1095,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             double fv[OLA_MAX];
 #pragma unroll
             for (int k = 0; k < OLA_MAX; ++k)
-                fv[k] = off[i][k] >= 0 ? __longlong_as_double((long long)__hip_atomic_load(
-                                             (gu64_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                fv[k] = off[i][k] >= 0 ? (double)__uint_as_float(__hip_atomic_load(
+                                             (gu32_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                                        : 0.0;
             float y = 0.f;
 #pragma unroll
@@ -1135,8 +1147,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const int n = edge_sample(tid, i) - g.woff;
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
             if (n >= 0 && n < g.win)
-                __hip_atomic_store((gu64_t*)(dst + n + g.woff - g.fb),
-                                   (unsigned long long)__double_as_longlong(wo[i] * (zv * (1.0 / NH))),
+                __hip_atomic_store((gu32_t*)(dst + n + g.woff - g.fb),
+                                   __float_as_uint((frame_t)(wo[i] * (zv * (1.0 / NH)))),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -1154,7 +1166,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
 
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
 struct FinArgs {
-    const double* frames;
+    const frame_t* frames;
     const int* F;
     int Fmax, B;
     Geo g;
@@ -1178,7 +1190,7 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     // (contributor loads issued together when the geometry allows it: bitwise the same sum; the
     // window sum-square from the periodic table where no contributor is clipped, as ola_sample
     // would sum it, else summed here)
-    const double* fr = a.frames + (int64_t)b * a.Fmax * a.g.winp;
+    const frame_t* fr = a.frames + (int64_t)b * a.Fmax * a.g.winp;
     const Geo& g = a.g;
     const int q = p + NFFT / 2;
     float yv;
@@ -1193,7 +1205,7 @@ __global__ void gl_ola_kernel(const FinArgs a) {
 #pragma unroll
         for (int k = 0; k < OLA_MAX; ++k) {
             const int i = ilo + k;
-            fv[k] = i <= ihi ? fr[(int64_t)i * g.winp + (q - i * g.hop - g.fb)] : 0.0;
+            fv[k] = i <= ihi ? (double)fr[(int64_t)i * g.winp + (q - i * g.hop - g.fb)] : 0.0;
         }
         float y = 0.f, wss = 0.f;
 #pragma unroll
@@ -1392,7 +1404,8 @@ struct tts_gl {
     bool wave = true;       // batched iterations on gl_iter_wave_kernel (TTS_GL_WAVE=0: gl_iter_kernel)
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
-    double *S = nullptr, *frames = nullptr;
+    spec_t* S = nullptr;
+    frame_t* frames = nullptr;
     float* y = nullptr;
     int* F = nullptr;
     int Fcap_B = 0;
@@ -1404,7 +1417,7 @@ struct tts_gl {
     int last_path = TTS_GL_PATH_UNFUSED;
     unsigned* flags = nullptr;  // persistent loop: [flags_n] tags
     size_t flags_n = 0;
-    double* pfr = nullptr;      // persistent loop: one frame slot per iteration
+    frame_t* pfr = nullptr;     // persistent loop: one frame slot per iteration
     size_t pfr_n = 0;
     int* pstatus = nullptr;     // [dev] status of the persistent loop
     int* host_status = nullptr; // pinned
@@ -1596,8 +1609,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     // run's stream has been synchronised by its caller before the next run)
     if (!g->pipeline) TTS_HIP(hipStreamSynchronize(s));
     tts_status st;
-    if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, 8))) return st;
-    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, 8))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, sizeof(spec_t)))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, sizeof(frame_t)))) return st;
     if ((st = grow(reinterpret_cast<void**>(&g->y), g->y_n, needY, 4))) return st;
     if (B > g->Fcap_B) {
         if (g->F) TTS_HIP(hipFree(g->F));
@@ -1649,11 +1662,11 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         if (need > g->pfr_n) {
             if (g->pfr) TTS_HIP(hipFree(g->pfr));
             g->pfr = nullptr;
-            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(double)));
+            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(frame_t)));
             g->pfr_n = need;
         }
     }
-    double* const fr0 = persistent ? g->pfr : g->frames;
+    frame_t* const fr0 = persistent ? g->pfr : g->frames;
     IterArgs ia{};
     ia.S = g->S;
     ia.F = g->F;
@@ -1726,7 +1739,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                                   &persistent_ran));
         if (!persistent_ran) {
             // the initial iSTFT wrote slot 0 of the persistent frame buffer: hand it to the fused loop
-            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(double), hipMemcpyDeviceToDevice, s));
+            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(frame_t), hipMemcpyDeviceToDevice, s));
             if (prof) {
                 TTS_HIP(hipStreamSynchronize(s));
                 TTS_HIP(hipFree(prof));
