@@ -1,6 +1,6 @@
 import os, sys
 import numpy as np, torch
-sys.path.insert(0, "tests")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 from conftest import load_pkg
 audio = load_pkg("audio"); cfg = load_pkg("generic_utils").default_config("config_tacotron2.json")
 rng = np.random.Generator(np.random.PCG64(2))

@@ -11,10 +11,13 @@
 //   S      [B][Fmax][1025] f32    |S|^power, frame-major (one 4.1 KB row per frame; computed in
 //                                 float64, stored rounded: the linear path's values are float32
 //                                 already, the mel path's rounding moves the waveform ~1e-6)
-//   frames [2][B][Fmax][WINP] f32 windowed inverse-FFT output of every frame, window support only
-//                                 (WIN = 1102 samples; the padded Hann is zero elsewhere), rounded
-//                                 to float32 once before librosa's float32 overlap-add (round 3:
-//                                 the float64 slots were 2/3 of the batched loop's HBM traffic)
+//   frames [2][B][Fmax][WINP]     windowed inverse-FFT output of every frame, window support only
+//                                 (WIN = 1102 samples; the padded Hann is zero elsewhere).  The
+//                                 batched (unfused) loop stores them float32, rounded once before
+//                                 librosa's float32 overlap-add (round 3: float64 slots were 2/3 of
+//                                 its HBM traffic); the fused and persistent loops, which gather
+//                                 every sample from its <= 5 contributing frames, keep float64 (their
+//                                 sc1 4-byte gathers measured 2.4 -> 4.3 us per iteration)
 // One workgroup per (sentence, frame) per iteration does the whole GL iteration for its frame:
 //   overlap-add gather of the previous iteration's frames (<= 5 contributors per sample) with the
 //   window-sum-square normalisation and the STFT's reflect padding -> window -> 2048-point real
@@ -34,8 +37,9 @@ using namespace tts;
 
 namespace {
 
-typedef float spec_t;   // |S|^power storage
-typedef float frame_t;  // windowed iSTFT frame storage
+typedef float spec_t;    // |S|^power storage
+typedef float frame_t;   // windowed iSTFT frame storage of the batched (unfused) loop
+typedef double pframe_t; // ... of the fused and persistent loops
 
 constexpr int NFFT = 2048;
 constexpr int NB = 1025;  // bins
@@ -243,7 +247,8 @@ __device__ __forceinline__ int reflect_idx(int p, int N) {
 // float32 y[p] of the previous iteration's iSTFT (librosa istft): float64 frame contributions
 // added frame by frame into a float32 accumulator, divided (float32) by the float32 window
 // sum-square where it exceeds float32 tiny.  q = p + n_fft/2 is the untrimmed position.
-__device__ __forceinline__ float ola_sample(const frame_t* __restrict__ fr, int q, int F, const Geo& g,
+template <typename FT>
+__device__ __forceinline__ float ola_sample(const FT* __restrict__ fr, int q, int F, const Geo& g,
                                             const double* __restrict__ win2) {
     if (q < g.woff) return 0.f;
     int ilo = q - g.woff - g.win + 1;
@@ -262,7 +267,8 @@ __device__ __forceinline__ float ola_sample(const frame_t* __restrict__ fr, int 
 // ola_sample with the <= OLA_MAX contributing frames' loads issued together (the sum still runs
 // frame by frame in index order; absent contributors add exact zeros): bitwise equal to it.
 constexpr int OLA_MAX = 5;  // ceil(win / hop) for the reference geometry (1102 / 275)
-__device__ __forceinline__ float ola_sample_unrolled(const frame_t* __restrict__ fr, int q, int F, const Geo& g,
+template <typename FT>
+__device__ __forceinline__ float ola_sample_unrolled(const FT* __restrict__ fr, int q, int F, const Geo& g,
                                                      const double* __restrict__ win2) {
     if (q < g.woff) return 0.f;
     int ilo = q - g.woff - g.win + 1;
@@ -387,9 +393,9 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
 struct IterArgs {
     const spec_t* S;      // [B][Fmax][1025]
     const float* y;       // [B][Nmax] the previous iteration's float32 signal (gl_ola_kernel)
-    const frame_t* prev;  // FUSED: the previous iteration's frames (overlap-added here instead)
+    const void* prev;     // FUSED: the previous iteration's frames (overlap-added here instead)
     int64_t Nmax;
-    frame_t* next;        // frames written by this iteration
+    void* next;           // frames written by this iteration (frame_t or pframe_t: see the kernels)
     const int* F;
     int Fmax;
     int B;
@@ -415,7 +421,7 @@ __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned
 // FUSED (small batches): the frame's own 2048 STFT input samples are overlap-added from the
 // previous iteration's frames inside this launch (bitwise the values gl_ola_kernel would store),
 // so an iteration is one launch instead of two.
-template <bool INIT, bool FUSED = false>
+template <bool INIT, bool FUSED, typename FT>
 // Four workgroups per CU (32 KB of LDS, <= 128 VGPRs each).  Measured at B = 64: the same speed
 // as three workgroups with the FFT twiddles held in registers, faster than five (which spill).
 __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a) {
@@ -469,7 +475,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
             const int n = edge_sample(tid, i);  // the first butterfly's operands stay in registers
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
             if (FUSED) {
-                const frame_t* fb = a.prev + (int64_t)b * a.Fmax * g.winp;
+                const FT* fb = static_cast<const FT*>(a.prev) + (int64_t)b * a.Fmax * g.winp;
                 yi[i] = sup ? ola_sample_unrolled(fb, reflect_idx(f * g.hop + n - NFFT / 2, N) + NFFT / 2, Fb, g, a.c.win2)
                             : 0.f;
             } else {
@@ -536,12 +542,12 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
     // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft), from
     // the last butterfly's registers
-    frame_t* out = a.next + ((int64_t)b * a.Fmax + f) * g.winp;
+    FT* out = static_cast<FT*>(a.next) + ((int64_t)b * a.Fmax + f) * g.winp;
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i) - g.woff;
         const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = (frame_t)(wo[i] * (zv * (1.0 / NH)));
+        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = (FT)(wo[i] * (zv * (1.0 / NH)));
     }
 }
 
@@ -914,7 +920,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // is one 8-byte store (float32 pair; a wave's 64 pairs are 128 consecutive samples) into the
     // frame slot [fb, fb + winp), pairs outside the slot dropped by its range; the slot's one or two
     // samples outside the support are never read)
-    const auto rO = buf_rsrc(a.next + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.winp * 4);
+    const auto rO = buf_rsrc(static_cast<frame_t*>(a.next) + ((int64_t)b * a.Fmax + f) * g.winp, (unsigned)g.winp * 4);
     __builtin_amdgcn_sched_barrier(0);
     const double2 s0 = buf_c64(rC, 16 * L, 2048), s1 = buf_c64(rC, 16 * L, 3072);
     double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
@@ -952,7 +958,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 // 1e-4..1e-2 rel RMS errors.  Every wait is bounded.
 struct PersArgs {
     IterArgs it;        // S, F, Fmax, B, geometry, constants (y / next / prev unused)
-    frame_t* frames;    // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
+    pframe_t* frames;   // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
     int64_t fstride;
     int iters;          // iterations after the initial one
     int it0;            // first iteration index of this launch (parity of the frames it reads)
@@ -1052,8 +1058,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         tp = tn;                                         \
     }
     for (int it = p.it0; it < p.it0 + p.iters; ++it) {
-        const frame_t* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
-        frame_t* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
+        const pframe_t* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
+        pframe_t* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
         if (it > p.it0 && wave == 0) {
             // the previous iteration of every contributor frame, one lane per frame: its tag is it
             // or, when that frame already finished this iteration too, it + 1 (never further: the
@@ -1095,8 +1101,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             double fv[OLA_MAX];
 #pragma unroll
             for (int k = 0; k < OLA_MAX; ++k)
-                fv[k] = off[i][k] >= 0 ? (double)__uint_as_float(__hip_atomic_load(
-                                             (gu32_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                fv[k] = off[i][k] >= 0 ? __longlong_as_double((long long)__hip_atomic_load(
+                                             (gu64_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                                        : 0.0;
             float y = 0.f;
 #pragma unroll
@@ -1147,8 +1153,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const int n = edge_sample(tid, i) - g.woff;
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
             if (n >= 0 && n < g.win)
-                __hip_atomic_store((gu32_t*)(dst + n + g.woff - g.fb),
-                                   __float_as_uint((frame_t)(wo[i] * (zv * (1.0 / NH)))),
+                __hip_atomic_store((gu64_t*)(dst + n + g.woff - g.fb),
+                                   (unsigned long long)__double_as_longlong(wo[i] * (zv * (1.0 / NH))),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -1166,7 +1172,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
 
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
 struct FinArgs {
-    const frame_t* frames;
+    const void* frames;  // frame_t (batched loop) or pframe_t (fused / persistent): gl_ola_kernel<FT>
     const int* F;
     int Fmax, B;
     Geo g;
@@ -1178,6 +1184,7 @@ struct FinArgs {
                         // exists, by (q - woff) mod hop (summed on the host in ola_sample's order)
 };
 
+template <typename FT>
 __global__ void gl_ola_kernel(const FinArgs a) {
     const int b = blockIdx.y;
     const int Fb = a.F[b];
@@ -1190,7 +1197,7 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     // (contributor loads issued together when the geometry allows it: bitwise the same sum; the
     // window sum-square from the periodic table where no contributor is clipped, as ola_sample
     // would sum it, else summed here)
-    const frame_t* fr = a.frames + (int64_t)b * a.Fmax * a.g.winp;
+    const FT* fr = static_cast<const FT*>(a.frames) + (int64_t)b * a.Fmax * a.g.winp;
     const Geo& g = a.g;
     const int q = p + NFFT / 2;
     float yv;
@@ -1405,7 +1412,7 @@ struct tts_gl {
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
     spec_t* S = nullptr;
-    frame_t* frames = nullptr;
+    void* frames = nullptr;  // frame_t or pframe_t slots (sized for pframe_t)
     float* y = nullptr;
     int* F = nullptr;
     int Fcap_B = 0;
@@ -1413,11 +1420,12 @@ struct tts_gl {
     float last_ms = 0.f;
     int last_launches = 0;
     bool last_fused = false;
+    bool last_f64 = false;  // the last run stored its frames float64
     bool last_persistent = false;
     int last_path = TTS_GL_PATH_UNFUSED;
     unsigned* flags = nullptr;  // persistent loop: [flags_n] tags
     size_t flags_n = 0;
-    frame_t* pfr = nullptr;     // persistent loop: one frame slot per iteration
+    pframe_t* pfr = nullptr;    // persistent loop: one frame slot per iteration
     size_t pfr_n = 0;
     int* pstatus = nullptr;     // [dev] status of the persistent loop
     int* host_status = nullptr; // pinned
@@ -1610,7 +1618,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     if (!g->pipeline) TTS_HIP(hipStreamSynchronize(s));
     tts_status st;
     if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, sizeof(spec_t)))) return st;
-    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, sizeof(frame_t)))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, sizeof(pframe_t)))) return st;
     if ((st = grow(reinterpret_cast<void**>(&g->y), g->y_n, needY, 4))) return st;
     if (B > g->Fcap_B) {
         if (g->F) TTS_HIP(hipFree(g->F));
@@ -1657,16 +1665,25 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     int frames_total = 0;
     for (int b = 0; b < B; ++b) frames_total += F[b];
     const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+    // frame storage: float64 for the small-batch fused / persistent loops, float32 for the batched
+    // loop and for the forced fused form (TTS_GL_FUSED=1, whose waveform the tests compare bitwise
+    // with the batched loop's)
+    const bool f64 = fused && !(fz && fz[0] == '1');
     if (persistent) {
         const size_t need = fstride * (size_t)(iters + 1);
         if (need > g->pfr_n) {
             if (g->pfr) TTS_HIP(hipFree(g->pfr));
             g->pfr = nullptr;
-            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(frame_t)));
+            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(pframe_t)));
             g->pfr_n = need;
         }
     }
-    frame_t* const fr0 = persistent ? g->pfr : g->frames;
+    void* const fr0 = persistent ? static_cast<void*>(g->pfr) : g->frames;
+    // frame slot i of the two ping-pong slots, in the loop's storage type
+    auto slot = [&](int i) -> void* {
+        return f64 ? static_cast<void*>(static_cast<pframe_t*>(g->frames) + (i & 1) * fstride)
+                   : static_cast<void*>(static_cast<frame_t*>(g->frames) + (i & 1) * fstride);
+    };
     IterArgs ia{};
     ia.S = g->S;
     ia.F = g->F;
@@ -1695,7 +1712,8 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         ia.zero_status = g->pstatus;
     }
     const dim3 grid(Fmax, B), block(GL_THREADS);
-    hipLaunchKernelGGL(gl_iter_kernel<true>, grid, block, 0, s, ia);
+    if (f64) hipLaunchKernelGGL((gl_iter_kernel<true, false, pframe_t>), grid, block, 0, s, ia);
+    else hipLaunchKernelGGL((gl_iter_kernel<true, false, frame_t>), grid, block, 0, s, ia);
     ia.zero_flags = nullptr;
     ia.zero_status = nullptr;
     TTS_HIP(hipGetLastError());
@@ -1739,7 +1757,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                                   &persistent_ran));
         if (!persistent_ran) {
             // the initial iSTFT wrote slot 0 of the persistent frame buffer: hand it to the fused loop
-            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(frame_t), hipMemcpyDeviceToDevice, s));
+            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(pframe_t), hipMemcpyDeviceToDevice, s));
             if (prof) {
                 TTS_HIP(hipStreamSynchronize(s));
                 TTS_HIP(hipFree(prof));
@@ -1771,18 +1789,19 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             for (int i = 0; i < iters; ++i) {
                 IterArgs a = ia;
                 a.phase_u = nullptr;
-                a.next = g->frames + ((i + 1) & 1) * fstride;
+                a.next = slot(i + 1);
                 if (fused) {
-                    a.prev = g->frames + (i & 1) * fstride;
-                    hipLaunchKernelGGL((gl_iter_kernel<false, true>), grid, block, 0, s, a);
+                    a.prev = slot(i);
+                    if (f64) hipLaunchKernelGGL((gl_iter_kernel<false, true, pframe_t>), grid, block, 0, s, a);
+                    else hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
                 } else {
                     FinArgs o = fa;
-                    o.frames = g->frames + (i & 1) * fstride;
-                    hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, o);
+                    o.frames = slot(i);
+                    hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, o);
                     if (g->wave)
                         hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
                     else
-                        hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+                        hipLaunchKernelGGL((gl_iter_kernel<false, false, frame_t>), grid, block, 0, s, a);
                 }
             }
             hipError_t ce = hipGetLastError();
@@ -1797,9 +1816,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
     TTS_HIP(hipEventRecord(g->ev_t1, s));
-    fa.frames = persistent_ran ? g->pfr + (size_t)iters * fstride : g->frames + (iters & 1) * fstride;
+    fa.frames = persistent_ran ? static_cast<void*>(g->pfr + (size_t)iters * fstride) : slot(iters);
     fa.status = persistent_ran ? g->pstatus : nullptr;
-    hipLaunchKernelGGL(gl_ola_kernel, ogrid, oblock, 0, s, fa);
+    if (f64) hipLaunchKernelGGL(gl_ola_kernel<pframe_t>, ogrid, oblock, 0, s, fa);
+    else hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, fa);
     fa.status = nullptr;
     TTS_HIP(hipGetLastError());
     {
@@ -1829,6 +1849,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         if (cst) return cst;
     }
     g->last_fused = fused;
+    g->last_f64 = f64;
     g->have_last = true;
     g->last_iter = ia;
     g->last_fin = fa;
@@ -1852,21 +1873,25 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
     for (int r = 0; r < reps; ++r) {
         // one GL iteration as tts_gl_run launches it: overlap-add -> per-frame STFT/iSTFT
         FinArgs f = g->last_fin;
-        f.frames = g->frames + (r & 1) * g->last_fstride;
+        const size_t es = g->last_f64 ? sizeof(pframe_t) : sizeof(frame_t);
+        f.frames = static_cast<char*>(g->frames) + (r & 1) * g->last_fstride * es;
         IterArgs a = ia;
         a.phase_u = nullptr;
-        a.next = g->frames + ((r + 1) & 1) * g->last_fstride;
+        a.next = static_cast<char*>(g->frames) + ((r + 1) & 1) * g->last_fstride * es;
         a.prev = f.frames;
         TTS_HIP(hipEventRecord(ev[0], s));
-        if (!g->last_fused) hipLaunchKernelGGL(gl_ola_kernel, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
+        if (!g->last_fused)
+            hipLaunchKernelGGL(gl_ola_kernel<frame_t>, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[1], s));
-        if (g->last_fused)
-            hipLaunchKernelGGL((gl_iter_kernel<false, true>), grid, block, 0, s, a);
+        if (g->last_fused && g->last_f64)
+            hipLaunchKernelGGL((gl_iter_kernel<false, true, pframe_t>), grid, block, 0, s, a);
+        else if (g->last_fused)
+            hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
         else if (g->wave)
             hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
         else
-            hipLaunchKernelGGL(gl_iter_kernel<false>, grid, block, 0, s, a);
+            hipLaunchKernelGGL((gl_iter_kernel<false, false, frame_t>), grid, block, 0, s, a);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[2], s));
         TTS_HIP(hipEventSynchronize(ev[2]));
