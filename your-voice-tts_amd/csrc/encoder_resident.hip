@@ -12,6 +12,10 @@
 // with agent-scope loads: XCD-local hand-offs, no fences.  Waits are bounded (status on timeout).
 #include "encoder_resident.h"
 
+#ifndef ENC_SLEEP
+#define ENC_SLEEP 1  // s_sleep between hand-off polls
+#endif
+
 namespace tts {
 namespace {
 
@@ -50,7 +54,7 @@ __device__ __forceinline__ bool sweep4(u64* g, unsigned tag, float (&v)[4], long
         if (__all(ok)) return true;
         if (spin == 0) t_end = (long long)wall_clock64() + tmo;
         else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) return false;
-        __builtin_amdgcn_s_sleep(1);
+        if (ENC_SLEEP) __builtin_amdgcn_s_sleep(ENC_SLEEP);
     }
 }
 __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {

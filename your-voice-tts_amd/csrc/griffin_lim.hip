@@ -33,6 +33,10 @@
 
 #include "common.h"
 
+#ifndef GLP_SLEEP
+#define GLP_SLEEP 1  // persistent loop: s_sleep between neighbour-tag polls
+#endif
+
 using namespace tts;
 
 namespace {
@@ -1083,7 +1087,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
                     }
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                if (GLP_SLEEP) __builtin_amdgcn_s_sleep(GLP_SLEEP);
             }
 #if GL_ACQUIRE
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

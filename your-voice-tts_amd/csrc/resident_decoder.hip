@@ -27,7 +27,7 @@ typedef __attribute__((address_space(1))) int gint;
 #define RES_GW 4
 #endif
 #ifndef RES_SLEEP
-#define RES_SLEEP 1
+#define RES_SLEEP 0  // s_sleep between polls: 0 measured 11.03 -> 10.70 us per step (tools/dec_ab.sh)
 #endif
 constexpr int GW = RES_GW;  // waves that sweep the 1024- and 512-granule vectors
 
