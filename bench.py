@@ -537,9 +537,10 @@ def main():
         Lmean = float(np.mean([len(x) for x in ids]))
         steps = max(out["steps"])
         frames_total = sum(out["frames"])
-        resident = (not gst) and model.last_timing.get("resident", False)
-        # resident batch-1 decoder: ONE launch runs every step (csrc/resident_decoder.hip), timed
-        # with HIP events on the library stream around that launch; otherwise the per-step kernels
+        resident = bool(model.last_timing.get("resident", False))
+        # resident decoders: ONE launch runs every step (csrc/resident_decoder.hip for the batch-1
+        # Tacotron2, csrc/tacotron_resident.hip for the TacotronGST batch), timed with HIP events on
+        # the library stream around that launch; otherwise the per-step kernels
         kd = {} if resident else model.profile_step_kernels(reps=50 if not gst else 20)
         # small batches run every GL iteration after the first in ONE persistent launch
         # (griffin_lim.hip: gl_persistent_kernel), timed with HIP events around it
@@ -556,7 +557,14 @@ def main():
             kind, alg = (kernel_algorithmic_gst if gst else kernel_algorithmic)(k, B, Lmean, frames_total)
             kernels[k] = dict(mean_ms=ms, launches_per_step=launches[k], ms_per_step=ms * launches[k],
                               algorithmic_bytes=alg, achieved_gbs=alg / (ms * 1e-3) / 1e9 if ms > 0 else None)
-        if resident:
+        if resident and gst:
+            # the per-step kernels' algorithmic bytes (weights once per batch-step) x steps
+            alg = sum(kernel_algorithmic_gst(k, B, Lmean, frames_total)[1]
+                      for k in audiomod._native.TACOTRON_STEP_KERNELS) * steps
+            kernels["tacotron_resident"] = dict(mean_ms=dec_ms, launches_per_step=1, ms_per_step=dec_ms,
+                                                decoder_steps=steps, us_per_decoder_step=1000 * dec_ms / steps,
+                                                algorithmic_bytes=alg, achieved_gbs=alg / (dec_ms * 1e-3) / 1e9)
+        elif resident:
             alg = decoder_step_algorithmic(B, Lmean) * steps
             kernels["resident_decoder"] = dict(mean_ms=dec_ms, launches_per_step=1, ms_per_step=dec_ms,
                                                decoder_steps=steps, us_per_decoder_step=1000 * dec_ms / steps,
@@ -601,8 +609,7 @@ def main():
                 device_wide_edges_us_per_step=edges, handoff_floor_us_per_step=sum(edges.values()),
                 us_per_step=us, handoff_share_of_step=sum(edges.values()) / us)
     # the headline workload's paths, before any other region runs on the same handles
-    paths = dict(decoder=("resident" if model.last_timing.get("resident") else "multi-launch") if not gst
-                 else "multi-launch",
+    paths = dict(decoder="resident" if model.last_timing.get("resident") else "multi-launch",
                  encoder_bilstm=("resident" if model.last_timing.get("encoder_resident") else "per-step")
                  if not gst else "per-step",
                  griffin_lim=ap.last_gl_path())

@@ -297,6 +297,16 @@ tts_status tts_tacotron_postnet(tts_tacotron* t, const float* mel, const int32_t
 
 tts_status tts_tacotron_last_timing(tts_tacotron* t, float* loop_ms, int* steps_run);
 
+/* Which implementation ran the last tts_tacotron_decode (no reference counterpart): *resident = 1
+ * for the resident single-launch decoder (each XCD holds the step weights on its 32 compute units
+ * and decodes up to 4 sentences; hand-offs stay inside the XCD), 0 for the per-step multi-launch
+ * hipGraph path.  The resident path serves B <= 32, Lmax <= 256, r <= 6, max_steps <= 1000 under
+ * config_tacotron_gst.json's attention (sigmoid norm, forward attention without the eval mask, no
+ * transition agent / location / windowing) on a GPU with >= 256 compute units; TTS_RESIDENT=0 in
+ * the environment at tts_tacotron_create disables it.  A resident run whose hand-off wait timed
+ * out re-runs the batch on the multi-launch path (reported 0). */
+tts_status tts_tacotron_last_path(tts_tacotron* t, int* resident);
+
 /* Measurement only: mean duration (ms) of each decoder-step kernel over up to `reps` eager steps
  * of the last decode's batch, HIP events on the library stream, in launch order: prenet2,
  * attention GRU, query, attention, project_to_decoder_in, decoder GRU 1, decoder GRU 2, mel,

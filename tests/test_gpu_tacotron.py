@@ -245,3 +245,90 @@ def test_fused_query_matches_separate_query_launch(monkeypatch):
         T = a["frames"][b_]
         assert rel_rms(a["linear"][b_, :T].cpu().numpy(), b["linear"][b_, :T].cpu().numpy()) < 1e-5
         assert rel_rms(a["mel"][b_, :T].cpu().numpy(), b["mel"][b_, :T].cpu().numpy()) < 1e-5
+
+
+def _config5_batch(n, seed=4):
+    w = weights_mod()
+    lens = w.synthetic_lengths(n, seed)
+    ids = [w.synthetic_ids(int(L), 200 + b) for b, L in enumerate(lens)]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    style = torch.from_numpy(rng.uniform(0, 1, size=(n, 200, 80)).astype(np.float32))
+    return ids, [b % 4 for b in range(n)], style
+
+
+def _decode_enc(m, enc, lens):
+    out = m.inference_batch(None, enc=enc, lens=lens, postnet=False)
+    return out, dict(m.last_timing)
+
+
+@pytest.mark.parametrize("B", [32, 5])
+def test_resident_decoder_matches_multilaunch(monkeypatch, B):
+    """The resident decoder (tacotron_resident.hip: one launch, each XCD decoding up to 4 sentences
+    with the step weights on its 32 CUs) against the per-step multi-launch path on the same encoder
+    outputs (config-5 shaped batch, full 500-step cap): identical step counts, stop decisions and
+    alignment argmax per step; mel, stop and alignment within 1e-5 (the two differ only in fp32
+    summation order and in alpha = w / sum(w) without the sigmoid normaliser, which cancels)."""
+    gu = load_pkg("generic_utils")
+    cfg = gu.default_config("config_tacotron_gst.json")
+    ids, spk, style = _config5_batch(B)
+    m = gu.setup_model(130, 4, cfg).cuda().eval()
+    L = max(len(x) for x in ids)
+    x = torch.zeros(B, L, dtype=torch.long)
+    lens = [len(s) for s in ids]
+    for b, s in enumerate(ids):
+        x[b, :lens[b]] = torch.from_numpy(s)
+    enc = m.encode(x.cuda(), lens, spk, style)
+    res, tr = _decode_enc(m, enc, lens)
+    assert tr["resident"], "resident decoder did not run"
+    monkeypatch.setenv("TTS_RESIDENT", "0")
+    m2 = gu.setup_model(130, 4, cfg).cuda().eval()
+    ml, tm = _decode_enc(m2, enc, lens)
+    assert not tm["resident"]
+    assert res["steps"] == ml["steps"]
+    for b in range(B):
+        T, S = res["frames"][b], res["steps"][b]
+        a1 = res["align"][b, :S, :lens[b]].cpu().numpy()
+        a2 = ml["align"][b, :S, :lens[b]].cpu().numpy()
+        np.testing.assert_array_equal(a1.argmax(1), a2.argmax(1))
+        assert np.abs(a1 - a2).max() < 1e-5
+        assert torch.all(res["align"][b, :S, lens[b]:] == 0)
+        s1, s2 = res["stop"][b, :S].cpu().numpy(), ml["stop"][b, :S].cpu().numpy()
+        np.testing.assert_array_equal(s1 > 0.6, s2 > 0.6)
+        assert np.abs(s1 - s2).max() < 1e-5
+        assert rel_rms(res["mel"][b, :T].cpu().numpy(), ml["mel"][b, :T].cpu().numpy()) < 1e-5
+        assert torch.all(res["mel"][b, T:] == 0)
+
+
+def test_resident_decoder_deterministic_and_timeout_rerun(monkeypatch):
+    """Two resident runs of the same batch are bitwise identical (fixed reduction orders); with a
+    1-tick hand-off timeout every wait fails, the kernel drains with its status and the batch re-runs
+    on the multi-launch path, bitwise equal to a TTS_RESIDENT=0 handle."""
+    gu = load_pkg("generic_utils")
+    cfg = gu.default_config("config_tacotron_gst.json")
+    ids, spk, style = _config5_batch(6, seed=9)
+    m = gu.setup_model(130, 4, cfg).cuda().eval()
+    m.decoder.max_decoder_steps = 150
+    L = max(len(x) for x in ids)
+    x = torch.zeros(6, L, dtype=torch.long)
+    lens = [len(s) for s in ids]
+    for b, s in enumerate(ids):
+        x[b, :lens[b]] = torch.from_numpy(s)
+    enc = m.encode(x.cuda(), lens, spk, style)
+    r1, t1 = _decode_enc(m, enc, lens)
+    r2, t2 = _decode_enc(m, enc, lens)
+    assert t1["resident"] and t2["resident"]
+    for k in ("mel", "stop", "align"):
+        assert torch.equal(r1[k], r2[k]), k
+    monkeypatch.setenv("TTS_DEC_WAIT_TICKS", "1")
+    mt = gu.setup_model(130, 4, cfg).cuda().eval()
+    mt.decoder.max_decoder_steps = 150
+    rt, tt = _decode_enc(mt, enc, lens)
+    assert not tt["resident"]
+    monkeypatch.delenv("TTS_DEC_WAIT_TICKS")
+    monkeypatch.setenv("TTS_RESIDENT", "0")
+    m0 = gu.setup_model(130, 4, cfg).cuda().eval()
+    m0.decoder.max_decoder_steps = 150
+    r0, _ = _decode_enc(m0, enc, lens)
+    assert rt["steps"] == r0["steps"]
+    for k in ("mel", "stop", "align"):
+        assert torch.equal(rt[k], r0[k]), k

@@ -64,3 +64,55 @@ hipError_t fold_pre1_stop(const float* W1, const float* b1, const float* ws, con
 hipError_t launch_fill_int(int* p, int n, int v, hipStream_t s);
 
 }  // namespace tts
+
+namespace tts {
+
+// Resident decoder for TacotronGST / Tacotron (tacotron_resident.hip): the whole decoder loop of
+// Decoder.inference (layers/tacotron.py:439-470) as ONE launch of 256 workgroups (one per CU).
+// Each XCD runs its own group of up to TR_SPX sentences with a full copy of the step weights held
+// on chip by its 32 CUs (6.7 MB per XCD: 106 VGPRs per thread); every hand-off stays inside the
+// XCD.  Scope: the fast attention configuration (sigmoid norm, forward attention without the eval
+// mask, no location / windowing / transition agent), memory_size == r, B <= 32, L <= 256,
+// nmel <= 512, max_steps <= 1000.
+constexpr int TR_CUS = 256, TR_THREADS = 512, TR_WAVES = TR_THREADS / 64;
+constexpr int TR_SPX = 4;                    // sentences per XCD group
+constexpr int TR_GROUPS = 8;                 // XCD groups
+constexpr int TR_RANKS = 32;                 // CUs per group doing work
+constexpr int TR_CPS = TR_RANKS / TR_SPX;    // attention CUs per sentence (positions split 8 ways)
+constexpr int TR_PPC = 32;                   // encoder positions per attention CU (L <= 256)
+constexpr int TR_LMAX = TR_CPS * TR_PPC;
+constexpr int TR_NMEL_MAX = 512;
+constexpr int TR_STATUS_PLACEMENT = 50;      // an XCD holds fewer than TR_RANKS workgroups
+
+struct TResArgs {
+    // weights, reference layouts (rows picked per XCD rank at run time)
+    const float *a_wih, *a_whh, *a_bih, *a_bhh;  // attention_rnn [768][384], [768][256], [768], [768]
+    const float *g_wih[2], *g_whh[2], *g_bih[2], *g_bhh[2];  // decoder_rnns [768][256] ...
+    const float *w_proj, *b_proj;                // project_to_decoder_in [256][512], [256]
+    const float *w_mel, *b_mel;                  // proj_to_mel [nmel][256], [nmel]
+    const float *w_pre1, *b_pre1;                // prenet layer 0 [256][nmel], [256]
+    const float *w_pre2, *b_pre2;                // prenet layer 1 [128][256], [128]
+    const float* w_q;                            // query_layer [128][256]
+    const float *v, *v_b;                        // attention v [128], [1]
+    const float *w_stop, *b_stop;                // stopnet [256 + nmel], [1]
+    int B, nmel, Lcap, Lalign, max_steps, hist_cap;
+    const int* lens;     // [B] (device)
+    const float* enc;    // [B][Lcap][256]
+    const float* Pt;     // [B][128][Lcap]
+    // initial state: the multi-launch buffers after launch_tacotron_init + the prenet go step
+    const float *pre1, *h_att, *h1, *h2;  // pre1 [B][256]; step 0 reads slot 1 of h_att / h1 / h2
+    int64_t h_pstride;
+    const float* alpha;  // [B][Lcap]
+    float *mel_hist, *stop_hist, *align_hist;  // [B][hist_cap][nmel], [B][hist_cap], [B][hist_cap][Lalign]
+    int *done, *n_steps;
+    unsigned long long* gran;  // tres_granules() granules (zeroed at create)
+    int* status;               // 0 ok; TR_STATUS_PLACEMENT; else the id of the wait that timed out
+    unsigned salt;             // per launch, 18 bits
+    long long timeout_ticks;   // wall_clock64 ticks per wait
+};
+size_t tres_granules();
+size_t tres_smem_bytes();
+hipError_t tres_prepare();
+hipError_t launch_tacotron_resident(const TResArgs& a, hipStream_t s, bool* launched);
+
+}  // namespace tts

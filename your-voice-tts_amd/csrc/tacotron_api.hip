@@ -100,6 +100,13 @@ struct tts_tacotron {
     // sequence workspace (encoder, GST, postnet), grown on demand
     int *ids = nullptr, *T = nullptr, *spk_ids = nullptr, *gT = nullptr;
     Buf bank, p0, y, hwa, hwb, xi, seq_out, pre_a, pre_b, g0, g1, gxi, gh, gst_out, spk_rows;
+    // resident decoder (tacotron_resident.hip): raw-layout weight copies, granules, state
+    bool resident = false;
+    TResArgs rw{};                  // weight pointers (the rest filled per launch)
+    unsigned long long* tr_gran = nullptr;  // tres_granules() granules, then the status word
+    long long res_ticks = 0;
+    unsigned res_salt = 0;
+    int res_timeouts = 0, last_resident = 0;
     // last decode (profiling)
     float last_ms = 0.f;
     int last_steps = 0, last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
@@ -831,6 +838,65 @@ tts_status create_workspace(tts_tacotron* t, hipStream_t s) {
     return TTS_OK;
 }
 
+// The resident decoder serves the attention configuration of config_tacotron_gst.json (sigmoid norm,
+// forward attention without the eval mask, no transition agent / location / windowing) on a GPU
+// with >= 256 compute units; TTS_RESIDENT=0 at create disables it.  Its weights are plain copies of
+// the reference tensors (the kernel picks its rows at launch).
+tts_status create_resident(tts_tacotron* t, const WeightMap& wm, hipStream_t s) {
+    const tts_tacotron_config& c = t->cfg;
+    const char* env = getenv("TTS_RESIDENT");
+    int dev = 0, ncu = 0, rate_khz = 0;
+    if (!(c.attn_norm == 1 && c.forward_attn && !c.trans_agent && !c.forward_attn_mask && !c.location_attn &&
+          !c.windowing && t->nmel <= TR_NMEL_MAX && c.max_steps <= 1000) ||
+        (env && env[0] == '0') || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < TR_CUS ||
+        hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0 ||
+        tres_prepare() != hipSuccess)
+        return TTS_OK;
+    const int nmel = t->nmel;
+    TResArgs& a = t->rw;
+    tts_status st;
+#define CPY(dst, key, n)                      \
+    do {                                      \
+        GET(src_, key, n);                    \
+        float* d_ = nullptr;                  \
+        if ((st = copy_w(t, &d_, src_, (size_t)(n), s))) return st; \
+        dst = d_;                             \
+    } while (0)
+    CPY(a.a_wih, "decoder.attention_rnn.weight_ih", (int64_t)3 * T_DEC * T_XA);
+    CPY(a.a_whh, "decoder.attention_rnn.weight_hh", (int64_t)3 * T_DEC * T_DEC);
+    CPY(a.a_bih, "decoder.attention_rnn.bias_ih", 3 * T_DEC);
+    CPY(a.a_bhh, "decoder.attention_rnn.bias_hh", 3 * T_DEC);
+    for (int i = 0; i < 2; ++i) {
+        const std::string pre = "decoder.decoder_rnns." + std::to_string(i) + ".";
+        CPY(a.g_wih[i], pre + "weight_ih", 3 * T_DEC * T_DEC);
+        CPY(a.g_whh[i], pre + "weight_hh", 3 * T_DEC * T_DEC);
+        CPY(a.g_bih[i], pre + "bias_ih", 3 * T_DEC);
+        CPY(a.g_bhh[i], pre + "bias_hh", 3 * T_DEC);
+    }
+    CPY(a.w_proj, "decoder.project_to_decoder_in.weight", T_DEC * 2 * T_DEC);
+    CPY(a.b_proj, "decoder.project_to_decoder_in.bias", T_DEC);
+    CPY(a.w_mel, "decoder.proj_to_mel.weight", (int64_t)nmel * T_DEC);
+    CPY(a.b_mel, "decoder.proj_to_mel.bias", nmel);
+    CPY(a.w_pre1, "decoder.prenet.layers.0.linear_layer.weight", (int64_t)T_PRE1 * nmel);
+    CPY(a.b_pre1, "decoder.prenet.layers.0.linear_layer.bias", T_PRE1);
+    CPY(a.w_pre2, "decoder.prenet.layers.1.linear_layer.weight", T_PRE2 * T_PRE1);
+    CPY(a.b_pre2, "decoder.prenet.layers.1.linear_layer.bias", T_PRE2);
+    CPY(a.w_q, "decoder.attention_layer.query_layer.linear_layer.weight", ADIM * T_DEC);
+    CPY(a.w_stop, "decoder.stopnet.linear.weight", T_DEC + nmel);
+    CPY(a.b_stop, "decoder.stopnet.linear.bias", 1);
+#undef CPY
+    a.v = t->v;
+    a.v_b = t->v_b;
+    if ((st = talloc(t, &t->tr_gran, tres_granules() + 2))) return st;
+    TTS_HIP(hipMemsetAsync(t->tr_gran, 0, sizeof(unsigned long long) * (tres_granules() + 2), s));
+    t->res_ticks = (long long)rate_khz * 50;  // 50 ms per hand-off wait
+    // fault injection for the timeout fallback test (TTS_DEC_WAIT_TICKS wall-clock ticks)
+    if (const char* tk = getenv("TTS_DEC_WAIT_TICKS"); tk && tk[0]) t->res_ticks = std::max(1LL, atoll(tk));
+    t->resident = true;
+    return TTS_OK;
+}
+
 #undef GET
 
 }  // namespace
@@ -887,6 +953,7 @@ tts_status tts_tacotron_create(const tts_tacotron_config* cfg, const tts_tensor*
     for (int i = 0; i < n_tensors; ++i) wm.m[tensors[i].key] = {tensors[i].data, tensors[i].numel};
     tts_status st = create_weights(t, wm, s);
     if (!st) st = create_workspace(t, s);
+    if (!st) st = create_resident(t, wm, s);
     if (!st && hipStreamSynchronize(s) != hipSuccess) {
         set_error("weight repacking failed");
         st = TTS_ERR_HIP;
@@ -1000,6 +1067,56 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
     ia.n_steps = t->n_steps; ia.state = t->state;
     TTS_HIP(launch_tacotron_init(ia, s));
     { tts_status st = enqueue_prenet_go(t, B, s); if (st) return st; }
+    int run = 0;
+    t->last_resident = 0;
+    if (t->resident && B <= TR_SPX * TR_GROUPS && Lmax <= TR_LMAX) {
+        // one persistent launch runs every step (tacotron_resident.hip), from the state the init
+        // and go-frame launches above left, into the same history buffers
+        TResArgs a = t->rw;
+        a.B = B; a.nmel = t->nmel; a.Lcap = t->Lcap; a.Lalign = Lmax; a.max_steps = max_steps;
+        a.hist_cap = t->hist_cap;
+        a.lens = t->lens; a.enc = t->denc; a.Pt = t->Pt;
+        a.pre1 = t->pre1; a.h_att = t->h_att; a.h1 = t->h1; a.h2 = t->h2; a.h_pstride = (int64_t)t->Bcap * T_DEC;
+        a.alpha = t->alpha;
+        a.mel_hist = t->mel_hist; a.stop_hist = t->stop_hist; a.align_hist = t->align_hist;
+        a.done = t->done; a.n_steps = t->n_steps;
+        a.gran = t->tr_gran;
+        a.status = reinterpret_cast<int*>(t->tr_gran + tres_granules());
+        t->res_salt = (t->res_salt + 1) & 0x3FFFF;
+        if (t->res_salt == 0) t->res_salt = 1;
+        a.salt = t->res_salt;
+        a.timeout_ticks = t->res_ticks;
+        TTS_HIP(hipMemsetAsync(a.status, 0, sizeof(int), s));
+        TTS_HIP(hipEventRecord(t->ev_t0, s));
+        bool launched = false;
+        TTS_HIP(launch_tacotron_resident(a, s, &launched));
+        if (!launched) {
+            // the grid cannot be co-resident on this device: nothing ran, the initial state is
+            // untouched; the multi-launch path serves this handle from now on
+            t->resident = false;
+        } else {
+            TTS_HIP(hipEventRecord(t->ev_t1, s));
+            TTS_HIP(hipMemcpyAsync(t->host_flags, a.status, sizeof(int), hipMemcpyDeviceToHost, s));
+            TTS_HIP(hipMemcpyAsync(n_steps, t->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+            TTS_HIP(hipStreamSynchronize(s));
+            const int code = t->host_flags[0];
+            if (code == 0) {
+                for (int b = 0; b < B; ++b) run = std::max(run, (int)n_steps[b]);
+                t->last_resident = 1;
+            } else {
+                // TR_STATUS_PLACEMENT: some XCD holds fewer than TR_RANKS workgroups, the kernel
+                // stopped before touching any state (multi-launch from now on); otherwise a hand-off
+                // wait timed out (a workgroup could not become resident beside other work) and every
+                // wave drained: this batch re-runs from its initial state on the multi-launch path
+                if (code == TR_STATUS_PLACEMENT) t->resident = false;
+                else ++t->res_timeouts;
+                TTS_HIP(launch_tacotron_init(ia, s));
+                tts_status st = enqueue_prenet_go(t, B, s);
+                if (st) return st;
+            }
+        }
+    }
+    if (!t->last_resident) {
     auto key = std::make_tuple(B, Lmax, max_steps);
     auto it = t->graphs.find(key);
     if (it == t->graphs.end()) {
@@ -1012,7 +1129,6 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
     }
     const TGraphs& g = it->second;
     TTS_HIP(hipEventRecord(t->ev_t0, s));
-    int run = 0;
     auto launch_steps = [&](int n) -> tts_status {
         while (n > 0) {
             if ((run & 1) == 0 && n >= TCHUNK) {
@@ -1040,6 +1156,7 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
     TTS_HIP(hipEventRecord(t->ev_t1, s));
     TTS_HIP(hipMemcpyAsync(n_steps, t->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     TTS_HIP(hipStreamSynchronize(s));
+    }
     int nmax = 0;
     for (int b = 0; b < B; ++b) nmax = std::max(nmax, (int)n_steps[b]);
     const size_t nm = t->nmel;
@@ -1102,6 +1219,12 @@ tts_status tts_tacotron_last_timing(tts_tacotron* t, float* loop_ms, int* steps_
     TTS_CHECK(t && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
     *loop_ms = t->last_ms;
     *steps_run = t->last_steps;
+    return TTS_OK;
+}
+
+tts_status tts_tacotron_last_path(tts_tacotron* t, int* resident) {
+    TTS_CHECK(t && resident, TTS_ERR_INVALID, "null argument");
+    *resident = t->last_resident;
     return TTS_OK;
 }
 

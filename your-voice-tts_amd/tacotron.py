@@ -248,7 +248,9 @@ class TacotronGST:
             out["linear"] = self.postnet(out["mel"], frames)
         ms, ns = ctypes.c_float(), ctypes.c_int()
         lib.tts_tacotron_last_timing(h, ctypes.byref(ms), ctypes.byref(ns))
-        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value)
+        res = ctypes.c_int()
+        lib.tts_tacotron_last_path(h, ctypes.byref(res))
+        self.last_timing = dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value))
         self.last_lengths = frames
         return out
 
