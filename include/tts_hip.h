@@ -307,6 +307,17 @@ tts_status tts_tacotron_last_timing(tts_tacotron* t, float* loop_ms, int* steps_
  * out re-runs the batch on the multi-launch path (reported 0). */
 tts_status tts_tacotron_last_path(tts_tacotron* t, int* resident);
 
+/* Measurement only: re-runs the last resident tts_tacotron_decode batch with phase timers and
+ * returns the mean microseconds per decoder step of each phase on compute units 0 (the attention
+ * leader of sentence 0) and 1 (a non-leader) of XCD 0: us[0..15] and us[16..31] (n >= 32):
+ * 0 wait prenet-1 + continue flags, 1 prenet-2 rows + gather, 2 attention-GRU unit + gather, 3 query
+ * rows + gather, 4 energies / weights / context partial, 5 leader: slice sums + publish, 6 gather
+ * contexts, 7 alignment + project_to_decoder_in + gather, 8 decoder GRU 1 + gather, 9 GRU 2 +
+ * gather, 10 mel rows + gather, 11 prenet-1 rows + stopnet; 12-15 split the compute (up to the
+ * publish) out of 2, 8, 9 and 10. */
+#define TTS_TACOTRON_RESIDENT_PHASES 16
+tts_status tts_tacotron_resident_phases(tts_tacotron* t, float* us, int n);
+
 /* Measurement only: mean duration (ms) of each decoder-step kernel over up to `reps` eager steps
  * of the last decode's batch, HIP events on the library stream, in launch order: prenet2,
  * attention GRU, query, attention, project_to_decoder_in, decoder GRU 1, decoder GRU 2, mel,

@@ -31,7 +31,8 @@ EXPORTS = (
     "tts_gl_set_mel_basis", "tts_gl_melspectrogram",
     "tts_synth_create", "tts_synth_destroy", "tts_synth_run", "tts_synth_sync",
     "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
-    "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_last_path", "tts_tacotron_profile",
+    "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_last_path", "tts_tacotron_resident_phases",
+    "tts_tacotron_profile",
     "tts_last_error", "tts_version",
 )
 
@@ -119,6 +120,7 @@ def _declare(lib):
     lib.tts_tacotron_postnet.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
     lib.tts_tacotron_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_tacotron_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_tacotron_resident_phases.argtypes = [vp, FP, ctypes.c_int]
     lib.tts_tacotron_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_last_error.restype = ctypes.c_char_p
     lib.tts_version.restype = ctypes.c_char_p

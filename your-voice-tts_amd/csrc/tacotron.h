@@ -83,6 +83,7 @@ constexpr int TR_PPC = 32;                   // encoder positions per attention 
 constexpr int TR_LMAX = TR_CPS * TR_PPC;
 constexpr int TR_NMEL_MAX = 512;
 constexpr int TR_STATUS_PLACEMENT = 50;      // an XCD holds fewer than TR_RANKS workgroups
+constexpr int TR_PHASES = 16;                // phase timers (tts_tacotron_resident_phases)
 
 struct TResArgs {
     // weights, reference layouts (rows picked per XCD rank at run time)
@@ -109,6 +110,7 @@ struct TResArgs {
     int* status;               // 0 ok; TR_STATUS_PLACEMENT; else the id of the wait that timed out
     unsigned salt;             // per launch, 18 bits
     long long timeout_ticks;   // wall_clock64 ticks per wait
+    long long* prof;           // null, or [2][TR_PHASES] phase ticks of CUs 0 and 1 of XCD 0 (measurement)
 };
 size_t tres_granules();
 size_t tres_smem_bytes();

@@ -107,6 +107,7 @@ struct tts_tacotron {
     long long res_ticks = 0;
     unsigned res_salt = 0;
     int res_timeouts = 0, last_resident = 0;
+    TResArgs last_ra{};
     // last decode (profiling)
     float last_ms = 0.f;
     int last_steps = 0, last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
@@ -1086,6 +1087,8 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
         if (t->res_salt == 0) t->res_salt = 1;
         a.salt = t->res_salt;
         a.timeout_ticks = t->res_ticks;
+        a.prof = nullptr;
+        t->last_ra = a;
         TTS_HIP(hipMemsetAsync(a.status, 0, sizeof(int), s));
         TTS_HIP(hipEventRecord(t->ev_t0, s));
         bool launched = false;
@@ -1225,6 +1228,46 @@ tts_status tts_tacotron_last_timing(tts_tacotron* t, float* loop_ms, int* steps_
 tts_status tts_tacotron_last_path(tts_tacotron* t, int* resident) {
     TTS_CHECK(t && resident, TTS_ERR_INVALID, "null argument");
     *resident = t->last_resident;
+    return TTS_OK;
+}
+
+tts_status tts_tacotron_resident_phases(tts_tacotron* t, float* us, int n) {
+    TTS_CHECK(t && us && n >= 2 * TR_PHASES, TTS_ERR_INVALID, "bad arguments");
+    TTS_CHECK(t->last_resident && t->last_steps > 0, TTS_ERR_INVALID,
+              "tts_tacotron_resident_phases needs a previous resident tts_tacotron_decode");
+    TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else on the device
+    hipStream_t s = t->stream;
+    long long* prof = nullptr;
+    TTS_HIP(hipMalloc(&prof, sizeof(long long) * 2 * TR_PHASES));
+    TTS_HIP(hipMemsetAsync(prof, 0, sizeof(long long) * 2 * TR_PHASES, s));
+    TTS_HIP(launch_tacotron_init(t->last_init, s));
+    tts_status st = enqueue_prenet_go(t, t->last_B, s);
+    TResArgs a = t->last_ra;
+    a.prof = prof;
+    t->res_salt = (t->res_salt + 1) & 0x3FFFF;
+    if (t->res_salt == 0) t->res_salt = 1;
+    a.salt = t->res_salt;
+    if (!st) {
+        TTS_HIP(hipMemsetAsync(a.status, 0, sizeof(int), s));
+        bool launched = false;
+        TTS_HIP(launch_tacotron_resident(a, s, &launched));
+        if (!launched) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(prof);
+            TTS_CHECK(false, TTS_ERR_UNSUPPORTED, "resident decoder cannot be co-resident on this device now");
+        }
+    }
+    long long h[2 * TR_PHASES];
+    TTS_HIP(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipMemcpyAsync(t->host_flags, a.status, sizeof(int), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipStreamSynchronize(s));
+    (void)hipFree(prof);
+    if (st) return st;
+    TTS_CHECK(t->host_flags[0] == 0, TTS_ERR_HIP, "resident decoder: a hand-off wait timed out");
+    int dev = 0, rate_khz = 1;
+    TTS_HIP(hipGetDevice(&dev));
+    TTS_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));
+    for (int i = 0; i < 2 * TR_PHASES; ++i) us[i] = (float)(1e3 * (double)h[i] / rate_khz / t->last_steps);
     return TTS_OK;
 }
 

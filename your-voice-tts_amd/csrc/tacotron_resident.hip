@@ -77,7 +77,8 @@ constexpr int L_BIAS = L_STOP + TD + TR_NMEL_MAX;        // [8 waves][16] per-wa
 constexpr int L_CTL = L_BIAS + TR_WAVES * 16;            // [SPX] normaliser, [SPX] tail, [SPX][8] bnd, ints
 constexpr int L_W1 = L_CTL + TR_SPX * (2 + TR_CPS) + 32; // [8 waves][8][64] prenet-L1 row U (lane-strided)
 constexpr int L_WM = L_W1 + TR_WAVES * 8 * 64;           // [8 waves][8][64] proj_to_mel rows m0 (0-3), m1 (4-7)
-constexpr int L_TOTAL = L_WM + TR_WAVES * 8 * 64;
+constexpr int L_PROF = L_WM + TR_WAVES * 8 * 64;          // [TR_PHASES] u64 phase timers (measurement)
+constexpr int L_TOTAL = L_PROF + 2 * TR_PHASES;
 
 __device__ __forceinline__ void publish(u64* g, unsigned tag, float v) {
     __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
@@ -131,6 +132,26 @@ __device__ __forceinline__ float lds_dot(const float* w, const float* x, int n, 
     for (int i = 0; i < n; ++i) s = fmaf(w[i], x[lane + 64 * i], s);
     return s;
 }
+// p[s] = sum_{i < N} w[i] * x[s * ld + lane + 64 i] for the group's four sentences (interleaved)
+template <int N>
+__device__ __forceinline__ void dot4(float (&p)[TR_SPX], const float* w, const float* x, int ld, int lane) {
+#pragma unroll
+    for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(w[i], x[s * ld + lane + 64 * i], p[s]);
+}
+// the wave totals of p[0..3] (four independent reductions), total s returned in lane s
+__device__ __forceinline__ float to_lanes(const float (&p)[TR_SPX], int lane) {
+    float out = 0.f;
+#pragma unroll
+    for (int s = 0; s < TR_SPX; ++s) {
+        const float v = wave_sum_dpp(p[s]);
+        out = lane == s ? v : out;
+    }
+    return out;
+}
 __device__ __forceinline__ float lds_dot2(const float* w, const float* x, int n, int lane) {
     // sum_{i < n} w[64 i + lane] * x[lane + 64 i] (both in LDS)
     float s = 0.f;
@@ -145,6 +166,16 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
     extern __shared__ __align__(16) float sm[];
     int* ctl = reinterpret_cast<int*>(sm + L_CTL + TR_SPX * (2 + TR_CPS));  // [0] abort, [1] rank, [2] nx, [3] all done, [4..8) done
     const long long tmo = a.timeout_ticks;
+    // phase timers (measurement only, tts_tacotron_resident_phases): CUs 0 and 1 of group 0
+    bool prof = false;
+    long long plast = 0;
+    unsigned long long* pacc = reinterpret_cast<unsigned long long*>(sm + L_PROF);
+#define MARK(k)                                                 \
+    if (prof && tid == 0) {                                     \
+        const long long now_ = (long long)wall_clock64();       \
+        pacc[k] += (unsigned long long)(now_ - plast);          \
+        plast = now_;                                           \
+    }
     // ---- XCD discovery: rank = #CUs of this XCD with a lower block index
     int xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -177,6 +208,8 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
     __syncthreads();
     if (ctl[0]) return;
     const int r = ctl[1];
+    prof = a.prof != nullptr && xcc == 0 && r < 2;
+    if (prof && tid < TR_PHASES) pacc[tid] = 0;
     const int b0 = xcc * TR_SPX;                         // this group's first sentence
     const int ns = min(TR_SPX, a.B - b0);                // its sentences
     if (r >= TR_RANKS || ns <= 0) return;                // idle CU / group
@@ -306,6 +339,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
     float* mel = sm + L_MEL;
     float* q = sm + L_Q;
     float* red = sm + L_RED;
+    if (prof && tid == 0) plast = (long long)wall_clock64();
     for (int t = 0;; ++t) {
         // the lane index as an opaque per-step value: the hand-off indices below are recomputed
         // every step instead of being hoisted out of the loop as 64-bit offsets (register budget)
@@ -321,101 +355,104 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         float* h1 = sm + L_H1 + (t & 1) * TR_SPX * TD;
         float* h2_prev = sm + L_H2 + ((t + 1) & 1) * TR_SPX * TD;
         float* h2 = sm + L_H2 + (t & 1) * TR_SPX * TD;
+        // gathers: wave w fetches half gf = (w >> 2) of sentence (w & 3)'s vector
+        const int gs = wave & 3, gf = wave >> 2;
+        const bool gon = gs < ns;
         // ---- 0) prenet L1 of this step (+ the continue flags), from step t-1
         if (t > 0) {
-            if (wave < TR_SPX) {  // wave s gathers sentence s's 256 values (+ wave 0 the flags)
-                const int s = wave;
-                float v5[5];
-                const bool ok = sweep<5>(Gp + G_PRE1, Ep + P_PRE1, v5, [&](int i) {
-                    if (s >= ns) return -1;
-                    if (i < 4) return s * T_PRE1 + ln * 4 + i;
-                    return (s == 0 && ln < ns) ? TR_SPX * T_PRE1 + ln : -1;
+            if (gon) {
+                float v3[3];
+                const bool ok = sweep<3>(Gp + G_PRE1, Ep + P_PRE1, v3, [&](int i) {
+                    if (i < 2) return gs * T_PRE1 + gf * 128 + ln + 64 * i;
+                    return (wave == 0 && ln < ns) ? TR_SPX * T_PRE1 + ln : -1;
                 }, tmo);
-                if (s < ns)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) pre1[s * T_PRE1 + lane * 4 + i] = v5[i];
-                if (s == 0 && lane < ns) dn[lane] = v5[4] == 0.f ? 1 : 0;
+                pre1[gs * T_PRE1 + gf * 128 + lane] = v3[0];
+                pre1[gs * T_PRE1 + gf * 128 + 64 + lane] = v3[1];
+                if (wave == 0 && lane < ns) dn[lane] = v3[2] == 0.f ? 1 : 0;
                 if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 1); }
             }
             __syncthreads();
             if (ctl[0]) return;
             bool all = true;
             for (int s = 0; s < ns; ++s) all = all && dn[s];
+            MARK(0);
             if (all) break;
         }
         // ---- 1) prenet L2 (waves 0-3, row 4r + w) -> xa[s][0:128]
         if (wave < 4) {
-            for (int s = 0; s < ns; ++s) {
-                const float v = wave_sum_dpp(lds_dot(w2q, pre1 + s * T_PRE1, 4, lane));
-                if (lane == 0) publish(G + G_PRE2 + s * T_PRE2 + r2, E + P_PRE2, fmaxf(v + bias[14], 0.f));
-            }
+            float p[TR_SPX];
+            dot4<4>(p, w2q, pre1, T_PRE1, lane);
+            const float v = to_lanes(p, lane);
+            if (lane < ns) publish(G + G_PRE2 + lane * T_PRE2 + r2, E + P_PRE2, fmaxf(v + bias[14], 0.f));
         }
-        if (wave < TR_SPX && wave < ns) {  // wave s gathers sentence s
-            const int s = wave;
-            float v2[2];
-            const bool ok = sweep<2>(G + G_PRE2, E + P_PRE2, v2, [&](int i) { return s * T_PRE2 + ln + 64 * i; }, tmo);
-            xa[s * TXA + lane] = v2[0];
-            xa[s * TXA + 64 + lane] = v2[1];
+        if (gon) {
+            float v1[1];
+            const bool ok = sweep<1>(G + G_PRE2, E + P_PRE2, v1, [&](int i) { return gs * T_PRE2 + gf * 64 + ln; }, tmo);
+            xa[gs * TXA + gf * 64 + lane] = v1[0];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 2); }
         }
         __syncthreads();
         if (ctl[0]) return;
-        // ---- 2) attention GRU, unit U: x = [prenet | ctx_{t-1}], h = h_att_{t-1} (:370)
-        for (int s = 0; s < ns; ++s) {
-            const float* x = xa + s * TXA;
-            const float* h = hatt_prev + s * TD;
-            float pr = 0.f, pz = 0.f, pn = 0.f, qn = 0.f;
+        MARK(1);
+        // ---- 2) attention GRU, unit U: x = [prenet | ctx_{t-1}], h = h_att_{t-1} (:370); the four
+        // sentences' dot products interleaved, sentence s finished by lane s
+        {
+            float pr[TR_SPX], pz[TR_SPX], pn[TR_SPX], qn[TR_SPX];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const float xv = x[lane + 64 * i];
-                pr = fmaf(axr[i], xv, pr);
-                pz = fmaf(axz[i], xv, pz);
-                pn = fmaf(axn[i], xv, pn);
-            }
+            for (int s = 0; s < TR_SPX; ++s) pr[s] = pz[s] = pn[s] = qn[s] = 0.f;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float hv = h[lane + 64 * i];
-                pr = fmaf(ahr[i], hv, pr);
-                pz = fmaf(ahz[i], hv, pz);
-                qn = fmaf(ahn[i], hv, qn);
-            }
-            pr = wave_sum_dpp(pr);
-            pz = wave_sum_dpp(pz);
-            pn = wave_sum_dpp(pn);
-            qn = wave_sum_dpp(qn);
-            if (lane == 0) {
-                const float rg = sigmoidf_(pr + bias[0]);
-                const float zg = sigmoidf_(pz + bias[1]);
-                const float ng = tanhf((pn + bias[2]) + rg * (qn + bias[3]));
-                publish(G + G_HATT + s * TD + U, E + P_HATT, (h[U] - ng) * zg + ng);
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) {
+                    const float xv = xa[s * TXA + lane + 64 * i];
+                    pr[s] = fmaf(axr[i], xv, pr[s]);
+                    pz[s] = fmaf(axz[i], xv, pz[s]);
+                    pn[s] = fmaf(axn[i], xv, pn[s]);
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) {
+                    const float hv = hatt_prev[s * TD + lane + 64 * i];
+                    pr[s] = fmaf(ahr[i], hv, pr[s]);
+                    pz[s] = fmaf(ahz[i], hv, pz[s]);
+                    qn[s] = fmaf(ahn[i], hv, qn[s]);
+                }
+            const float R = to_lanes(pr, lane), Z = to_lanes(pz, lane), N = to_lanes(pn, lane), Q = to_lanes(qn, lane);
+            if (lane < ns) {
+                const float rg = sigmoidf_(R + bias[0]);
+                const float zg = sigmoidf_(Z + bias[1]);
+                const float ng = tanhf((N + bias[2]) + rg * (Q + bias[3]));
+                publish(G + G_HATT + lane * TD + U, E + P_HATT, (hatt_prev[lane * TD + U] - ng) * zg + ng);
             }
         }
-        if (wave < TR_SPX && wave < ns) {
-            const int s = wave;
-            float v4[4];
-            const bool ok = sweep<4>(G + G_HATT, E + P_HATT, v4, [&](int i) { return s * TD + ln + 64 * i; }, tmo);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) hatt[s * TD + lane + 64 * i] = v4[i];
+        MARK(12);
+        if (gon) {
+            float v2[2];
+            const bool ok = sweep<2>(G + G_HATT, E + P_HATT, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo);
+            hatt[gs * TD + gf * 128 + lane] = v2[0];
+            hatt[gs * TD + gf * 128 + 64 + lane] = v2[1];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 3); }
         }
         __syncthreads();
         if (ctl[0]) return;
+        MARK(2);
         // ---- 3) query_layer (waves 4-7, row 4r + w - 4) over h_att_t (common_layers.py:179)
         if (wave >= 4) {
-            for (int s = 0; s < ns; ++s) {
-                const float v = wave_sum_dpp(lds_dot(w2q, hatt + s * TD, 4, lane));
-                if (lane == 0) publish(G + G_Q + s * ADIM + r2, E + P_Q, v);
-            }
+            float p[TR_SPX];
+            dot4<4>(p, w2q, hatt, TD, lane);
+            const float v = to_lanes(p, lane);
+            if (lane < ns) publish(G + G_Q + lane * ADIM + r2, E + P_Q, v);
         }
-        if (att_on && wave == 0) {
-            float v2[2];
-            const bool ok = sweep<2>(G + G_Q, E + P_Q, v2, [&](int i) { return sa * ADIM + ln + 64 * i; }, tmo);
-            q[lane] = v2[0];
-            q[64 + lane] = v2[1];
+        if (att_on && wave < 2) {
+            float v1[1];
+            const bool ok = sweep<1>(G + G_Q, E + P_Q, v1, [&](int i) { return sa * ADIM + wave * 64 + ln; }, tmo);
+            q[wave * 64 + lane] = v1[0];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 4); }
         }
         __syncthreads();
         if (ctl[0]) return;
+        MARK(3);
         // ---- 4) attention over this CU's 32 positions (common_layers.py:178-182, 199-217, 241-243)
         if (att_on) {
             const int jl = tid >> 4, dc = tid & 15;
@@ -459,6 +496,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                 const int jt = La - 1 - j0;
                 publish(gp + TD + 2, E + P_ATTP, (jt >= 0 && jt < TR_PPC) ? wj[jt] : 0.f);
             }
+            MARK(4);
             // the sentence's first CU adds the 8 slices' partials in slice order
             if (ka == 0) {
                 float v8[TR_CPS];
@@ -488,25 +526,28 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                     const int k = tid - TD - 2;
                     publish(gc + TD + 2 + k, E + P_CTXF, red[280 + k] / W);         // alpha at slice ends
                 }
+                MARK(5);
             }
         }
         // everyone: the contexts, normalisers, tails and boundary alphas of the group's sentences
-        if (wave < TR_SPX && wave < ns) {
-            const int s = wave;
-            float v5[5];
-            const bool ok = sweep<5>(G + G_CTXF, E + P_CTXF, v5, [&](int i) {
-                const int k = ln + 64 * i;
-                return k < TD + 2 + TR_CPS ? s * CTXF_W + k : -1;
+        if (gon) {
+            float v3[3];
+            const bool ok = sweep<3>(G + G_CTXF, E + P_CTXF, v3, [&](int i) {
+                if (i < 2) return gs * CTXF_W + gf * 128 + ln + 64 * i;
+                return (gf == 1 && ln < 2 + TR_CPS) ? gs * CTXF_W + TD + ln : -1;
             }, tmo);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) xa[s * TXA + T_PRE2 + lane + 64 * i] = v5[i];
-            if (lane == 0) nrm[s] = v5[4];
-            if (lane == 1) tl[s] = v5[4];
-            if (lane >= 2 && lane < 2 + TR_CPS) bnd[s * TR_CPS + lane - 2] = v5[4];
+            xa[gs * TXA + T_PRE2 + gf * 128 + lane] = v3[0];
+            xa[gs * TXA + T_PRE2 + gf * 128 + 64 + lane] = v3[1];
+            if (gf == 1) {
+                if (lane == 0) nrm[gs] = v3[2];
+                if (lane == 1) tl[gs] = v3[2];
+                if (lane >= 2 && lane < 2 + TR_CPS) bnd[gs * TR_CPS + lane - 2] = v3[2];
+            }
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 6); }
         }
         __syncthreads();
         if (ctl[0]) return;
+        MARK(6);
         if (att_on) {
             // this step's alpha at this CU's positions (next step's prev_alpha) and the alignment row
             if (tid < TR_PPC) {
@@ -519,25 +560,31 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             if (tid == TR_PPC) al[TR_PPC] = ka > 0 ? bnd[sa * TR_CPS + ka - 1] : 0.f;
         }
         // ---- 5) project_to_decoder_in, row U, over [h_att_t | ctx_t] (:373-375)
-        for (int s = 0; s < ns; ++s) {
-            float p = 0.f;
+        {
+            float p[TR_SPX];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) p = fmaf(wp[i], hatt[s * TD + lane + 64 * i], p);
+            for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
 #pragma unroll
-            for (int i = 4; i < 8; ++i) p = fmaf(wp[i], xa[s * TXA + T_PRE2 + lane + 64 * (i - 4)], p);
-            p = wave_sum_dpp(p);
-            if (lane == 0) publish(G + G_DIN + s * TD + U, E + P_DIN, p + bias[12]);
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(wp[i], hatt[s * TD + lane + 64 * i], p[s]);
+#pragma unroll
+            for (int i = 4; i < 8; ++i)
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(wp[i], xa[s * TXA + T_PRE2 + lane + 64 * (i - 4)], p[s]);
+            const float v = to_lanes(p, lane);
+            if (lane < ns) publish(G + G_DIN + lane * TD + U, E + P_DIN, v + bias[12]);
         }
-        if (wave < TR_SPX && wave < ns) {
-            const int s = wave;
-            float v4[4];
-            const bool ok = sweep<4>(G + G_DIN, E + P_DIN, v4, [&](int i) { return s * TD + ln + 64 * i; }, tmo);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) din[s * TD + lane + 64 * i] = v4[i];
+        if (gon) {
+            float v2[2];
+            const bool ok = sweep<2>(G + G_DIN, E + P_DIN, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo);
+            din[gs * TD + gf * 128 + lane] = v2[0];
+            din[gs * TD + gf * 128 + 64 + lane] = v2[1];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 7); }
         }
         __syncthreads();
         if (ctl[0]) return;
+        MARK(7);
         // ---- 6, 7) decoder GRUs with residuals (:377-382): x -> h' = GRU(x, h); out = h' + x
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
@@ -547,115 +594,142 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             float* Dn = g == 0 ? d1 : d2;
             u64* gg = G + (g == 0 ? G_H1 : G_H2);
             const unsigned tg = E + (g == 0 ? P_H1 : P_H2);
-            for (int s = 0; s < ns; ++s) {
-                float pr = 0.f, pz = 0.f, pn = 0.f, qn = 0.f;
+            {
+                float pr[TR_SPX], pz[TR_SPX], pn[TR_SPX], qn[TR_SPX];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float xv = X[s * TD + lane + 64 * i];
-                    const float hv = Hp[s * TD + lane + 64 * i];
-                    pr = fmaf(gx[g][0][i], xv, pr);
-                    pz = fmaf(gx[g][1][i], xv, pz);
-                    pn = fmaf(gx[g][2][i], xv, pn);
-                    pr = fmaf(gh[g][0][i], hv, pr);
-                    pz = fmaf(gh[g][1][i], hv, pz);
-                    qn = fmaf(gh[g][2][i], hv, qn);
-                }
-                pr = wave_sum_dpp(pr);
-                pz = wave_sum_dpp(pz);
-                pn = wave_sum_dpp(pn);
-                qn = wave_sum_dpp(qn);
-                if (lane == 0) {
-                    const float rg = sigmoidf_(pr + bias[4 + 4 * g]);
-                    const float zg = sigmoidf_(pz + bias[5 + 4 * g]);
-                    const float ng = tanhf((pn + bias[6 + 4 * g]) + rg * (qn + bias[7 + 4 * g]));
-                    const float hn = (Hp[s * TD + U] - ng) * zg + ng;
-                    publish(gg + s * TD + U, tg, hn);
-                    publish(gg + TR_SPX * TD + s * TD + U, tg, hn + X[s * TD + U]);
+                for (int s = 0; s < TR_SPX; ++s) pr[s] = pz[s] = pn[s] = qn[s] = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int s = 0; s < TR_SPX; ++s) {
+                        const float xv = X[s * TD + lane + 64 * i];
+                        const float hv = Hp[s * TD + lane + 64 * i];
+                        pr[s] = fmaf(gx[g][0][i], xv, pr[s]);
+                        pz[s] = fmaf(gx[g][1][i], xv, pz[s]);
+                        pn[s] = fmaf(gx[g][2][i], xv, pn[s]);
+                        pr[s] = fmaf(gh[g][0][i], hv, pr[s]);
+                        pz[s] = fmaf(gh[g][1][i], hv, pz[s]);
+                        qn[s] = fmaf(gh[g][2][i], hv, qn[s]);
+                    }
+                const float R = to_lanes(pr, lane), Z = to_lanes(pz, lane), N = to_lanes(pn, lane),
+                            Q = to_lanes(qn, lane);
+                if (lane < ns) {
+                    const float rg = sigmoidf_(R + bias[4 + 4 * g]);
+                    const float zg = sigmoidf_(Z + bias[5 + 4 * g]);
+                    const float ng = tanhf((N + bias[6 + 4 * g]) + rg * (Q + bias[7 + 4 * g]));
+                    const float hn = (Hp[lane * TD + U] - ng) * zg + ng;
+                    publish(gg + lane * TD + U, tg, hn);
+                    publish(gg + TR_SPX * TD + lane * TD + U, tg, hn + X[lane * TD + U]);
                 }
             }
-            if (wave < TR_SPX && wave < ns) {
-                const int s = wave;
-                float v8[8];
-                const bool ok = sweep<8>(gg, tg, v8, [&](int i) {
-                    return (i < 4 ? s * TD : TR_SPX * TD + s * TD) + ln + 64 * (i & 3);
+            MARK(13 + g);
+            if (gon) {
+                float v4[4];
+                const bool ok = sweep<4>(gg, tg, v4, [&](int i) {
+                    return (i < 2 ? 0 : TR_SPX * TD) + gs * TD + gf * 128 + ln + 64 * (i & 1);
                 }, tmo);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    Hn[s * TD + lane + 64 * i] = v8[i];
-                    Dn[s * TD + lane + 64 * i] = v8[4 + i];
-                }
+                Hn[gs * TD + gf * 128 + lane] = v4[0];
+                Hn[gs * TD + gf * 128 + 64 + lane] = v4[1];
+                Dn[gs * TD + gf * 128 + lane] = v4[2];
+                Dn[gs * TD + gf * 128 + 64 + lane] = v4[3];
                 if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 10 + g); }
             }
             __syncthreads();
             if (ctl[0]) return;
+            MARK(8 + g);
         }
         // ---- 8) output = sigmoid(proj_to_mel(decoder_output)), rows m0, m1 (:385-386) -> history
-        for (int s = 0; s < ns; ++s) {
-            const float* x = d2 + s * TD;
-            const float v0 = wave_sum_dpp(lds_dot2(wm, x, 4, lane));
-            const float v1 = wave_sum_dpp(lds_dot2(wm + 4 * 64, x, 4, lane));
-            if (lane == 0) {
-                const int b = b0 + s;
+        {
+            float p0[TR_SPX], p1[TR_SPX];
+#pragma unroll
+            for (int s = 0; s < TR_SPX; ++s) p0[s] = p1[s] = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float w0 = wm[64 * i + lane], w1_ = wm[64 * (4 + i) + lane];
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) {
+                    const float xv = d2[s * TD + lane + 64 * i];
+                    p0[s] = fmaf(w0, xv, p0[s]);
+                    p1[s] = fmaf(w1_, xv, p1[s]);
+                }
+            }
+            const float v0 = to_lanes(p0, lane), v1 = to_lanes(p1, lane);
+            if (lane < ns) {
+                const int b = b0 + lane;
                 if (m0 < nmel) {
                     const float o = sigmoidf_(v0 + bm0);
-                    publish(G + G_MEL + s * TR_NMEL_MAX + m0, E + P_MEL, o);
+                    publish(G + G_MEL + lane * TR_NMEL_MAX + m0, E + P_MEL, o);
                     if (t < a.hist_cap) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m0] = o;
                 }
                 if (m1 < nmel) {
                     const float o = sigmoidf_(v1 + bm1);
-                    publish(G + G_MEL + s * TR_NMEL_MAX + m1, E + P_MEL, o);
+                    publish(G + G_MEL + lane * TR_NMEL_MAX + m1, E + P_MEL, o);
                     if (t < a.hist_cap) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m1] = o;
                 }
             }
         }
-        if (wave < TR_SPX && wave < ns) {
-            const int s = wave;
-            float v8[8];
-            const bool ok = sweep<8>(G + G_MEL, E + P_MEL, v8, [&](int i) {
-                const int k = ln + 64 * i;
-                return k < nmel ? s * TR_NMEL_MAX + k : -1;
+        MARK(15);
+        if (gon) {
+            float v4[4];
+            const bool ok = sweep<4>(G + G_MEL, E + P_MEL, v4, [&](int i) {
+                const int k = gf * 256 + ln + 64 * i;
+                return k < nmel ? gs * TR_NMEL_MAX + k : -1;
             }, tmo);
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (lane + 64 * i < nmel) mel[s * TR_NMEL_MAX + lane + 64 * i] = v8[i];
+            for (int i = 0; i < 4; ++i)
+                if (gf * 256 + lane + 64 * i < nmel) mel[gs * TR_NMEL_MAX + gf * 256 + lane + 64 * i] = v4[i];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 12); }
         }
         __syncthreads();
         if (ctl[0]) return;
-        // ---- 9) prenet L1 of step t+1, row U (memory = this output, memory_size == r: :396-404)
-        for (int s = 0; s < ns; ++s) {
-            const float v = wave_sum_dpp(lds_dot2(w1, mel + s * TR_NMEL_MAX, 8, lane));
-            if (lane == 0) publish(G + G_PRE1 + s * T_PRE1 + U, E + P_PRE1, fmaxf(v + bias[13], 0.f));
-        }
-        // stopnet over [decoder_output | output] + stop rule (:388-393, 459-469), rank 0, wave 0
-        if (r == 0 && wave == 0) {
-            for (int s = 0; s < ns; ++s) {
-                float p = 0.f;
+        MARK(10);
+        // ---- 9) stopnet over [decoder_output | output] + stop rule (:388-393, 459-469): rank 0, wave s
+        // for sentence s, published before the prenet rows so it is off the critical path
+        if (r == 0 && wave < ns) {
+            const int s = wave;
+            float p = 0.f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) p = fmaf(sm[L_STOP + lane + 64 * i], d2[s * TD + lane + 64 * i], p);
+            for (int i = 0; i < 4; ++i) p = fmaf(sm[L_STOP + lane + 64 * i], d2[s * TD + lane + 64 * i], p);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) p = fmaf(sm[L_STOP + TD + lane + 64 * i], mel[s * TR_NMEL_MAX + lane + 64 * i], p);
-                p = wave_sum_dpp(p);
-                if (lane == 0) {
-                    const int b = b0 + s;
-                    int nd = dn[s];
-                    if (!nd) {
-                        const float stv = sigmoidf_(p + bstop);
-                        if (t < a.hist_cap) a.stop_hist[(int64_t)b * a.hist_cap + t] = stv;
-                        // t = step + 1 after the append: t > L/4 and (stop > 0.6 [float32] or
-                        // alignment[-1] > 0.6 [double]); elif t > max_decoder_steps
-                        const int t1 = t + 1;
-                        if ((4 * t1 > Ls[s] && (stv > 0.6f || (double)tl[s] > 0.6)) || t1 > a.max_steps) {
-                            nd = 1;
-                            a.done[b] = 1;
-                            a.n_steps[b] = t1;
-                        }
+            for (int i = 0; i < 8; ++i) p = fmaf(sm[L_STOP + TD + lane + 64 * i], mel[s * TR_NMEL_MAX + lane + 64 * i], p);
+            p = wave_sum_dpp(p);
+            if (lane == 0) {
+                const int b = b0 + s;
+                int nd = dn[s];
+                if (!nd) {
+                    const float stv = sigmoidf_(p + bstop);
+                    if (t < a.hist_cap) a.stop_hist[(int64_t)b * a.hist_cap + t] = stv;
+                    // t = step + 1 after the append: t > L/4 and (stop > 0.6 [float32] or
+                    // alignment[-1] > 0.6 [double]); elif t > max_decoder_steps
+                    const int t1 = t + 1;
+                    if ((4 * t1 > Ls[s] && (stv > 0.6f || (double)tl[s] > 0.6)) || t1 > a.max_steps) {
+                        nd = 1;
+                        a.done[b] = 1;
+                        a.n_steps[b] = t1;
                     }
-                    publish(G + G_PRE1 + TR_SPX * T_PRE1 + s, E + P_PRE1, nd ? 0.f : 1.f);
                 }
+                publish(G + G_PRE1 + TR_SPX * T_PRE1 + s, E + P_PRE1, nd ? 0.f : 1.f);
             }
         }
+        // prenet L1 of step t+1, row U (memory = this output, memory_size == r: :396-404)
+        {
+            float p[TR_SPX];
+#pragma unroll
+            for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float w = w1[64 * i + lane];
+#pragma unroll
+                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(w, mel[s * TR_NMEL_MAX + lane + 64 * i], p[s]);
+            }
+            const float v = to_lanes(p, lane);
+            if (lane < ns) publish(G + G_PRE1 + lane * T_PRE1 + U, E + P_PRE1, fmaxf(v + bias[13], 0.f));
+        }
+        MARK(11);
     }
+    __syncthreads();
+    if (prof && tid < TR_PHASES) a.prof[r * TR_PHASES + tid] = (long long)pacc[tid];
+#undef MARK
 }
 
 }  // namespace

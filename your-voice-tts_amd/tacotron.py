@@ -284,6 +284,20 @@ class TacotronGST:
         _native.check(lib.tts_tacotron_profile(h, int(reps), ms, n), "tts_tacotron_profile")
         return dict(zip(_native.TACOTRON_STEP_KERNELS, [float(v) for v in ms]))
 
+    RESIDENT_PHASES = ("wait_pre1", "pre2_gather", "att_gru_gather", "query_gather", "attention_partial",
+                       "leader_sum", "ctx_gather", "proj_gather", "gru1_gather", "gru2_gather", "mel_gather",
+                       "pre1_stop", "att_gru_compute", "gru1_compute", "gru2_compute", "mel_compute")
+
+    def profile_resident_phases(self):
+        """Mean µs per decoder step of each phase of the resident decoder (last batch re-run with
+        timers; measurement only): {"cu0": {...}, "cu1": {...}} (cu0 = an attention leader)."""
+        lib, h = self._handle(1, 1)
+        k = len(self.RESIDENT_PHASES)
+        us = (ctypes.c_float * (2 * k))()
+        _native.check(lib.tts_tacotron_resident_phases(h, us, 2 * k), "tts_tacotron_resident_phases")
+        return {"cu0": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[:k]])),
+                "cu1": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[k:]]))}
+
     __call__ = inference
 
 
