@@ -101,14 +101,18 @@ __device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx
     long long t_end = 0;
     for (int spin = 0;; ++spin) {
         bool ok = true;
+        // every load issued unconditionally (a slot with idx < 0 re-reads slot 0 and is ignored), so
+        // the N loads of a poll are in flight together
+        u64 x[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
             const int k = idx(i);
-            if (k >= 0) {
-                const u64 x = peek(g + k);
-                v[i] = __uint_as_float((unsigned)x);
-                ok = ok && (unsigned)(x >> 32) == tag;
-            }
+            x[i] = peek(g + (k >= 0 ? k : 0));
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            v[i] = __uint_as_float((unsigned)x[i]);
+            ok = ok & ((idx(i) < 0) | ((unsigned)(x[i] >> 32) == tag));  // no short-circuit branches
         }
         if (__all(ok)) return true;
         if (spin == 0) {
@@ -126,37 +130,60 @@ __device__ __forceinline__ float row_sum16(float v) {
     v += dpp_move<0x118, 0xf>(v, 0.f);
     return v;
 }
-__device__ __forceinline__ float lds_dot(const float* w, const float* x, int n, int lane) {
-    // sum_{i < n} w[i] * x[lane + 64 i] (w in registers, x in LDS)
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s = fmaf(w[i], x[lane + 64 * i], s);
-    return s;
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_all(float v) {  // full-wave DPP move, every lane written
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-// p[s] = sum_{i < N} w[i] * x[s * ld + lane + 64 i] for the group's four sentences (interleaved)
-template <int N>
+// partner of `lane` at halving stage st (0..3): xor 32, xor 16, xor 8, mirror within 8 (xor 7);
+// every pair differs in bit 5 - st, which picks the half a lane keeps
+template <int ST>
+__device__ __forceinline__ float partner(float v) {
+    if constexpr (ST == 0) return __shfl_xor(v, 32, 64);
+    else if constexpr (ST == 1) return __shfl_xor(v, 16, 64);
+    else if constexpr (ST == 2) return dpp_all<0x128>(v);  // row_ror:8
+    else return dpp_all<0x141>(v);                         // row_half_mirror
+}
+// Transposed wave reduction of N in {4, 8, 16} per-lane partial sums: log2(N) halving stages
+// (each lane keeps half of its values, adding its partner's copy of them), then plain sums over
+// the remaining lane bits.  The total of value k ends in lane (64 / N) k (and its neighbours
+// (64 / N) k + 1..3); 2 N - 1 + (6 - log2 N) lane moves instead of 6 N.  Fixed order per value.
+template <int N, int ST = 0>
+__device__ __forceinline__ float xreduce(const float (&v)[N], int lane) {
+    if constexpr (N == 1) {
+        float x = v[0];
+        if constexpr (ST <= 0) x += partner<0>(x);
+        if constexpr (ST <= 1) x += partner<1>(x);
+        if constexpr (ST <= 2) x += partner<2>(x);
+        if constexpr (ST <= 3) x += partner<3>(x);
+        x += dpp_all<0x4E>(x);  // quad_perm [2,3,0,1]
+        x += dpp_all<0xB1>(x);  // quad_perm [1,0,3,2]
+        return x;
+    } else {
+        const bool hi = (lane >> (5 - ST)) & 1;
+        float w[N / 2];
+#pragma unroll
+        for (int k = 0; k < N / 2; ++k) {
+            const float keep = hi ? v[k + N / 2] : v[k];
+            const float send = hi ? v[k] : v[k + N / 2];
+            w[k] = keep + partner<ST>(send);
+        }
+        return xreduce<N / 2, ST + 1>(w, lane);
+    }
+}
+// p[s] = sum_i w[i] * x[s * ld + 4 lane + i] (i < 4) for the group's four sentences
 __device__ __forceinline__ void dot4(float (&p)[TR_SPX], const float* w, const float* x, int ld, int lane) {
 #pragma unroll
-    for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(w[i], x[s * ld + lane + 64 * i], p[s]);
-}
-// the wave totals of p[0..3] (four independent reductions), total s returned in lane s
-__device__ __forceinline__ float to_lanes(const float (&p)[TR_SPX], int lane) {
-    float out = 0.f;
-#pragma unroll
     for (int s = 0; s < TR_SPX; ++s) {
-        const float v = wave_sum_dpp(p[s]);
-        out = lane == s ? v : out;
+        const float4 xv = ld4(x + s * ld + 4 * lane);
+        p[s] = fmaf(w[3], xv.w, fmaf(w[2], xv.z, fmaf(w[1], xv.y, w[0] * xv.x)));
     }
-    return out;
 }
-__device__ __forceinline__ float lds_dot2(const float* w, const float* x, int n, int lane) {
-    // sum_{i < n} w[64 i + lane] * x[lane + 64 i] (both in LDS)
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s = fmaf(w[64 * i + lane], x[lane + 64 * i], s);
-    return s;
+// totals of four sentences' partials, sentence s's total returned in lane s (lanes 0-3)
+__device__ __forceinline__ float to_lanes(const float (&p)[TR_SPX], int lane) {
+    const float tot = xreduce<TR_SPX>(p, lane);
+    return __shfl(tot, 16 * (lane & 3), 64);
 }
 
 __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const TResArgs a) {
@@ -214,19 +241,20 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
     const int ns = min(TR_SPX, a.B - b0);                // its sentences
     if (r >= TR_RANKS || ns <= 0) return;                // idle CU / group
     const int nmel = a.nmel;
-    // ---- weights into registers (reference layouts, lane-strided k = lane + 64 i)
+    // ---- weights into registers (reference layouts): lane l holds k = 4l + i of every 256-wide
+    // segment (one ds_read_b128 of the input per segment), k = 2l + i of the 128-wide prenet part
     const int U = 8 * r + wave;  // attention-GRU / decoder-GRU unit, proj row, prenet-L1 row
     float axr[6], axz[6], axn[6], ahr[4], ahz[4], ahn[4];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const int k = lane + 64 * i;
+        const int k = i < 2 ? 2 * lane + i : T_PRE2 + 4 * lane + (i - 2);
         axr[i] = a.a_wih[(int64_t)U * TXA + k];
         axz[i] = a.a_wih[(int64_t)(TD + U) * TXA + k];
         axn[i] = a.a_wih[(int64_t)(2 * TD + U) * TXA + k];
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int k = lane + 64 * i;
+        const int k = 4 * lane + i;
         ahr[i] = a.a_whh[(int64_t)U * TD + k];
         ahz[i] = a.a_whh[(int64_t)(TD + U) * TD + k];
         ahn[i] = a.a_whh[(int64_t)(2 * TD + U) * TD + k];
@@ -238,29 +266,32 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         for (int q = 0; q < 3; ++q)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                gx[g][q][i] = a.g_wih[g][(int64_t)(q * TD + U) * TD + lane + 64 * i];
-                gh[g][q][i] = a.g_whh[g][(int64_t)(q * TD + U) * TD + lane + 64 * i];
+                gx[g][q][i] = a.g_wih[g][(int64_t)(q * TD + U) * TD + 4 * lane + i];
+                gh[g][q][i] = a.g_whh[g][(int64_t)(q * TD + U) * TD + 4 * lane + i];
             }
     float wp[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wp[i] = a.w_proj[(int64_t)U * 2 * TD + lane + 64 * i];
+    for (int i = 0; i < 8; ++i) wp[i] = a.w_proj[(int64_t)U * 2 * TD + (i < 4 ? 4 * lane + i : TD + 4 * lane + i - 4)];
     const int m0 = r + 32 * wave, m1 = r + 32 * (wave + 8);  // this wave's mel rows (if < nmel)
-    // these two are read from LDS (register budget): [i][lane] per wave, conflict-free
+    // these two are read from LDS (register budget), one float4 per lane and segment:
+    // wm [row m0 | row m1][lane][4] (k = 4 lane + i), w1 [2][lane][4] (k = 8 lane + 4 h + i)
     float* wm = sm + L_WM + wave * 8 * 64;
     float* w1 = sm + L_W1 + wave * 8 * 64;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        wm[i * 64 + lane] = m0 < nmel ? a.w_mel[(int64_t)m0 * TD + lane + 64 * i] : 0.f;
-        wm[(4 + i) * 64 + lane] = m1 < nmel ? a.w_mel[(int64_t)m1 * TD + lane + 64 * i] : 0.f;
+        wm[lane * 4 + i] = m0 < nmel ? a.w_mel[(int64_t)m0 * TD + 4 * lane + i] : 0.f;
+        wm[256 + lane * 4 + i] = m1 < nmel ? a.w_mel[(int64_t)m1 * TD + 4 * lane + i] : 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        w1[i * 64 + lane] = lane + 64 * i < nmel ? a.w_pre1[(int64_t)U * nmel + lane + 64 * i] : 0.f;
+    for (int i = 0; i < 8; ++i) {
+        const int k = 8 * lane + i;
+        w1[(i >> 2) * 256 + lane * 4 + (i & 3)] = k < nmel ? a.w_pre1[(int64_t)U * nmel + k] : 0.f;
+    }
     const int r2 = 4 * r + (wave & 3);  // prenet-L2 row (waves 0-3) / query row (waves 4-7)
     float w2q[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        w2q[i] = wave < 4 ? a.w_pre2[(int64_t)r2 * TD + lane + 64 * i] : a.w_q[(int64_t)r2 * TD + lane + 64 * i];
+        w2q[i] = wave < 4 ? a.w_pre2[(int64_t)r2 * TD + 4 * lane + i] : a.w_q[(int64_t)r2 * TD + 4 * lane + i];
     // per-wave biases (LDS): [0..3] attention GRU r, z, n_x, n_h; [4..11] decoder GRUs; [12] proj;
     // [13] prenet L1; [14] prenet L2 (waves 0-3); [15] unused; mel biases by row below
     float* bias = sm + L_BIAS + wave * 16;
@@ -316,8 +347,8 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         sm[L_H1 + TR_SPX * TD + i] = on ? a.h1[a.h_pstride + (int64_t)b * TD + k] : 0.f;
         sm[L_H2 + TR_SPX * TD + i] = on ? a.h2[a.h_pstride + (int64_t)b * TD + k] : 0.f;
         sm[L_PRE1 + i] = on ? a.pre1[(int64_t)b * T_PRE1 + k] : 0.f;
-        sm[L_XA + s * TXA + T_PRE2 + k] = 0.f;
     }
+    for (int i = tid; i < TR_SPX * TXA; i += TR_THREADS) sm[L_XA + i] = 0.f;
     for (int i = tid; i < TR_SPX * TR_NMEL_MAX; i += TR_THREADS) sm[L_MEL + i] = 0.f;
     int* dn = ctl + 4;  // done flags of the group's sentences (as of this step's start)
     if (tid < TR_SPX) dn[tid] = tid < ns ? 0 : 1;
@@ -381,7 +412,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         // ---- 1) prenet L2 (waves 0-3, row 4r + w) -> xa[s][0:128]
         if (wave < 4) {
             float p[TR_SPX];
-            dot4<4>(p, w2q, pre1, T_PRE1, lane);
+            dot4(p, w2q, pre1, T_PRE1, lane);
             const float v = to_lanes(p, lane);
             if (lane < ns) publish(G + G_PRE2 + lane * T_PRE2 + r2, E + P_PRE2, fmaxf(v + bias[14], 0.f));
         }
@@ -397,28 +428,35 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         // ---- 2) attention GRU, unit U: x = [prenet | ctx_{t-1}], h = h_att_{t-1} (:370); the four
         // sentences' dot products interleaved, sentence s finished by lane s
         {
-            float pr[TR_SPX], pz[TR_SPX], pn[TR_SPX], qn[TR_SPX];
+            float v[4 * TR_SPX];  // [gate r, z, n_x, n_h][sentence]
 #pragma unroll
-            for (int s = 0; s < TR_SPX; ++s) pr[s] = pz[s] = pn[s] = qn[s] = 0.f;
+            for (int s = 0; s < TR_SPX; ++s) {
+                const float2 xp = ld2(xa + s * TXA + 2 * lane);
+                const float4 xc = ld4(xa + s * TXA + T_PRE2 + 4 * lane);
+                const float4 hv = ld4(hatt_prev + s * TD + 4 * lane);
+                const float x6[6] = {xp.x, xp.y, xc.x, xc.y, xc.z, xc.w};
+                const float h4[4] = {hv.x, hv.y, hv.z, hv.w};
+                float pr = 0.f, pz = 0.f, pn = 0.f, qn = 0.f;
 #pragma unroll
-            for (int i = 0; i < 6; ++i)
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) {
-                    const float xv = xa[s * TXA + lane + 64 * i];
-                    pr[s] = fmaf(axr[i], xv, pr[s]);
-                    pz[s] = fmaf(axz[i], xv, pz[s]);
-                    pn[s] = fmaf(axn[i], xv, pn[s]);
+                for (int i = 0; i < 6; ++i) {
+                    pr = fmaf(axr[i], x6[i], pr);
+                    pz = fmaf(axz[i], x6[i], pz);
+                    pn = fmaf(axn[i], x6[i], pn);
                 }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) {
-                    const float hv = hatt_prev[s * TD + lane + 64 * i];
-                    pr[s] = fmaf(ahr[i], hv, pr[s]);
-                    pz[s] = fmaf(ahz[i], hv, pz[s]);
-                    qn[s] = fmaf(ahn[i], hv, qn[s]);
+                for (int i = 0; i < 4; ++i) {
+                    pr = fmaf(ahr[i], h4[i], pr);
+                    pz = fmaf(ahz[i], h4[i], pz);
+                    qn = fmaf(ahn[i], h4[i], qn);
                 }
-            const float R = to_lanes(pr, lane), Z = to_lanes(pz, lane), N = to_lanes(pn, lane), Q = to_lanes(qn, lane);
+                v[s] = pr;
+                v[TR_SPX + s] = pz;
+                v[2 * TR_SPX + s] = pn;
+                v[3 * TR_SPX + s] = qn;
+            }
+            const float tot = xreduce<4 * TR_SPX>(v, lane);  // value k = 4 gate + s in lane 4k
+            const float R = __shfl(tot, 4 * (lane & 3), 64), Z = __shfl(tot, 4 * (4 + (lane & 3)), 64),
+                        N = __shfl(tot, 4 * (8 + (lane & 3)), 64), Q = __shfl(tot, 4 * (12 + (lane & 3)), 64);
             if (lane < ns) {
                 const float rg = sigmoidf_(R + bias[0]);
                 const float zg = sigmoidf_(Z + bias[1]);
@@ -440,7 +478,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         // ---- 3) query_layer (waves 4-7, row 4r + w - 4) over h_att_t (common_layers.py:179)
         if (wave >= 4) {
             float p[TR_SPX];
-            dot4<4>(p, w2q, hatt, TD, lane);
+            dot4(p, w2q, hatt, TD, lane);
             const float v = to_lanes(p, lane);
             if (lane < ns) publish(G + G_Q + lane * ADIM + r2, E + P_Q, v);
         }
@@ -563,15 +601,12 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         {
             float p[TR_SPX];
 #pragma unroll
-            for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(wp[i], hatt[s * TD + lane + 64 * i], p[s]);
-#pragma unroll
-            for (int i = 4; i < 8; ++i)
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(wp[i], xa[s * TXA + T_PRE2 + lane + 64 * (i - 4)], p[s]);
+            for (int s = 0; s < TR_SPX; ++s) {
+                const float4 h = ld4(hatt + s * TD + 4 * lane);
+                const float4 x = ld4(xa + s * TXA + T_PRE2 + 4 * lane);
+                p[s] = fmaf(wp[7], x.w, fmaf(wp[6], x.z, fmaf(wp[5], x.y, fmaf(wp[4], x.x,
+                       fmaf(wp[3], h.w, fmaf(wp[2], h.z, fmaf(wp[1], h.y, wp[0] * h.x)))))));
+            }
             const float v = to_lanes(p, lane);
             if (lane < ns) publish(G + G_DIN + lane * TD + U, E + P_DIN, v + bias[12]);
         }
@@ -595,24 +630,33 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             u64* gg = G + (g == 0 ? G_H1 : G_H2);
             const unsigned tg = E + (g == 0 ? P_H1 : P_H2);
             {
-                float pr[TR_SPX], pz[TR_SPX], pn[TR_SPX], qn[TR_SPX];
+                float v[4 * TR_SPX];
 #pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) pr[s] = pz[s] = pn[s] = qn[s] = 0.f;
+                for (int s = 0; s < TR_SPX; ++s) {
+                    const float4 xv = ld4(X + s * TD + 4 * lane);
+                    const float4 hv = ld4(Hp + s * TD + 4 * lane);
+                    const float x4[4] = {xv.x, xv.y, xv.z, xv.w}, h4[4] = {hv.x, hv.y, hv.z, hv.w};
+                    float pr = 0.f, pz = 0.f, pn = 0.f, qn = 0.f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int s = 0; s < TR_SPX; ++s) {
-                        const float xv = X[s * TD + lane + 64 * i];
-                        const float hv = Hp[s * TD + lane + 64 * i];
-                        pr[s] = fmaf(gx[g][0][i], xv, pr[s]);
-                        pz[s] = fmaf(gx[g][1][i], xv, pz[s]);
-                        pn[s] = fmaf(gx[g][2][i], xv, pn[s]);
-                        pr[s] = fmaf(gh[g][0][i], hv, pr[s]);
-                        pz[s] = fmaf(gh[g][1][i], hv, pz[s]);
-                        qn[s] = fmaf(gh[g][2][i], hv, qn[s]);
+                    for (int i = 0; i < 4; ++i) {
+                        pr = fmaf(gx[g][0][i], x4[i], pr);
+                        pz = fmaf(gx[g][1][i], x4[i], pz);
+                        pn = fmaf(gx[g][2][i], x4[i], pn);
                     }
-                const float R = to_lanes(pr, lane), Z = to_lanes(pz, lane), N = to_lanes(pn, lane),
-                            Q = to_lanes(qn, lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        pr = fmaf(gh[g][0][i], h4[i], pr);
+                        pz = fmaf(gh[g][1][i], h4[i], pz);
+                        qn = fmaf(gh[g][2][i], h4[i], qn);
+                    }
+                    v[s] = pr;
+                    v[TR_SPX + s] = pz;
+                    v[2 * TR_SPX + s] = pn;
+                    v[3 * TR_SPX + s] = qn;
+                }
+                const float tot = xreduce<4 * TR_SPX>(v, lane);
+                const float R = __shfl(tot, 4 * (lane & 3), 64), Z = __shfl(tot, 4 * (4 + (lane & 3)), 64),
+                            N = __shfl(tot, 4 * (8 + (lane & 3)), 64), Q = __shfl(tot, 4 * (12 + (lane & 3)), 64);
                 if (lane < ns) {
                     const float rg = sigmoidf_(R + bias[4 + 4 * g]);
                     const float zg = sigmoidf_(Z + bias[5 + 4 * g]);
@@ -640,31 +684,25 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         }
         // ---- 8) output = sigmoid(proj_to_mel(decoder_output)), rows m0, m1 (:385-386) -> history
         {
-            float p0[TR_SPX], p1[TR_SPX];
+            float p[2 * TR_SPX];  // [row m0, m1][sentence]
+            const float4 w0 = ld4(wm + 4 * lane), w1_ = ld4(wm + 256 + 4 * lane);
 #pragma unroll
-            for (int s = 0; s < TR_SPX; ++s) p0[s] = p1[s] = 0.f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float w0 = wm[64 * i + lane], w1_ = wm[64 * (4 + i) + lane];
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) {
-                    const float xv = d2[s * TD + lane + 64 * i];
-                    p0[s] = fmaf(w0, xv, p0[s]);
-                    p1[s] = fmaf(w1_, xv, p1[s]);
-                }
+            for (int s = 0; s < TR_SPX; ++s) {
+                const float4 x = ld4(d2 + s * TD + 4 * lane);
+                p[s] = fmaf(w0.w, x.w, fmaf(w0.z, x.z, fmaf(w0.y, x.y, w0.x * x.x)));
+                p[TR_SPX + s] = fmaf(w1_.w, x.w, fmaf(w1_.z, x.z, fmaf(w1_.y, x.y, w1_.x * x.x)));
             }
-            const float v0 = to_lanes(p0, lane), v1 = to_lanes(p1, lane);
-            if (lane < ns) {
+            const float tot = xreduce<2 * TR_SPX>(p, lane);  // value k in lane 8k
+            const float v0 = __shfl(tot, 8 * (lane & 3), 64), v1 = __shfl(tot, 8 * (4 + (lane & 3)), 64);
+            if (lane < ns) {  // rows past nmel publish 0 (the gather reads all TR_NMEL_MAX)
                 const int b = b0 + lane;
-                if (m0 < nmel) {
-                    const float o = sigmoidf_(v0 + bm0);
-                    publish(G + G_MEL + lane * TR_NMEL_MAX + m0, E + P_MEL, o);
-                    if (t < a.hist_cap) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m0] = o;
-                }
-                if (m1 < nmel) {
-                    const float o = sigmoidf_(v1 + bm1);
-                    publish(G + G_MEL + lane * TR_NMEL_MAX + m1, E + P_MEL, o);
-                    if (t < a.hist_cap) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m1] = o;
+                const float o0 = m0 < nmel ? sigmoidf_(v0 + bm0) : 0.f;
+                const float o1 = m1 < nmel ? sigmoidf_(v1 + bm1) : 0.f;
+                publish(G + G_MEL + lane * TR_NMEL_MAX + m0, E + P_MEL, o0);
+                publish(G + G_MEL + lane * TR_NMEL_MAX + m1, E + P_MEL, o1);
+                if (t < a.hist_cap) {
+                    if (m0 < nmel) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m0] = o0;
+                    if (m1 < nmel) a.mel_hist[((int64_t)b * a.hist_cap + t) * nmel + m1] = o1;
                 }
             }
         }
@@ -672,12 +710,10 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         if (gon) {
             float v4[4];
             const bool ok = sweep<4>(G + G_MEL, E + P_MEL, v4, [&](int i) {
-                const int k = gf * 256 + ln + 64 * i;
-                return k < nmel ? gs * TR_NMEL_MAX + k : -1;
+                return gs * TR_NMEL_MAX + gf * 256 + ln + 64 * i;
             }, tmo);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (gf * 256 + lane + 64 * i < nmel) mel[gs * TR_NMEL_MAX + gf * 256 + lane + 64 * i] = v4[i];
+            for (int i = 0; i < 4; ++i) mel[gs * TR_NMEL_MAX + gf * 256 + lane + 64 * i] = v4[i];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 12); }
         }
         __syncthreads();
@@ -714,13 +750,13 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         // prenet L1 of step t+1, row U (memory = this output, memory_size == r: :396-404)
         {
             float p[TR_SPX];
+            const float4 wa = ld4(w1 + 4 * lane), wb = ld4(w1 + 256 + 4 * lane);
 #pragma unroll
-            for (int s = 0; s < TR_SPX; ++s) p[s] = 0.f;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const float w = w1[64 * i + lane];
-#pragma unroll
-                for (int s = 0; s < TR_SPX; ++s) p[s] = fmaf(w, mel[s * TR_NMEL_MAX + lane + 64 * i], p[s]);
+            for (int s = 0; s < TR_SPX; ++s) {
+                const float4 xa_ = ld4(mel + s * TR_NMEL_MAX + 8 * lane);
+                const float4 xb_ = ld4(mel + s * TR_NMEL_MAX + 8 * lane + 4);
+                p[s] = fmaf(wb.w, xb_.w, fmaf(wb.z, xb_.z, fmaf(wb.y, xb_.y, fmaf(wb.x, xb_.x,
+                       fmaf(wa.w, xa_.w, fmaf(wa.z, xa_.z, fmaf(wa.y, xa_.y, wa.x * xa_.x)))))));
             }
             const float v = to_lanes(p, lane);
             if (lane < ns) publish(G + G_PRE1 + lane * T_PRE1 + U, E + P_PRE1, fmaxf(v + bias[13], 0.f));
