@@ -33,7 +33,18 @@ void encoder_set_pipeline(tts_encoder* e, bool on);
 // *placement_failed = 1: the resident encoder could not be placed, or one of its hand-off waits
 // timed out: the caller reruns the encoder (with per-step launches)
 tts_status encoder_pending_status(tts_encoder* e, int* placement_failed);
+// the encoder handle's own ids / output buffers: a pipeline passes them as tts_encoder_run's ids /
+// out to skip the staging copies (null ids buffer: B x Lmax exceeds the handle's capacity)
+int32_t* encoder_ids_buffer(tts_encoder* e, int B, int Lmax);
+float* encoder_out_buffer(tts_encoder* e);
 void decoder_set_pipeline(tts_decoder* d, bool on);
+// the decoder's mel history (sentence b at mel + b * sentence_floats, rows of nmel * r floats) and
+// its device step counts, where a pipeline-mode run (decoder_set_pipeline) leaves its output
+void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floats, const int** n_steps);
+// postnet.hip: tts_postnet_run with device frame counts (T_dev[b] * tmul) and input rows mel_tmax
+// frames apart (0 = Tmax); T holds the same counts on the host
+tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
+                           int B, int Tmax, float* out, hipStream_t s);
 void gl_set_pipeline(tts_gl* g, bool on);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 
@@ -53,6 +64,9 @@ hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args,
 hipError_t frag_mirror(const float* src, int64_t ld, int B, int K, float* dst, int ntf, hipStream_t s);
 // the CU count launch_persistent plans with (device CUs, capped by TTS_CU_CAP)
 int usable_cus();
+// record `ev` on `s` and wait for it by polling (runtime.hip: the blocking wait's wake-up latency
+// sits on the synthesis critical path)
+hipError_t spin_sync(hipStream_t s, hipEvent_t ev);
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 

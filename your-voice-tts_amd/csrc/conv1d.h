@@ -21,6 +21,7 @@ struct ConvArgs {
     const float* table;  // [rows][Cin]
     float* out;          // [B][Tmax][Cout]
     const float* W;      // packed [Cin][KW][co_pad]
+    const float* Wf;     // optional fragment-order copy of W (conv_pack_frag): small batches use it
     const float* scale;  // [Cout] (null = 1)
     const float* shift;  // [Cout] (null = 0)
     const float* resid;  // [B][Tmax][out_ld] or null: out = resid + y (CONV_HIGHWAY: the layer input)
@@ -35,8 +36,15 @@ struct ConvArgs {
     float* part;
     int Ttile;  // frames covered by output tiles (>= max T_b; 0 = Tmax): a caller whose buffers are
                 // sized for a cap (postnet: max_decoder_steps + 20) passes the batch's longest sentence
+    int in_tmax;  // frames per sentence of `in` (0 = Tmax) and of `resid` (res_tmax): the synthesis
+    int res_tmax; // postnet reads the decoder's mel history in place (max_decoder_steps + 21 steps)
+    int tmul;     // T[b] counts groups of tmul frames (0 = 1): the decoder's step counts, r frames each
+    // optional [CONV_TICKETS] zeroed ints beside `part`: the split-K launch then reduces its own
+    // partials (the last workgroup of each output tile; the words are left zero again)
+    int* tickets;
 };
 constexpr size_t CONV_SPLITK_FLOATS = (size_t)1 << 20;  // split x tiles <= 1024 -> <= 1M partials
+constexpr int CONV_TICKETS = 1024;                       // output tiles of one split-K launch
 
 constexpr int CONV_BN = 64;  // output channels per tile
 inline int conv_co_pad(int Cout) { return (Cout + CONV_BN - 1) / CONV_BN * CONV_BN; }
@@ -49,6 +57,8 @@ hipError_t conv_pack(const float* W, int Cout, int Cin, int KW, float* out, hipS
 // The caller zeroes the slab first.
 hipError_t conv_pack_bank(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad, float* out,
                           hipStream_t s);
+// packed [K = Cin * KW][co_pad] -> the small-batch kernel's fragment order (K % 8 == 0, co_pad % 32 == 0)
+hipError_t conv_pack_frag(const float* W, int K, int co_pad, float* out, hipStream_t s);
 // W [Cout][Cin] (Linear layout, rows stacked into Cout) -> packed [Cin][1][co_pad]
 hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,
                                hipStream_t s);

@@ -10,11 +10,16 @@
 // long CBHG bank slabs (KW 8 / 16) accumulate every tap into one set (register budget).  Two tile
 // shapes: BM=64 (2x2 waves of 32x32) for large batches (BM=32, 2x2 waves of 16x32, for the KW=5
 // convs), BM=16 (1x4 waves of 16x16) so that a single sentence still spreads over >= 100 workgroups.
+#include <algorithm>
+#include <cstdlib>
+
 #include "conv1d.h"
 
 namespace tts {
 
 namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int KW, int BM, int WM, int WN, bool SPLIT = false>
 __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit = 1, int nb = 1) {
@@ -39,8 +44,9 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
     const int b = rest / mtiles;
     const int t0 = (rest % mtiles) * BM;
     const int c0 = ntile * BN;
-    const int Tb = a.T[b];
+    const int Tb = a.tmul > 1 ? a.T[b] * a.tmul : a.T[b];
     if (t0 >= Tb) return;
+    const int64_t Tin = a.in_tmax ? a.in_tmax : a.Tmax;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wt = (wave / WN) * (BM / WM);
     const int wc = (wave % WN) * (BN / WN);
@@ -74,12 +80,12 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
             const int t = t0 - PAD + r;                                                                          \
             const bool ok = t >= 0 && t < Tb;                                                                    \
             const int tc = ok ? t : 0;                                                                           \
-            const float* src = idsb ? a.table + (int64_t)idsb[tc] * a.Cin : a.in + ((int64_t)b * a.Tmax + tc) * a.Cin; \
+            const float* src = idsb ? a.table + (int64_t)idsb[tc] * a.Cin : a.in + ((int64_t)b * Tin + tc) * a.Cin; \
             float4 v = *reinterpret_cast<const float4*>(src + ci0_ + c4 * 4);                                    \
             if (a.pool2) { /* max(in[t], in[t+1]), in[T_b] = 0 */                                                \
                 const bool ok1 = ok && t + 1 < Tb;                                                               \
                 const float4 v1 = *reinterpret_cast<const float4*>(                                              \
-                    a.in + ((int64_t)b * a.Tmax + (ok1 ? t + 1 : tc)) * a.Cin + ci0_ + c4 * 4);                   \
+                    a.in + ((int64_t)b * Tin + (ok1 ? t + 1 : tc)) * a.Cin + ci0_ + c4 * 4);                      \
                 const float4 p1 = ok1 ? v1 : float4{0.f, 0.f, 0.f, 0.f};                                         \
                 v = float4{fmaxf(v.x, p1.x), fmaxf(v.y, p1.y), fmaxf(v.z, p1.z), fmaxf(v.w, p1.w)};              \
             }                                                                                                    \
@@ -146,6 +152,70 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
 #undef CONV_GLOAD
 #undef CONV_LSTORE
     // epilogue: D lane l holds C[(l>>4)*4 + r][l&15]  (row = frame, col = channel)
+    if (SPLIT && a.tickets) {
+        // Fused reduction: the LAST of the tile's nsplit workgroups to arrive sums the partials in
+        // split order and applies the epilogue (conv_reduce_kernel's arithmetic, bitwise).  Hand-off
+        // (MI355X_MICROARCH.md, inter-workgroup visibility, sc1 table row 1): every partial is
+        // stored write-through (16-byte sc1 stores: a lane's 4 rows are consecutive frames in the
+        // [z][b][co][t] layout), every storing wave drains, then one lane per workgroup adds to the
+        // tile's ticket; the workgroup whose add returns nsplit - 1 reads the partials with sc1
+        // loads after a barrier, and resets the ticket for the next launch.
+        const int Tp = (Tt + 3) & ~3;
+        const auto prs = __builtin_amdgcn_make_buffer_rsrc(a.part, (short)0, (int)(CONV_SPLITK_FLOATS * 4), 0x00020000);
+        const int64_t pz = (int64_t)nb * a.co_pad * Tp;  // floats per split slice
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int tb = t0 + wt + i * 16 + (lane >> 4) * 4;
+                const int co = c0 + wc + j * 16 + (lane & 15);
+                floatx4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float sum = acc[0][i][j][r];
+#pragma unroll
+                    for (int k = 1; k < NACC; ++k) sum += acc[k][i][j][r];
+                    v[r] = sum;
+                }
+                if (tb < Tb)
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), prs,
+                                                           (int)((z * pz + ((int64_t)b * a.co_pad + co) * Tp + tb) * 4), 0, 16);
+            }
+        __shared__ int last_arriver;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int tk = __hip_atomic_fetch_add(a.tickets + bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last_arriver = tk == nsplit - 1;
+            if (tk == nsplit - 1) __hip_atomic_store(a.tickets + bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!last_arriver) return;
+        const int ld = a.out_ld ? a.out_ld : a.Cout;
+        const int rtm = a.res_tmax ? a.res_tmax : a.Tmax;
+        // thread: 4 consecutive frames of one channel
+        for (int e = tid; e < (BM / 4) * BN; e += 256) {
+            const int co = c0 + e / (BM / 4), tb = t0 + 4 * (e % (BM / 4));
+            if (tb >= Tb || co >= a.Cout) continue;
+            const int off = (int)((((int64_t)b * a.co_pad + co) * Tp + tb) * 4);
+            floatx4 sum = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(prs, off, 0, 16));
+            for (int zz = 1; zz < nsplit; ++zz)
+                sum += __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(prs, off + (int)(zz * pz * 4), 0, 16));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int t = tb + r;
+                if (t >= Tb) break;
+                float y = a.scale ? sum[r] * a.scale[co] : sum[r];
+                if (a.shift) y += a.shift[co];
+                if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+                else if (a.act == CONV_TANH) y = tanhf(y);
+                else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
+                if (a.resid) y = a.resid[((int64_t)b * rtm + t) * ld + co] + y;
+                a.out[((int64_t)b * a.Tmax + t) * ld + co] = y;
+            }
+        }
+        return;
+    }
     if (SPLIT) {
         // raw partial sums -> part[z][b][t][co_pad]; conv_reduce_kernel applies the epilogue
         const int64_t pb = ((int64_t)z * nb + b) * Tt;
@@ -167,7 +237,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
     }
     const int ld = a.out_ld ? a.out_ld : a.Cout;
     float* outb = a.out + (int64_t)b * a.Tmax * ld;
-    const float* resb = a.resid ? a.resid + (int64_t)b * a.Tmax * ld : nullptr;
+    const float* resb = a.resid ? a.resid + (int64_t)b * (a.res_tmax ? a.res_tmax : a.Tmax) * ld : nullptr;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -203,6 +273,156 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
             }
 }
 
+// ---------------------------------------------------------------- small-batch convolution
+// The batch-1 postnet / encoder convs (T ~ 100-300 frames, ~100 output tiles) were bound by the
+// tiled kernel's per-K-step global -> LDS -> barrier round trip (2 us per 16-channel step at one
+// workgroup per tile, measured).  Here a workgroup owns 16 frames x 32 output channels: it stages
+// its input rows (all Cin channels, KW - 1 halo rows) in LDS ONCE, then each of its CS_WAVES waves sweeps
+// a slice of the K = Cin * KW reduction with the MFMA B operands (weights) loaded straight from
+// the packed [Cin][KW][co_pad] layout into registers, CS_PR k-step pairs ahead, and no barrier until
+// the waves' partial tiles are summed (fixed order) for the epilogue.
+constexpr int CS_BM = 16, CS_BN = 32, CS_PR = 16, CS_WAVES = 8, CS_THREADS = 64 * CS_WAVES;
+template <int KW>
+__global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a) {
+    constexpr int PAD = (KW - 1) / 2;
+    constexpr int XR = CS_BM + KW - 1;
+    extern __shared__ float xs[];  // [XR][Cin + 1] input rows; then the waves' partial tiles
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Tt = a.Ttile ? a.Ttile : a.Tmax;
+    const int nct = a.co_pad / CS_BN, mtiles = (Tt + CS_BM - 1) / CS_BM;
+    const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
+    const int b = rest / mtiles, t0 = (rest % mtiles) * CS_BM, c0 = ct * CS_BN;
+    const int Tb = a.tmul > 1 ? a.T[b] * a.tmul : a.T[b];
+    if (t0 >= Tb) return;
+    const int Cin = a.Cin, ldx = Cin + 1;
+    const int64_t Tin = a.in_tmax ? a.in_tmax : a.Tmax;
+    const int* idsb = a.ids ? a.ids + (int64_t)b * a.Tmax : nullptr;
+    {
+        // every load of the stage is issued before the first LDS store (one memory round trip)
+        constexpr int XPT = (XR * 128 + CS_THREADS - 1) / CS_THREADS;  // float4 per thread at Cin <= 512
+        float4 xv[XPT];
+#pragma unroll
+        for (int u = 0; u < XPT; ++u) {
+            const int i = tid + u * CS_THREADS;
+            const int r = i / (Cin >> 2), c4 = i - r * (Cin >> 2), t = t0 - PAD + r;
+            const bool ok = r < XR && t >= 0 && t < Tb;
+            const int tc = ok ? t : 0;
+            const float* src = idsb ? a.table + (int64_t)idsb[tc] * Cin : a.in + ((int64_t)b * Tin + tc) * Cin;
+            const float4 v = *reinterpret_cast<const float4*>(src + 4 * (r < XR ? c4 : 0));
+            xv[u] = ok ? v : float4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < XPT; ++u) {
+            const int i = tid + u * CS_THREADS;
+            const int r = i / (Cin >> 2), c4 = i - r * (Cin >> 2);
+            if (r < XR) {
+                float* d = xs + r * ldx + 4 * c4;
+                d[0] = xv[u].x; d[1] = xv[u].y; d[2] = xv[u].z; d[3] = xv[u].w;
+            }
+        }
+    }
+    __syncthreads();
+    // wave w: k-steps [s_beg, s_end) of the K / 4 steps; lane supplies A[row][q] = x[t0 + row + tap - PAD][ci]
+    // and B[q][n] = W[k][c0 + 16 j + n] for k = 4 s + q = ci * KW + tap
+    const int nks = (Cin * KW) >> 2;
+    const int s_beg = wave * nks / 4, s_end = (wave + 1) * nks / 4;
+    const int q = lane >> 4, row = lane & 15;
+    const float* Wl = a.W + c0 + row;
+    const int64_t cp = a.co_pad;
+    // B operands from the fragment-order copy Wf (conv_pack_frag): one float4 per lane per pair
+    // of k-steps = W[k][c0 + r], W[k][c0 + 16 + r] at k = 8 p + q and 8 p + 4 + q; CS_PR pairs
+    // in flight in a register ring (each pair's reload issued right after its MFMAs)
+    const int np = nks >> 1;  // pairs (K is a multiple of 8)
+    const int p_beg = wave * np / CS_WAVES, p_end = (wave + 1) * np / CS_WAVES;
+    const float4* Wf = reinterpret_cast<const float4*>(a.Wf) + (int64_t)ct * np * 64 + lane;
+    float4 wr[CS_PR];
+#pragma unroll
+    for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)min(p_beg + i, p_end - 1) * 64];
+    int k0 = 8 * p_beg + q;
+    int ci = k0 / KW, tap = k0 - ci * KW;
+    auto next4 = [&]() {  // k += 4
+        if constexpr (KW == 1) {
+            ci += 4;
+        } else {
+            tap += 4;
+#pragma unroll
+            for (int w = 0; w < (4 + KW - 1) / KW; ++w) {
+                const bool wrap = tap >= KW;
+                tap = wrap ? tap - KW : tap;
+                ci = wrap ? ci + 1 : ci;
+            }
+        }
+    };
+    floatx4 acc0 = floatx4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    auto round = [&](int pc) {
+        // the round's A operands first (every LDS read in flight together), then per pair its MFMAs
+        // and the reload of its ring slot, in that order (sched_barrier)
+        float xa[2 * CS_PR];
+#pragma unroll
+        for (int i = 0; i < 2 * CS_PR; ++i) {
+            xa[i] = xs[(row + tap) * ldx + min(ci, Cin - 1)];
+            next4();
+        }
+#pragma unroll
+        for (int i = 0; i < CS_PR; ++i) {
+            // pairs past p_end multiply zero A operands (exact no-ops on the accumulators)
+            const bool ok = pc + i < p_end;
+            const float a0 = ok ? xa[2 * i] : 0.f, a1 = ok ? xa[2 * i + 1] : 0.f;
+            acc0 = mfma16x16x4(a0, wr[i].x, acc0);
+            acc1 = mfma16x16x4(a0, wr[i].y, acc1);
+            acc0 = mfma16x16x4(a1, wr[i].z, acc0);
+            acc1 = mfma16x16x4(a1, wr[i].w, acc1);
+            wr[i] = Wf[(int64_t)min(pc + i + CS_PR, p_end - 1) * 64];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    // two rounds per loop trip: the compiler drains every outstanding load at a loop header, so
+    // that drain is paid once per 2 * CS_PR pairs (the second round waits only for its own slot)
+    for (int pc = p_beg; pc < p_end; pc += 2 * CS_PR) {
+        round(pc);
+        if (pc + CS_PR < p_end) round(pc + CS_PR);
+    }
+    __syncthreads();  // every wave is done with the input rows: reuse them for the partial tiles
+    float* red = xs;  // [wave][j][lane][r]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        red[(wave * 2 + 0) * 256 + lane * 4 + r] = acc0[r];
+        red[(wave * 2 + 1) * 256 + lane * 4 + r] = acc1[r];
+    }
+    __syncthreads();
+    const int ld = a.out_ld ? a.out_ld : a.Cout;
+    const int rtm = a.res_tmax ? a.res_tmax : a.Tmax;
+    for (int e = tid; e < CS_BM * CS_BN; e += CS_THREADS) {
+        const int tl = e / CS_BN, cl = e % CS_BN, t = t0 + tl, co = c0 + cl;
+        if (t >= Tb || co >= a.Cout) continue;
+        const int j = cl >> 4, src_lane = (tl >> 2) * 16 + (cl & 15), idx = src_lane * 4 + (tl & 3);
+        float sum = red[j * 256 + idx];  // the waves' partial tiles in wave order
+#pragma unroll
+        for (int w = 1; w < CS_WAVES; ++w) sum += red[(2 * w + j) * 256 + idx];
+        float y = a.scale ? sum * a.scale[co] : sum;
+        if (a.shift) y += a.shift[co];
+        if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+        else if (a.act == CONV_TANH) y = tanhf(y);
+        else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
+        if (a.resid) y = a.resid[((int64_t)b * rtm + t) * ld + co] + y;
+        a.out[((int64_t)b * a.Tmax + t) * ld + co] = y;
+    }
+}
+
+template <int KW>
+bool launch_small(const ConvArgs& a, int B, int frames_hint, hipStream_t s, hipError_t* err) {
+    static const int limit = getenv("TTS_CONV_SMALL") ? atoi(getenv("TTS_CONV_SMALL")) : 1024;  // frames; 0 = off
+    if (!a.Wf || frames_hint > limit || a.pool2 || a.act == CONV_HIGHWAY || (a.Cin & 3) || a.Cin > 512 ||
+        (a.co_pad % CS_BN) || ((a.Cin * KW) & 7))
+        return false;
+    const int Tt = a.Ttile ? a.Ttile : a.Tmax;
+    const size_t smem = sizeof(float) * std::max((size_t)(CS_BM + KW - 1) * (a.Cin + 1), (size_t)2 * 256 * CS_WAVES);
+    const dim3 grid(((Tt + CS_BM - 1) / CS_BM) * (a.co_pad / CS_BN) * B);
+    hipLaunchKernelGGL(conv_small_kernel<KW>, grid, dim3(CS_THREADS), smem, s, a);
+    *err = hipGetLastError();
+    return true;
+}
+
 __global__ void conv_pack_kernel(const float* W, int Cout, int Cin, int KW, int co_pad, float* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)Cin * KW * co_pad;
@@ -211,6 +431,20 @@ __global__ void conv_pack_kernel(const float* W, int Cout, int Cin, int KW, int 
     const int k = (i / co_pad) % KW;
     const int ci = i / ((int64_t)co_pad * KW);
     out[i] = co < Cout ? W[((int64_t)co * Cin + ci) * KW + k] : 0.f;
+}
+
+// packed [K][co_pad] -> fragment order [co_pad / 32][K / 8][64 lanes][4]: lane (q, r) of pair p
+// holds W[8p + q][32ct + r], W[8p + q][32ct + 16 + r], W[8p + 4 + q][32ct + r], W[8p + 4 + q][32ct + 16 + r]
+__global__ void conv_pack_frag_kernel(const float* W, int K, int co_pad, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)K * co_pad) return;
+    const int e = i & 3, lane = (i >> 2) & 63;
+    const int64_t rest = i >> 8;
+    const int np = K >> 3;
+    const int p = rest % np, ct = rest / np;
+    const int q = lane >> 4, r = lane & 15;
+    const int k = 8 * p + 4 * (e >> 1) + q, co = 32 * ct + 16 * (e & 1) + r;
+    out[i] = W[(int64_t)k * co_pad + co];
 }
 
 __global__ void conv_pack_bank_kernel(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad,
@@ -256,7 +490,7 @@ __global__ void conv_reduce_kernel(const ConvArgs a, int B, int nsplit) {
     const int co = i % a.Cout;
     const int t = (i / a.Cout) % Tt;
     const int b = i / ((int64_t)a.Cout * Tt);
-    if (t >= a.T[b]) return;
+    if (t >= (a.tmul > 1 ? a.T[b] * a.tmul : a.T[b])) return;
     float sum = 0.f;
     for (int z = 0; z < nsplit; ++z) sum += a.part[(((int64_t)z * B + b) * Tt + t) * a.co_pad + co];
     float y = a.scale ? sum * a.scale[co] : sum;
@@ -265,13 +499,17 @@ __global__ void conv_reduce_kernel(const ConvArgs a, int B, int nsplit) {
     else if (a.act == CONV_TANH) y = tanhf(y);
     else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
     const int ld = a.out_ld ? a.out_ld : a.Cout;
-    if (a.resid) y = a.resid[((int64_t)b * a.Tmax + t) * ld + co] + y;
+    if (a.resid) y = a.resid[((int64_t)b * (a.res_tmax ? a.res_tmax : a.Tmax) + t) * ld + co] + y;
     a.out[((int64_t)b * a.Tmax + t) * ld + co] = y;
 }
 
 template <int KW>
 hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
     const dim3 block(256);
+    if constexpr (KW == 1 || KW == 5) {
+        hipError_t e = hipSuccess;
+        if (launch_small<KW>(a, B, frames_hint, s, &e)) return e;
+    }
     constexpr int BK = KW <= 5 ? 16 : (KW <= 8 ? 8 : 4);
     const int Tt = a.Ttile ? a.Ttile : a.Tmax;
     const int tiles = ((Tt + 15) / 16) * (a.co_pad / CONV_BN) * B;
@@ -279,11 +517,19 @@ hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
         // split the K steps so that the launch fills the chip: nsplit x tiles <= 1024
         const int nsteps = a.Cin / BK;
         int ns = 1;
-        while (ns * 2 <= 16 && tiles * ns * 2 <= 1024 && nsteps % (ns * 2) == 0 && nsteps / (ns * 2) >= 2) ns *= 2;
-        if (ns > 1 && (size_t)ns * B * Tt * a.co_pad <= CONV_SPLITK_FLOATS) {
-            hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4, true>), dim3(tiles * ns), block, 0, s, a, ns, B);
-            const int64_t total = (int64_t)B * Tt * a.Cout;
-            hipLaunchKernelGGL(conv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, B, ns);
+        static const int ns_max = getenv("TTS_CONV_NSMAX") ? atoi(getenv("TTS_CONV_NSMAX")) : 16;  // A/B knob
+        while (ns * 2 <= ns_max && tiles * ns * 2 <= 1024 && nsteps % (ns * 2) == 0 && nsteps / (ns * 2) >= 2) ns *= 2;
+        if (ns > 1 && (size_t)ns * B * ((Tt + 3) & ~3) * a.co_pad <= CONV_SPLITK_FLOATS) {
+            // the reduction rides in the same launch when the caller supplies ticket words
+            // (TTS_CONV_FUSED_REDUCE=0: separate reduce launch, A/B knob)
+            static const bool fused_ok = !(getenv("TTS_CONV_FUSED_REDUCE") && getenv("TTS_CONV_FUSED_REDUCE")[0] == '0');
+            ConvArgs b = a;
+            if (!fused_ok || tiles > CONV_TICKETS) b.tickets = nullptr;
+            hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4, true>), dim3(tiles * ns), block, 0, s, b, ns, B);
+            if (!b.tickets) {
+                const int64_t total = (int64_t)B * Tt * a.Cout;
+                hipLaunchKernelGGL(conv_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, B, ns);
+            }
             return hipGetLastError();
         }
     }
@@ -309,6 +555,13 @@ hipError_t conv_pack(const float* W, int Cout, int Cin, int KW, float* out, hipS
     const int co_pad = conv_co_pad(Cout);
     const int64_t total = (int64_t)Cin * KW * co_pad;
     hipLaunchKernelGGL(conv_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, Cout, Cin, KW, co_pad, out);
+    return hipGetLastError();
+}
+
+hipError_t conv_pack_frag(const float* W, int K, int co_pad, float* out, hipStream_t s) {
+    if ((K & 7) || (co_pad % CS_BN)) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)K * co_pad;
+    hipLaunchKernelGGL(conv_pack_frag_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, K, co_pad, out);
     return hipGetLastError();
 }
 

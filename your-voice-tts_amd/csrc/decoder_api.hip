@@ -39,6 +39,7 @@ struct tts_decoder {
     int nmel = 80;
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+    hipEvent_t ev_sync = nullptr;  // spin_sync (runtime.hip)
     std::vector<void*> allocs;
     // packed GEMM weights + logical biases
     float *W_pre1 = nullptr, *W_pre2 = nullptr, *W_att = nullptr, *b_att = nullptr, *W_q = nullptr;
@@ -70,6 +71,9 @@ struct tts_decoder {
     std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
     bool pipeline = false;  // tts_synth_run: work on the caller's stream
+    // tts_synth_run: leave mel / stop / alignments in the histories (decoder_histories) instead of
+    // copying them out (the postnet reads the mel history in place)
+    bool keep_hist = false;
     int last_steps = 0;
     int last_B = 0, last_Lmax = 0, last_max_steps = 0, last_first = 0;
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
@@ -326,6 +330,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_out, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&d->ev_t0) != hipSuccess || hipEventCreate(&d->ev_t1) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), 4 * sizeof(int)) != hipSuccess) {
         set_error("stream/event creation failed");
         return fail(TTS_ERR_HIP);
@@ -530,7 +535,7 @@ void tts_decoder_destroy(tts_decoder* d) {
     }
     for (void* p : d->allocs) (void)hipFree(p);
     if (d->host_flags) (void)hipHostFree(d->host_flags);
-    for (hipEvent_t e : {d->ev_in, d->ev_out, d->ev_t0, d->ev_t1})
+    for (hipEvent_t e : {d->ev_in, d->ev_out, d->ev_t0, d->ev_t1, d->ev_sync})
         if (e) (void)hipEventDestroy(e);
     if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
@@ -688,7 +693,8 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         TTS_HIP(hipEventRecord(d->ev_t1, s));
         TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
         TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-        TTS_HIP(hipStreamSynchronize(s));
+        // a polling wait: the sentence's next stages are enqueued right after it
+        TTS_HIP(spin_sync(s, d->ev_sync));
         if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
             // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
             // stopped before touching any state; use the multi-launch path from now on
@@ -748,7 +754,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     for (;;) {
         // n_active as seen by the next step (its parity slot)
         TTS_HIP(hipMemcpyAsync(d->host_flags, d->state + 2 * (run & 1), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-        TTS_HIP(hipStreamSynchronize(s));
+        TTS_HIP(spin_sync(s, d->ev_sync));
         if (d->host_flags[1] == 0) break;
         TTS_CHECK(run < max_steps + 20, TTS_ERR_HIP, "decoder did not stop within max_steps + 20 (internal error)");
         st = launch_steps(CHUNK);
@@ -756,11 +762,12 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     }
     TTS_HIP(hipEventRecord(d->ev_t1, s));
     TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-    TTS_HIP(hipStreamSynchronize(s));
+    TTS_HIP(spin_sync(s, d->ev_sync));
     }
     int nmax = 0;
     for (int b = 0; b < B; ++b) nmax = std::max(nmax, (int)n_steps[b]);
     const size_t nm = d->nmel;
+    if (!d->keep_hist) {
     TTS_HIP(hipMemcpy2DAsync(mel, (size_t)steps_cap * nm * 4, d->mel_hist, (size_t)d->hist_cap * nm * 4,
                              (size_t)nmax * nm * 4, B, hipMemcpyDeviceToDevice, s));
     TTS_HIP(hipMemcpy2DAsync(stop, (size_t)steps_cap * 4, d->stop_hist, (size_t)d->hist_cap * 4, (size_t)nmax * 4, B,
@@ -770,6 +777,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                                  (size_t)nmax * Lmax * 4, B, hipMemcpyDeviceToDevice, s));
     // the mel history is written unguarded by done[] (see EPI_MEL_FUSED): zero rows past n_steps
     TTS_HIP(launch_zero_tail(mel, (int64_t)steps_cap * nm, d->n_steps, (int)nm, nmax, B, s));
+    }
     if (s != cs) {
         TTS_HIP(hipEventRecord(d->ev_out, s));
         TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
@@ -871,5 +879,13 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
 }  // extern "C"
 
 namespace tts {
-void decoder_set_pipeline(tts_decoder* d, bool on) { d->pipeline = on; }
+void decoder_set_pipeline(tts_decoder* d, bool on) {
+    d->pipeline = on;
+    d->keep_hist = on;
+}
+void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floats, const int** n_steps) {
+    *mel = d->mel_hist;
+    *sentence_floats = (int64_t)d->hist_cap * d->nmel;
+    *n_steps = d->n_steps;
+}
 }  // namespace tts

@@ -16,6 +16,7 @@
 
 #include "conv1d.h"
 #include "encoder_resident.h"
+#include "resident.h"
 #include "sgemm.h"
 
 using namespace tts;
@@ -34,6 +35,7 @@ struct tts_encoder {
     float* emb = nullptr;
     float *Wc[3] = {}, *sc[3] = {}, *sh[3] = {};
     float *Wp = nullptr, *bp = nullptr;  // projection [512][1][2048], bias [2048]
+    float *Wcf[3] = {}, *Wpf = nullptr;  // fragment-order copies (conv_pack_frag): small-batch conv kernel
     float* Whh = nullptr;                // packed [2 directions][64 tiles][16 chunks][64][4]
     int *ids = nullptr, *T = nullptr;
     float *act0 = nullptr, *act1 = nullptr, *xi = nullptr, *h = nullptr, *c = nullptr, *out = nullptr;
@@ -45,6 +47,7 @@ struct tts_encoder {
     unsigned long long* rgran = nullptr;
     long long rtmo = 0;
     unsigned rsalt = 0;
+    bool rgran_clear = false;  // the resident granules were cleared once (then only on a salt wrap)
     int* host_status = nullptr;  // pinned
     bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
     bool status_pending = false;
@@ -66,9 +69,9 @@ tts_status emalloc(tts_encoder* e, T** p, size_t n) {
 }
 
 tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s, bool resident = false) {
-    // outputs past L_b and the initial LSTM state are zero
-    // outputs past L_b are zero; the initial LSTM state is set outside the graph (tts_encoder_run_state)
-    TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
+    // outputs past L_b are zero (the resident form runs one sentence of length Lmax: it writes every
+    // row); the initial LSTM state is set outside the graph (tts_encoder_run_state)
+    if (!resident) TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
     float* bufs[2] = {e->act0, e->act1};
     for (int l = 0; l < 3; ++l) {
         ConvArgs a{};
@@ -77,6 +80,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.table = e->emb;
         a.out = bufs[l & 1];
         a.W = e->Wc[l];
+        a.Wf = e->Wcf[l];
         a.scale = e->sc[l];
         a.shift = e->sh[l];
         a.T = e->T;
@@ -86,6 +90,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.co_pad = EDIM;
         a.act = CONV_RELU;
         a.part = e->part;
+        a.tickets = reinterpret_cast<int*>(e->part + CONV_SPLITK_FLOATS);
         TTS_HIP(conv_launch(a, 5, B, frames, s));
     }
     {
@@ -93,6 +98,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.in = bufs[0];  // conv 3 output
         a.out = e->xi;
         a.W = e->Wp;
+        a.Wf = e->Wpf;
         a.shift = e->bp;
         a.T = e->T;
         a.Tmax = Lmax;
@@ -101,6 +107,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.co_pad = 2 * EG;
         a.act = CONV_NONE;
         a.part = e->part;
+        a.tickets = reinterpret_cast<int*>(e->part + CONV_SPLITK_FLOATS);
         TTS_HIP(conv_launch(a, 1, B, frames, s));
     }
     const int64_t hs = (int64_t)e->Bcap * EH;  // per-direction stride; h slots [2][2][Bcap][H]
@@ -135,23 +142,27 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
 
 // B = 1: the whole recurrence in one direct launch (per-launch salt); h_0 / c_0 come from slot 1 / c,
 // h_n goes to slot (L-1) & 1 (where tts_encoder_run_state reads it) and c_n to c
-tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, hipStream_t s, bool* launched) {
+tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, bool zero_state, hipStream_t s, bool* launched) {
     const int64_t hs = (int64_t)e->Bcap * EH;
-    TTS_HIP(hipMemsetAsync(e->rgran, 0, sizeof(unsigned long long) * encoder_resident_granules(), s));
+    bool wrapped = false;
+    e->rsalt = res_next_salt(e->rsalt, &wrapped);
+    // salted tags and status (resident.h): the granules are cleared once per salt period
+    if (wrapped || !e->rgran_clear)
+        TTS_HIP(hipMemsetAsync(e->rgran, 0, sizeof(unsigned long long) * encoder_resident_granules(), s));
+    e->rgran_clear = true;
     EncResArgs a{};
     a.w = e->rw;
     a.xi = e->xi;
     a.L = Lmax;
     a.hdir = hs;
-    a.h0 = e->h + 2 * hs;
-    a.c0 = e->c;
+    a.h0 = zero_state ? nullptr : e->h + 2 * hs;  // null: the kernel starts from zeros
+    a.c0 = zero_state ? nullptr : e->c;
     a.h_fin = e->h + (int64_t)((Lmax - 1) & 1) * 2 * hs;
     a.c_fin = e->c;
     a.out = e->out;
     a.gran = e->rgran;
     a.status = reinterpret_cast<int*>(e->rgran + encoder_resident_granules() - 2);
     a.tmo = e->rtmo;
-    e->rsalt = (e->rsalt + 1) & 0x3FFFF;
     a.salt = e->rsalt;
     TTS_HIP(launch_encoder_resident(a, s, launched));
     return TTS_OK;
@@ -222,6 +233,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         CK(emalloc(e, &e->sc[l], EDIM));
         CK(emalloc(e, &e->sh[l], EDIM));
         HK(conv_pack(w, EDIM, EDIM, 5, e->Wc[l], s));
+        CK(emalloc(e, &e->Wcf[l], (size_t)EDIM * 5 * EDIM));
+        HK(conv_pack_frag(e->Wc[l], EDIM * 5, EDIM, e->Wcf[l], s));
         HK(fold_bn(bias, g, be, mu, var, EDIM, 1e-5f, e->sc[l], e->sh[l], s));
     }
     CK(emalloc(e, &e->Wp, (size_t)EDIM * 2 * EG));
@@ -240,6 +253,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         HK(sgemm_pack_bias(bih, bhh, EG, ROWMAP_IDENTITY, 0, e->bp + d * EG, s));
         HK(sgemm_pack(whh, EH, nullptr, 0, EG, ROWMAP_LSTM, EH, e->Whh + d * sgemm_packed_floats(EG, EH), s));
     }
+    CK(emalloc(e, &e->Wpf, (size_t)EDIM * 2 * EG));
+    HK(conv_pack_frag(e->Wp, EDIM, 2 * EG, e->Wpf, s));
     e->Bcap = max_batch;
     e->Lcap = max_len;
     const size_t BL = (size_t)max_batch * max_len;
@@ -251,7 +266,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
     CK(emalloc(e, &e->h, (size_t)4 * max_batch * EH));
     CK(emalloc(e, &e->c, (size_t)2 * max_batch * EH));
     CK(emalloc(e, &e->out, BL * EDIM));
-    CK(emalloc(e, &e->part, CONV_SPLITK_FLOATS));
+    CK(emalloc(e, &e->part, CONV_SPLITK_FLOATS + CONV_TICKETS));  // partials, then ticket words (zero at rest)
+    HK(hipMemsetAsync(e->part + CONV_SPLITK_FLOATS, 0, CONV_TICKETS * sizeof(int), s));
     {
         const char* env = getenv("TTS_RESIDENT");
         int dev = 0, ncu = 0, rate_khz = 0;
@@ -289,7 +305,8 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         TTS_HIP(hipEventRecord(e->ev_in, cs));
         TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
     }
-    TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
+    // (tts_synth_run uploads the ids straight into this handle's buffer: encoder_ids_buffer)
+    if (ids != e->ids) TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
     TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
     // initial state (h_0, c_0) of both directions: step 0 reads the parity-1 h slots
     const size_t hs = (size_t)e->Bcap * EH;  // per-direction stride
@@ -308,10 +325,14 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         }
         return TTS_OK;
     };
-    if (tts_status st = init_state()) return st;
     const bool skip_resident = e->skip_resident_once;
     e->skip_resident_once = false;
-    if (e->resident && !skip_resident && B == 1 && lens[0] == Lmax) {
+    const bool try_resident = e->resident && !skip_resident && B == 1 && lens[0] == Lmax;
+    // the resident kernel starts from zeros itself when there is no caller state
+    if (!(try_resident && !state_in)) {
+        if (tts_status st = init_state()) return st;
+    }
+    if (try_resident) {
         auto rit = e->rgraphs.find(Lmax);
         if (rit == e->rgraphs.end()) {
             hipGraph_t g = nullptr;
@@ -328,13 +349,16 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
         TTS_HIP(hipGraphLaunch(rit->second, s));
         bool launched = false;
         {
-            tts_status st = enqueue_encoder_resident(e, Lmax, s, &launched);
+            tts_status st = enqueue_encoder_resident(e, Lmax, !state_in, s, &launched);
             if (st) return st;
         }
         if (!launched) {
             // the grid cannot be co-resident on this device (launch_persistent): nothing ran, the
             // per-step launches below take over for the life of the handle
             e->resident = false;
+            if (!state_in) {
+                if (tts_status st = init_state()) return st;
+            }
         } else {
             e->last_resident = 1;
             TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
@@ -344,8 +368,10 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
                 goto done;
             }
             TTS_HIP(hipStreamSynchronize(s));
+            e->host_status[0] = res_status_code(e->host_status[0], e->rsalt);
             if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
                 e->resident = false;  // rerun below with the per-step launches (same state, untouched)
+                if (tts_status st = init_state()) return st;
             } else if (e->host_status[0] != 0) {
                 // a hand-off wait timed out (a workgroup could not be placed beside another stream's
                 // work): the grid drained; rerun this call with the per-step launches from the
@@ -377,7 +403,8 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
     e->last_resident = 0;
     }
 done:
-    TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
+    // (tts_synth_run hands this handle's own buffer to the decoder: encoder_out_buffer)
+    if (out != e->out) TTS_HIP(hipMemcpyAsync(out, e->out, sizeof(float) * (size_t)B * Lmax * EDIM, hipMemcpyDeviceToDevice, s));
     if (state_out) {
         // h_n of each direction: sentence b wrote its last state at step L_b - 1 (slot (L_b-1) & 1)
         for (int b = 0; b < B; ++b) {
@@ -401,11 +428,16 @@ done:
 
 namespace tts {
 void encoder_set_pipeline(tts_encoder* e, bool on) { e->pipeline = on; }
+int32_t* encoder_ids_buffer(tts_encoder* e, int B, int Lmax) {
+    return (size_t)B * Lmax <= (size_t)e->Bcap * e->Lcap ? e->ids : nullptr;
+}
+float* encoder_out_buffer(tts_encoder* e) { return e->out; }
 
 tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
     *placement_failed = 0;
     if (!e->status_pending) return TTS_OK;
     e->status_pending = false;  // the caller synchronised the stream the status copy ran on
+    e->host_status[0] = res_status_code(e->host_status[0], e->rsalt);
     if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
         e->resident = false;
         *placement_failed = 1;

@@ -91,9 +91,11 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
             info[1] = xcc == xref ? rank : -1;
             info[2] = nref;
             info[3] = 0;
-            if (!ok) __hip_atomic_store((gint*)a.status, 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // status word = salt << 8 | code (res_status_code): no clearing between launches
+            if (!ok) __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | 6u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else if (nref < 2 * ER_SLOTS && c == 0)
-                __hip_atomic_store((gint*)a.status, ENC_RES_STATUS_PLACEMENT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | (unsigned)ENC_RES_STATUS_PLACEMENT), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
@@ -148,7 +150,8 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
             float v[4];
             const bool ok = sweep4(gh, (a.salt << 14) | (unsigned)(s + 1), v, a.tmo);
             if (!ok) {
-                if (lane == 0) __hip_atomic_store((gint*)a.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0)
+                    __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 info[3] = 1;
             }
             *reinterpret_cast<float4*>(hsb[(s + 1) & 1] + lane * 4) = float4{v[0], v[1], v[2], v[3]};

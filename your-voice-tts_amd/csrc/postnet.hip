@@ -14,6 +14,7 @@ struct tts_postnet {
     int n_mel = 80;
     int cin[5], cout[5], co_pad[5];
     float* W[5] = {};
+    float* Wf[5] = {};  // fragment-order copies (conv_pack_frag): the small-batch conv kernel
     float* scale[5] = {};
     float* shift[5] = {};
     float* buf[2] = {};
@@ -29,6 +30,7 @@ void tts_postnet_destroy(tts_postnet* p) {
     if (!p) return;
     for (int i = 0; i < 5; ++i) {
         if (p->W[i]) (void)hipFree(p->W[i]);
+        if (p->Wf[i]) (void)hipFree(p->Wf[i]);
         if (p->scale[i]) (void)hipFree(p->scale[i]);
         if (p->shift[i]) (void)hipFree(p->shift[i]);
     }
@@ -68,17 +70,21 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
         const float* var = find(pre + "1.running_var", co);
         if (!w || !bias || !g || !be || !mu || !var) { tts_postnet_destroy(p); return TTS_ERR_INVALID; }
         const int64_t nw = (int64_t)ci * 5 * p->co_pad[l];
-        if (hipMalloc(&p->W[l], nw * 4) != hipSuccess || hipMalloc(&p->scale[l], co * 4) != hipSuccess ||
+        if (hipMalloc(&p->W[l], nw * 4) != hipSuccess || hipMalloc(&p->Wf[l], nw * 4) != hipSuccess ||
+            hipMalloc(&p->scale[l], co * 4) != hipSuccess ||
             hipMalloc(&p->shift[l], co * 4) != hipSuccess) {
             tts_postnet_destroy(p);
             set_error("hipMalloc failed");
             return TTS_ERR_NOMEM;
         }
         hipError_t e = conv_pack(w, co, ci, 5, p->W[l], s);
+        if (e == hipSuccess) e = conv_pack_frag(p->W[l], ci * 5, p->co_pad[l], p->Wf[l], s);
         if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, 1e-5f, p->scale[l], p->shift[l], s);
         if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     }
-    hipError_t e = hipMalloc(&p->part, CONV_SPLITK_FLOATS * sizeof(float));
+    // split-K partials, then the fused reduction's ticket words (zero at rest)
+    hipError_t e = hipMalloc(&p->part, CONV_SPLITK_FLOATS * sizeof(float) + CONV_TICKETS * sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(p->part + CONV_SPLITK_FLOATS, 0, CONV_TICKETS * sizeof(int), s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     *out = p;
@@ -87,6 +93,18 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
 
 tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, int B, int Tmax, float* out,
                            void* stream) {
+    return tts::postnet_run_dev(p, mel, 0, nullptr, 1, T, B, Tmax, out, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"
+
+namespace tts {
+// tts_postnet_run, optionally with the frame counts already on the device (T_dev[b] * tmul frames:
+// the decoder's step counts) and the input rows mel_tmax frames apart (0 = Tmax): the synthesis
+// path feeds the decoder's mel history in place, with no copy and no host-to-device transfer.
+// T still gives the host-side counts (tile sizes); both must agree.
+tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
+                           int B, int Tmax, float* out, hipStream_t s) {
     TTS_CHECK(p && mel && T && out && B >= 1 && Tmax >= 1, TTS_ERR_INVALID, "bad postnet_run arguments");
     int frames = 0, Tlong = 1;
     for (int b = 0; b < B; ++b) {
@@ -94,7 +112,6 @@ tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, i
         frames += T[b];
         Tlong = std::max(Tlong, (int)T[b]);
     }
-    hipStream_t s = static_cast<hipStream_t>(stream);
     const size_t need = (size_t)B * Tmax * 512;
     if (need > p->buf_floats) {
         for (int i = 0; i < 2; ++i) {
@@ -110,28 +127,32 @@ tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, i
         TTS_HIP(hipMalloc(&p->T, B * sizeof(int)));
         p->Tcap_B = B;
     }
-    TTS_HIP(hipMemcpyAsync(p->T, T, B * sizeof(int), hipMemcpyHostToDevice, s));
+    if (!T_dev) TTS_HIP(hipMemcpyAsync(p->T, T, B * sizeof(int), hipMemcpyHostToDevice, s));
     const float* in = mel;
     for (int l = 0; l < 5; ++l) {
         ConvArgs a{};
         a.in = in;
         a.out = l == 4 ? out : p->buf[l & 1];
         a.W = p->W[l];
+        a.Wf = p->Wf[l];
         a.scale = p->scale[l];
         a.shift = p->shift[l];
         a.resid = l == 4 ? mel : nullptr;
-        a.T = p->T;
+        a.T = T_dev ? T_dev : p->T;
+        a.tmul = T_dev ? tmul : 1;
         a.Tmax = Tmax;
+        a.in_tmax = l == 0 ? mel_tmax : 0;
+        a.res_tmax = l == 4 ? mel_tmax : 0;
         a.Cin = p->cin[l];
         a.Cout = p->cout[l];
         a.co_pad = p->co_pad[l];
         a.act = l < 4 ? CONV_TANH : CONV_NONE;
         a.part = p->part;
+        a.tickets = reinterpret_cast<int*>(p->part + CONV_SPLITK_FLOATS);
         a.Ttile = Tlong;
         TTS_HIP(conv_launch(a, 5, B, frames, s));
         in = a.out;
     }
     return TTS_OK;
 }
-
-}  // extern "C"
+}  // namespace tts

@@ -33,6 +33,17 @@ constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_HATT = 576, GR_HDEC = 2304, GR_PRE2
               GR_QX = 5632, GR_CTXX = 7680, GR_CTXX_STRIDE = ENC + 16, GR_TOTAL = 11904;
 constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-2 rows 8 per CU
 constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
+// the failure code of launch `salt` from its status word (salt << 8 | code; anything else: none)
+inline int res_status_code(int word, unsigned salt) {
+    return ((unsigned)word >> 8) == salt ? (word & 0xFF) : 0;
+}
+// next per-launch salt (18 bits, never 0); *wrapped: tags and status words of launches 2^18 back
+// could match again, the caller clears its granules once
+inline unsigned res_next_salt(unsigned salt, bool* wrapped) {
+    salt = (salt + 1) & 0x3FFFF;
+    *wrapped = salt == 0;
+    return salt == 0 ? 1u : salt;
+}
 
 struct ResWeights {
     float4* wa;   // [256 CU][14 i4][512 thr]   attention LSTM rows over [prenet | ctx | h_att]

@@ -1,4 +1,5 @@
 // Error reporting shared by every entry point of libtts_hip.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -81,6 +82,31 @@ hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args,
     }
     if (e == hipSuccess) *launched = true;
     return e;
+}
+
+// The runtime's stream / event synchronize blocks on an interrupt once its short active wait
+// expires: after a multi-millisecond persistent launch the host woke 35-50 us after the GPU went
+// idle (configs[1] timeline, round 3), and the next stage's launches waited for it.  This records
+// `ev` on `s` and polls it instead (one host core busy for the wait), falling back to the blocking
+// wait after TTS_SPIN_MS milliseconds (default 200; 0 = always block).
+hipError_t spin_sync(hipStream_t s, hipEvent_t ev) {
+    static const long long spin_ns = [] {
+        const char* v = std::getenv("TTS_SPIN_MS");
+        return (long long)((v && v[0]) ? std::atof(v) * 1e6 : 200e6);
+    }();
+    hipError_t e = hipEventRecord(ev, s);
+    if (e != hipSuccess) return e;
+    if (spin_ns > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned k = 0;; ++k) {
+            e = hipEventQuery(ev);
+            if (e != hipErrorNotReady) return e;
+            if ((k & 63) == 63 &&
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > spin_ns)
+                break;
+        }
+    }
+    return hipEventSynchronize(ev);
 }
 
 __global__ void frag_mirror_kernel(const float* src, int64_t ld, int B, int K, float* dst, int ntf) {

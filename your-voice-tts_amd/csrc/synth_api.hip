@@ -206,12 +206,17 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     // is the non-persistent per-iteration form; if its workgroups keep a resident encoder /
     // decoder workgroup from being placed, that launch's bounded waits drain it and the stage
     // re-runs multi-launch (decoder_api.hip, encoder_api.hip): slower, never wrong.
-    TTS_HIP(hipMemcpyAsync(s->ids, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
+    // the ids go straight into the encoder's own buffer, and the decoder reads the encoder's own
+    // output buffer (no device-to-device staging copies)
+    int32_t* ids_dev = tts::encoder_ids_buffer(s->e, B, Lmax);
+    if (!ids_dev) ids_dev = s->ids;
+    float* const enc = tts::encoder_out_buffer(s->e);
+    TTS_HIP(hipMemcpyAsync(ids_dev, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
     s->steps.assign(B, 0);
     for (int attempt = 0;; ++attempt) {
-        if ((st = tts_encoder_run(s->e, s->ids, h_lens, B, Lmax, s->enc, ss))) return st;
+        if ((st = tts_encoder_run(s->e, ids_dev, h_lens, B, Lmax, enc, ss))) return st;
         // synchronises ss: the encoder's placement status is then readable
-        if ((st = tts_decoder_run(s->d, s->enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr,
+        if ((st = tts_decoder_run(s->d, enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr,
                                   s->steps.data(), ss)))
             return st;
         int rerun = 0;
@@ -228,7 +233,16 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
     std::copy(h_frames, h_frames + B, frames);
     float* const post = s->post[par];
-    if ((st = tts_postnet_run(s->p, s->mel, h_frames, B, (int)T, post, ss))) return st;
+    {
+        // the postnet reads the decoder's mel history in place, with the step counts the decoder left
+        // on the device (pipeline mode: no history copies, no frame-count upload)
+        const float* hist = nullptr;
+        int64_t sent_floats = 0;
+        const int* n_dev = nullptr;
+        tts::decoder_histories(s->d, &hist, &sent_floats, &n_dev);
+        if ((st = tts::postnet_run_dev(s->p, hist, (int)(sent_floats / s->nmel), n_dev, s->r, h_frames, B, (int)T, post, ss)))
+            return st;
+    }
     const float* spec = post;
     if (B > 1) {  // GL input is [B][Fmax][nmel]: compact the rows of each sentence
         const size_t row = (size_t)s->nmel * sizeof(float);
