@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
 // a slice of the K = Cin * KW reduction with the MFMA B operands (weights) loaded straight from
 // the packed [Cin][KW][co_pad] layout into registers, CS_PR k-step pairs ahead, and no barrier until
 // the waves' partial tiles are summed (fixed order) for the epilogue.
-constexpr int CS_BM = 16, CS_BN = 32, CS_PR = 16, CS_WAVES = 8, CS_THREADS = 64 * CS_WAVES;
+constexpr int CS_BM = 16, CS_BN = 32, CS_PR = 8, CS_WAVES = 8, CS_THREADS = 64 * CS_WAVES;
 template <int KW>
 __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a) {
     constexpr int PAD = (KW - 1) / 2;
@@ -297,8 +297,20 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     const int Cin = a.Cin, ldx = Cin + 1;
     const int64_t Tin = a.in_tmax ? a.in_tmax : a.Tmax;
     const int* idsb = a.ids ? a.ids + (int64_t)b * a.Tmax : nullptr;
+    // B operands from the fragment-order copy Wf (conv_pack_frag): one float4 per lane per pair
+    // of k-steps = W[k][c0 + r], W[k][c0 + 16 + r] at k = 8 p + q and 8 p + 4 + q; CS_PR pairs
+    // in flight in a register ring (each pair's reload issued right after its MFMAs)
+    const int nks = (Cin * KW) >> 2;
+    const int q = lane >> 4, row = lane & 15;
+    const int np = nks >> 1;  // pairs (K is a multiple of 8)
+    const int p_beg = wave * np / CS_WAVES, p_end = (wave + 1) * np / CS_WAVES;
+    const float4* Wf = reinterpret_cast<const float4*>(a.Wf) + (int64_t)ct * np * 64 + lane;
+    float4 wr[CS_PR];
+#pragma unroll
+    for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)min(p_beg + i, p_end - 1) * 64];
     {
-        // every load of the stage is issued before the first LDS store (one memory round trip)
+        // every load of the stage is issued before the first LDS store (one memory round trip, beside the
+        // first weight loads)
         constexpr int XPT = (XR * 128 + CS_THREADS - 1) / CS_THREADS;  // float4 per thread at Cin <= 512
         float4 xv[XPT];
 #pragma unroll
@@ -322,22 +334,8 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
         }
     }
     __syncthreads();
-    // wave w: k-steps [s_beg, s_end) of the K / 4 steps; lane supplies A[row][q] = x[t0 + row + tap - PAD][ci]
-    // and B[q][n] = W[k][c0 + 16 j + n] for k = 4 s + q = ci * KW + tap
-    const int nks = (Cin * KW) >> 2;
-    const int s_beg = wave * nks / 4, s_end = (wave + 1) * nks / 4;
-    const int q = lane >> 4, row = lane & 15;
-    const float* Wl = a.W + c0 + row;
-    const int64_t cp = a.co_pad;
-    // B operands from the fragment-order copy Wf (conv_pack_frag): one float4 per lane per pair
-    // of k-steps = W[k][c0 + r], W[k][c0 + 16 + r] at k = 8 p + q and 8 p + 4 + q; CS_PR pairs
-    // in flight in a register ring (each pair's reload issued right after its MFMAs)
-    const int np = nks >> 1;  // pairs (K is a multiple of 8)
-    const int p_beg = wave * np / CS_WAVES, p_end = (wave + 1) * np / CS_WAVES;
-    const float4* Wf = reinterpret_cast<const float4*>(a.Wf) + (int64_t)ct * np * 64 + lane;
-    float4 wr[CS_PR];
-#pragma unroll
-    for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)min(p_beg + i, p_end - 1) * 64];
+    // lane supplies A[row][q] = x[t0 + row + tap - PAD][ci] and B[q][n] = W[k][c0 + 16 j + n] for
+    // k = 4 s + q = ci * KW + tap
     int k0 = 8 * p_beg + q;
     int ci = k0 / KW, tap = k0 - ci * KW;
     auto next4 = [&]() {  // k += 4
@@ -520,9 +518,10 @@ hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
         static const int ns_max = getenv("TTS_CONV_NSMAX") ? atoi(getenv("TTS_CONV_NSMAX")) : 16;  // A/B knob
         while (ns * 2 <= ns_max && tiles * ns * 2 <= 1024 && nsteps % (ns * 2) == 0 && nsteps / (ns * 2) >= 2) ns *= 2;
         if (ns > 1 && (size_t)ns * B * ((Tt + 3) & ~3) * a.co_pad <= CONV_SPLITK_FLOATS) {
-            // the reduction rides in the same launch when the caller supplies ticket words
-            // (TTS_CONV_FUSED_REDUCE=0: separate reduce launch, A/B knob)
-            static const bool fused_ok = !(getenv("TTS_CONV_FUSED_REDUCE") && getenv("TTS_CONV_FUSED_REDUCE")[0] == '0');
+            // TTS_CONV_FUSED_REDUCE=1: the reduction rides in the same launch (last-arriving
+            // workgroup per tile); measured slower than the separate reduce launch at batch 1
+            // (34.5 vs 23.3 + 7.4 us per layer), so off by default
+            static const bool fused_ok = getenv("TTS_CONV_FUSED_REDUCE") && getenv("TTS_CONV_FUSED_REDUCE")[0] == '1';
             ConvArgs b = a;
             if (!fused_ok || tiles > CONV_TICKETS) b.tickets = nullptr;
             hipLaunchKernelGGL((conv_kernel<KW, 16, 1, 4, true>), dim3(tiles * ns), block, 0, s, b, ns, B);
