@@ -610,7 +610,7 @@ def main():
                 us_per_step=us, handoff_share_of_step=sum(edges.values()) / us)
     # the headline workload's paths, before any other region runs on the same handles
     paths = dict(decoder="resident" if model.last_timing.get("resident") else "multi-launch",
-                 encoder_bilstm=("resident" if model.last_timing.get("encoder_resident") else "per-step")
+                 encoder_bilstm={1: "resident", 2: "resident-batched"}.get(model.last_timing.get("encoder_path", 0), "per-step")
                  if not gst else "per-step",
                  griffin_lim=ap.last_gl_path())
     cpu = None

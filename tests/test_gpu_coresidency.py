@@ -137,3 +137,38 @@ def test_resident_decoder_timeout_reruns_multilaunch():
     m2 = _t2()
     again = m2.inference_batch(None, enc=enc, lens=[L])
     assert m2.last_timing["resident"] and again["frames"] == want["frames"] == [z["mel"].shape[0]]
+
+
+def test_batched_resident_encoder_matches_per_step_launches():
+    """The batched resident BiLSTM (encoder_resident_batch_kernel: XCD-local hand-offs, MFMA gate
+    rows) on a ragged 64-sentence batch against the per-step launches it replaces (TTS_CU_CAP makes
+    the grid non-co-resident): same outputs within fp32 reduction-order noise, zero rows past each
+    length; a second call takes the resident path again."""
+    w = load_pkg("weights")
+    lens = w.synthetic_lengths(64, 2)
+    ids = torch.zeros(64, int(max(lens)), dtype=torch.long)
+    for b, L in enumerate(lens):
+        ids[b, :int(L)] = torch.from_numpy(w.synthetic_ids(int(L), 200 + b))
+    m = _t2_batch(64)
+    res = m.encode(ids.cuda(), [int(x) for x in lens])
+    assert m._path_timing(*m._handles(ids.shape[1], 64)[:2])["encoder_path"] == 2
+    with _env(TTS_CU_CAP=64):
+        fb = _t2_batch(64)
+        ref = fb.encode(ids.cuda(), [int(x) for x in lens])
+        assert fb._path_timing(*fb._handles(ids.shape[1], 64)[:2])["encoder_path"] == 0
+    for b, L in enumerate(lens):
+        L = int(L)
+        d = float((res[b, :L] - ref[b, :L]).norm() / ref[b, :L].norm())
+        assert d < 1e-5, (b, d)
+        assert torch.all(res[b, L:] == 0)
+    again = m.encode(ids.cuda(), [int(x) for x in lens])
+    assert torch.equal(again, res)  # deterministic
+
+
+def _t2_batch(max_batch):
+    t2 = load_pkg("tacotron2")
+    fl = golden_flags(golden("t2_fwdmask_L100"))
+    m = t2.Tacotron2(130, 0, r=1, attn_win=fl["attn_win"], attn_norm=fl["attn_norm"], forward_attn=fl["forward_attn"],
+                     trans_agent=fl["trans_agent"], forward_attn_mask=fl["forward_attn_mask"],
+                     location_attn=fl["location_attn"], max_batch=max_batch)
+    return m.cuda().eval()

@@ -46,6 +46,9 @@ void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floa
 tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
                            int B, int Tmax, float* out, hipStream_t s);
 void gl_set_pipeline(tts_gl* g, bool on);
+// griffin_lim.hip: tts_gl_run with the frame counts also on the device (F_dev, or null)
+tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, const int* F_dev, int B, int Fmax,
+                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 
 // Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent

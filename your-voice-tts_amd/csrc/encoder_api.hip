@@ -48,12 +48,20 @@ struct tts_encoder {
     long long rtmo = 0;
     unsigned rsalt = 0;
     bool rgran_clear = false;  // the resident granules were cleared once (then only on a salt wrap)
+    unsigned rsalt_pending = 0;  // salt of the launch whose status a pipeline collects later
+    bool pending_batch = false;  // ... and whether it was the batched form
     int* host_status = nullptr;  // pinned
     bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
     bool status_pending = false;
     bool skip_resident_once = false;  // a pipelined resident run timed out: its rerun goes per-step
     int res_timeouts = 0;             // resident runs that timed out a hand-off and re-ran per-step
     std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
+    // batched resident BiLSTM (encoder_resident.h, 2 <= B <= 64, no caller state)
+    float* whh_raw = nullptr;                // [2][1024][256] W_hh, reference layout
+    unsigned long long* bgran = nullptr;     // encoder_resident_batch_granules()
+    unsigned bsalt = 0;
+    bool bgran_clear = false;
+    std::map<std::pair<int, int>, hipGraphExec_t> bgraphs;  // convs + projection, by (B, Lmax)
     int last_resident = 0;                  // the last run's BiLSTM path (tts_encoder_last_path)
 };
 
@@ -69,9 +77,9 @@ tts_status emalloc(tts_encoder* e, T** p, size_t n) {
 }
 
 tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStream_t s, bool resident = false) {
-    // outputs past L_b are zero (the resident form runs one sentence of length Lmax: it writes every
-    // row); the initial LSTM state is set outside the graph (tts_encoder_run_state)
-    if (!resident) TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
+    // outputs past L_b are zero (the batch-1 resident form runs one sentence of length Lmax: it
+    // writes every row); the initial LSTM state is set outside the graph (tts_encoder_run_state)
+    if (!(resident && B == 1)) TTS_HIP(hipMemsetAsync(e->out, 0, sizeof(float) * (size_t)B * Lmax * EDIM, s));
     float* bufs[2] = {e->act0, e->act1};
     for (int l = 0; l < 3; ++l) {
         ConvArgs a{};
@@ -177,6 +185,7 @@ void tts_encoder_destroy(tts_encoder* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (auto& kv : e->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto& kv : e->rgraphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : e->bgraphs) (void)hipGraphExecDestroy(kv.second);
     if (e->host_status) (void)hipHostFree(e->host_status);
     for (void* p : e->allocs) (void)hipFree(p);
     for (hipEvent_t ev : {e->ev_in, e->ev_out})
@@ -281,6 +290,14 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
             HK(encoder_resident_pack(get("encoder.lstm.weight_hh_l0", (int64_t)EG * EH),
                                      get("encoder.lstm.weight_hh_l0_reverse", (int64_t)EG * EH), e->rw, s));
             HK(hipHostMalloc(reinterpret_cast<void**>(&e->host_status), sizeof(int)));
+            if (max_batch >= 2) {
+                CK(emalloc(e, &e->whh_raw, (size_t)2 * EG * EH));
+                HK(hipMemcpyAsync(e->whh_raw, get("encoder.lstm.weight_hh_l0", (int64_t)EG * EH), sizeof(float) * EG * EH,
+                                  hipMemcpyDeviceToDevice, s));
+                HK(hipMemcpyAsync(e->whh_raw + (size_t)EG * EH, get("encoder.lstm.weight_hh_l0_reverse", (int64_t)EG * EH),
+                                  sizeof(float) * EG * EH, hipMemcpyDeviceToDevice, s));
+                CK(emalloc(e, &e->bgran, encoder_resident_batch_granules()));
+            }
             e->rtmo = (long long)rate_khz * 50;  // 50 ms per hand-off wait
             e->resident = true;
         }
@@ -361,6 +378,8 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
             }
         } else {
             e->last_resident = 1;
+            e->rsalt_pending = e->rsalt;
+            e->pending_batch = false;
             TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
                                    hipMemcpyDeviceToHost, s));
             if (e->pipeline) {  // the pipeline reads the status at its next synchronisation point
@@ -381,6 +400,60 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
             } else {
                 goto done;
             }
+        }
+    }
+    static const bool batch_off = getenv("TTS_ENC_BATCH_RESIDENT") && getenv("TTS_ENC_BATCH_RESIDENT")[0] == '0';  // A/B knob
+    if (e->resident && e->bgran && !skip_resident && B >= 2 && !state_in && !batch_off) {
+        // batched resident BiLSTM: the convs + projection graph, then one persistent launch
+        auto key = std::make_pair(B, Lmax);
+        auto bit = e->bgraphs.find(key);
+        if (bit == e->bgraphs.end()) {
+            hipGraph_t g = nullptr;
+            TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            tts_status st = enqueue_encoder(e, B, Lmax, B * Lmax, s, true);
+            hipError_t ee = hipStreamEndCapture(s, &g);
+            if (st) return st;
+            TTS_HIP(ee);
+            hipGraphExec_t exec = nullptr;
+            TTS_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+            TTS_HIP(hipGraphDestroy(g));
+            bit = e->bgraphs.emplace(key, exec).first;
+        }
+        TTS_HIP(hipGraphLaunch(bit->second, s));
+        bool wrapped = false;
+        e->bsalt = res_next_salt(e->bsalt, &wrapped);
+        if (wrapped || !e->bgran_clear)
+            TTS_HIP(hipMemsetAsync(e->bgran, 0, sizeof(unsigned long long) * encoder_resident_batch_granules(), s));
+        e->bgran_clear = true;
+        EncResBatchArgs ba{};
+        ba.whh = e->whh_raw;
+        ba.xi = e->xi;
+        ba.lens = e->T;
+        ba.B = B;
+        ba.Tmax = Lmax;
+        ba.out = e->out;
+        ba.gran = e->bgran;
+        ba.status = reinterpret_cast<int*>(e->bgran + encoder_resident_batch_granules() - 2);
+        ba.tmo = e->rtmo;
+        ba.salt = e->bsalt;
+        bool launched = false;
+        TTS_HIP(launch_encoder_resident_batch(ba, s, &launched));
+        if (launched) {
+            e->last_resident = 2;
+            e->rsalt_pending = e->bsalt;
+            e->pending_batch = true;
+            TTS_HIP(hipMemcpyAsync(e->host_status, ba.status, sizeof(int), hipMemcpyDeviceToHost, s));
+            if (e->pipeline) {
+                e->status_pending = true;
+                goto done;
+            }
+            TTS_HIP(hipStreamSynchronize(s));
+            e->host_status[0] = res_status_code(e->host_status[0], e->bsalt);
+            if (e->host_status[0] == 0) goto done;
+            // placement failed or a hand-off wait timed out: rerun with the per-step launches
+            if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) e->bgran = nullptr;  // not on this device
+            else ++e->res_timeouts;
+            if (tts_status st = init_state()) return st;
         }
     }
     {
@@ -437,9 +510,10 @@ tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
     *placement_failed = 0;
     if (!e->status_pending) return TTS_OK;
     e->status_pending = false;  // the caller synchronised the stream the status copy ran on
-    e->host_status[0] = res_status_code(e->host_status[0], e->rsalt);
+    e->host_status[0] = res_status_code(e->host_status[0], e->rsalt_pending);
     if (e->host_status[0] == ENC_RES_STATUS_PLACEMENT) {
-        e->resident = false;
+        if (e->pending_batch) e->bgran = nullptr;  // the batched form cannot be placed on this device
+        else e->resident = false;
         *placement_failed = 1;
         return TTS_OK;
     }

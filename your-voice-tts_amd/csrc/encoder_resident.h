@@ -23,6 +23,24 @@ struct EncResArgs {
                          // so no granule (or stale cache line) of an earlier launch can match
 };
 
+// Batched form (2 <= B <= 64, sentences at their own lengths, zero initial state): every XCD runs
+// one direction (xcc & 1) for one group of up to 16 sentences (xcc >> 1), its 32 workgroups each
+// holding 8 hidden units' W_hh rows as MFMA operands in registers; the step's h all-gather stays
+// inside the XCD.  Needs >= 32 workgroups on every XCD (else status ENC_RES_STATUS_PLACEMENT).
+struct EncResBatchArgs {
+    const float* whh;    // [2][1024][256] W_hh (reference layout, forward then reverse)
+    const float* xi;     // [B][Tmax][2][1024] input projection + both biases
+    const int* lens;     // [B]
+    int B, Tmax;
+    float* out;          // [B][Tmax][512]
+    unsigned long long* gran;  // encoder_resident_batch_granules() u64
+    int* status;         // salt << 8 | code on failure (res_status_code)
+    long long tmo;
+    unsigned salt;
+};
+size_t encoder_resident_batch_granules();  // includes the trailing status word
+hipError_t launch_encoder_resident_batch(const EncResBatchArgs& a, hipStream_t s, bool* launched);
+
 size_t encoder_resident_weight_float4();
 size_t encoder_resident_granules();  // includes the trailing status word
 hipError_t encoder_resident_pack(const float* whh_fwd, const float* whh_bwd, float4* out, hipStream_t s);

@@ -165,6 +165,160 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
     }
 }
 
+// ---------------------------------------------------------------- batched form (B >= 2)
+// XCD x: direction x & 1, sentences [g G, g G + G) with g = x >> 1 and G = ceil(B / 4).  Workgroup
+// of rank r (in its XCD) owns hidden units [8 r, 8 r + 8): W_hh rows j = 4 u + gate (u < 8) as two
+// 16-row MFMA A tiles.  Per step s, wave w multiplies tile w & 1 over k-steps [16 (w >> 1), +16)
+// (v_mfma_f32_16x16x4_f32, A = W rows in registers, B = h_{s-1}^T of the group's 16 sentence
+// columns from LDS); the 4 partial tiles of each row tile are summed in wave order through LDS;
+// waves 0 / 1 then hold, per lane, the 4 gate sums of one (unit, sentence) and update (c, h)
+// exactly as the ENC_LSTM epilogue (the input projection xi, both biases folded, added first);
+// h goes to the output row and to an XCD-local {tag, h} granule; every wave then gathers the
+// group's 256 x 16 granules into the other LDS h buffer.
+constexpr int EB_THREADS = 512, EB_UNITS = 8, EB_G = 16, EB_LDH = H + 4;
+constexpr int EB_GR_TABLE = 0, EB_GR_H = 256, EB_GR_PER = EB_G * H;  // per (parity, XCD)
+
+__global__ __launch_bounds__(EB_THREADS, 1) void encoder_resident_batch_kernel(const EncResBatchArgs a) {
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    __shared__ __align__(16) float hs[2][EB_G][EB_LDH];  // h_{s-1} of the group's sentences, by parity
+    __shared__ __align__(16) float red[8][64][4];        // partial gate tiles
+    __shared__ int info[4];
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    const unsigned setup_tag = (a.salt << 14) | 0x3FFFu;
+    if (tid == 0) pub_dev(a.gran + EB_GR_TABLE + c, setup_tag, __int_as_float(xcc));
+    if (wave == 0) {
+        float v[4];
+        const bool ok = sweep4(a.gran + EB_GR_TABLE, setup_tag, v, a.tmo);
+        int rank = 0, nmin = 256;
+        for (int x = 0; x < 8; ++x) {
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int xi = __float_as_int(v[i]) & 7;
+                cnt += __popcll(__ballot(xi == x));
+                if (x == xcc) rank += __popcll(__ballot(xi == x && lane * 4 + i < c));
+            }
+            nmin = min(nmin, cnt);
+        }
+        if (lane == 0) {
+            info[0] = ok ? 1 : 0;
+            info[1] = rank;
+            info[2] = nmin;
+            info[3] = 0;
+            if (!ok) __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | 6u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (nmin < 32 && c == 0)
+                __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | (unsigned)ENC_RES_STATUS_PLACEMENT), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const int rank = info[1];
+    if (!info[0] || info[2] < 32 || rank >= 32) return;
+    const int dir = xcc & 1, G = (a.B + 3) / 4, b0 = (xcc >> 1) * G;
+    const int nb = max(0, min(G, a.B - b0));  // sentences of this group
+    if (nb == 0) return;
+    int Lg = 0;
+    for (int n = 0; n < nb; ++n) Lg = max(Lg, a.lens[b0 + n]);
+    // A operands: tile rt = wave & 1, k-steps [16 kq, 16 kq + 16), kq = wave >> 1
+    const int rt = wave & 1, kq = wave >> 1, row = lane & 15, q = lane >> 4;
+    float wa[16];
+    {
+        const int j = rt * 16 + row, unit = rank * EB_UNITS + (j >> 2), gate = j & 3;
+        const float* wr = a.whh + ((int64_t)dir * G4 + gate * H + unit) * H + q;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wa[i] = wr[4 * (16 * kq + i)];
+    }
+    for (int i = tid; i < 2 * EB_G * EB_LDH; i += EB_THREADS) (&hs[0][0][0])[i] = 0.f;
+    // waves 0 / 1: lane's (unit, sentence n) and its cell
+    const int n = lane & 15, unit = rank * EB_UNITS + 4 * rt + (lane >> 4);
+    const int bsen = b0 + n, Ln = n < nb ? a.lens[bsen] : 0;
+    float cs = 0.f, hprev = 0.f;
+    float xg[4] = {0.f, 0.f, 0.f, 0.f};
+    auto load_xi = [&](int s) {
+        if (wave < 2 && s < Ln) {
+            const int pos = dir ? Ln - 1 - s : s;
+            const float* x = a.xi + ((int64_t)bsen * a.Tmax + pos) * (2 * G4) + dir * G4 + unit;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) xg[g] = x[g * H];
+        }
+    };
+    load_xi(0);
+    __syncthreads();
+    u64* gx = a.gran + EB_GR_H;  // + (parity * 8 + xcc) * EB_GR_PER
+    for (int s = 0; s < Lg; ++s) {
+        const int par = s & 1;
+        // ---- partial gates: 16 MFMAs over this wave's k quarter, B = h^T[k][n] from LDS
+        floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+        const float* hrow = &hs[par][n][0];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc = mfma16x16x4(wa[i], hrow[4 * (16 * kq + i) + q], acc);
+        *reinterpret_cast<floatx4*>(&red[wave][lane][0]) = acc;
+        __syncthreads();
+        if (wave < 2) {
+            floatx4 sum = *reinterpret_cast<const floatx4*>(&red[rt][lane][0]);
+#pragma unroll
+            for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const floatx4*>(&red[rt + 2 * w][lane][0]);
+            // D lane l holds rows 4 (l >> 4) + r of tile rt = gate r of unit 4 rt + (l >> 4), column n
+            const bool act = s < Ln;
+            const float gi = sum[0] + xg[0], gf = sum[1] + xg[1], gg = sum[2] + xg[2], go = sum[3] + xg[3];
+            load_xi(s + 1);  // next step's input projection, in flight during the hand-off
+            if (act) {
+                const float c2 = sigmoidf_(gf) * cs + sigmoidf_(gi) * tanhf(gg);
+                const float h = sigmoidf_(go) * tanhf(c2);
+                cs = c2;
+                hprev = h;
+                const int pos = dir ? Ln - 1 - s : s;
+                a.out[((int64_t)bsen * a.Tmax + pos) * (2 * H) + dir * H + unit] = h;
+            }
+            // every lane publishes (idle sentences: their last h) so the gather sees every tag
+            pub_xcd(gx + (int64_t)(par * 8 + xcc) * EB_GR_PER + n * H + unit, (a.salt << 14) | (unsigned)(s + 1), hprev);
+        }
+        // ---- gather the group's h_s into the other buffer: thread t sweeps granules t + 512 i
+        {
+            const unsigned tag = (a.salt << 14) | (unsigned)(s + 1);
+            u64* gp = gx + (int64_t)(par * 8 + xcc) * EB_GR_PER;
+            long long t_end = 0;
+            constexpr int PER = EB_GR_PER / EB_THREADS;  // 8
+            float v[PER];
+            bool ok = true;
+            for (int spin = 0;; ++spin) {
+                ok = true;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) {
+                    const int gidx = tid + i * EB_THREADS, nn = gidx / H;
+                    if (nn < nb) {
+                        const u64 x = peek(gp + gidx);
+                        v[i] = __uint_as_float((unsigned)x);
+                        ok = ok && (unsigned)(x >> 32) == tag;
+                    } else {
+                        v[i] = 0.f;
+                    }
+                }
+                if (__all(ok)) break;
+                if (spin == 0) t_end = (long long)wall_clock64() + a.tmo;
+                else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) break;
+                if (ENC_SLEEP) __builtin_amdgcn_s_sleep(ENC_SLEEP);
+            }
+            if (!__all(ok)) {
+                if (lane == 0) {
+                    __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    info[3] = 1;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int gidx = tid + i * EB_THREADS;
+                hs[par ^ 1][gidx / H][gidx % H] = v[i];
+            }
+        }
+        __syncthreads();
+        if (info[3]) return;
+    }
+}
+
 __global__ void enc_res_pack_kernel(const float* whh_f, const float* whh_b, float4* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)2 * ER_SLOTS * 16 * ER_THREADS) return;
@@ -178,6 +332,17 @@ __global__ void enc_res_pack_kernel(const float* whh_f, const float* whh_b, floa
 }
 
 }  // namespace
+
+size_t encoder_resident_batch_granules() { return EB_GR_H + (size_t)2 * 8 * EB_GR_PER + 2; }
+
+hipError_t launch_encoder_resident_batch(const EncResBatchArgs& a, hipStream_t s, bool* launched) {
+    *launched = false;
+    if (a.B < 2 || a.B > 4 * EB_G) return hipErrorInvalidValue;
+    EncResBatchArgs arg = a;
+    void* args[] = {&arg};
+    return launch_persistent(reinterpret_cast<const void*>(&encoder_resident_batch_kernel), dim3(256), dim3(EB_THREADS),
+                             args, 0, s, launched);
+}
 
 size_t encoder_resident_weight_float4() { return (size_t)2 * ER_SLOTS * 16 * ER_THREADS; }
 size_t encoder_resident_granules() { return GR_H + 4 * H + 2; }

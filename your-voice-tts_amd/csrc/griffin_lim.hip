@@ -388,7 +388,12 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
 #pragma unroll
         for (int i = 0; i < FW; ++i) {
             const int f = wave * FW + i;
-            if (f < nf) S[(int64_t)f * NB + k] = (spec_t)pow(fmax(acc[i], 1e-10), (double)a.power);
+            if (f < nf) {
+                // power 1.5 (the reference configs): x * sqrt(x), within an ulp of pow in float64
+                // and far below the float32 rounding of the stored value; else pow
+                const double x = fmax(acc[i], 1e-10);
+                S[(int64_t)f * NB + k] = (spec_t)(a.power == 1.5f ? x * sqrt(x) : pow(x, (double)a.power));
+            }
         }
     }
 }
@@ -1184,6 +1189,7 @@ struct FinArgs {
     float* y;  // [B][Nmax]
     int64_t Nmax;
     const int* status;  // the persistent loop's status word, or null: nonzero poisons the signal (NaN)
+    int* host_status;   // pinned host word the status is copied to by thread 0 of block (0, 0), or null
     const float* wssp;  // [hop] float32 window sum-square of a sample whose every contributing frame
                         // exists, by (q - woff) mod hop (summed on the host in ola_sample's order)
 };
@@ -1194,6 +1200,8 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     const int Fb = a.F[b];
     const int N = a.g.hop * (Fb - 1);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a.host_status && p == 0 && b == 0)  // the persistent loop's status, for the host's collect
+        __hip_atomic_store(a.host_status, *a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (p >= N) return;
     // a persistent loop whose hand-off wait timed out left frames unwritten: never hand out a
     // plausible-looking waveform for it (the run's error status is raised when it is collected)
@@ -1593,11 +1601,22 @@ extern "C" {
 
 tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
                       const double* phase_u, uint64_t seed, int iters, double* wav, void* stream) {
+    return tts::gl_run_dev(g, mode, spec, F, nullptr, B, Fmax, phase_u, seed, iters, wav, static_cast<hipStream_t>(stream));
+}
+}  // extern "C"
+
+namespace tts {
+// tts_gl_run, optionally with the frame counts also on the device (F_dev, the same values as F:
+// tts_synth_run passes the decoder's step counts at r = 1): the persistent loop's launches then
+// read them there and the upload is skipped (the graph-replayed fallbacks still upload into the
+// handle's own array, which their graphs bake in).
+tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, const int* F_dev, int B, int Fmax,
+                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream) {
     TTS_CHECK(g && spec && F && wav && B >= 1 && Fmax >= 2 && iters >= 0, TTS_ERR_INVALID, "bad gl_run arguments");
     TTS_CHECK(mode == TTS_GL_FROM_MEL || mode == TTS_GL_FROM_LINEAR, TTS_ERR_INVALID, "bad mode");
     TTS_CHECK(mode == TTS_GL_FROM_LINEAR || g->pinv, TTS_ERR_INVALID, "mel mode needs inv_mel_basis at create");
     for (int b = 0; b < B; ++b) TTS_CHECK(F[b] >= 2 && F[b] <= Fmax, TTS_ERR_INVALID, "F[b] out of range [2, Fmax]");
-    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t cs = stream;
     hipStream_t s = g->pipeline ? cs : g->stream;
     const Geo geo = g->g;
     const int64_t Nmax = (int64_t)geo.hop * (Fmax - 1);
@@ -1639,13 +1658,22 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipEventRecord(g->ev_in, cs));
         TTS_HIP(hipStreamWaitEvent(s, g->ev_in, 0));
     }
-    TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+    // path choice (host values only): small batches fuse the overlap-add into the iteration launch;
+    // at most 256 frames in all run the whole loop as one persistent launch
+    const char* fz = getenv("TTS_GL_FUSED");
+    const bool fused = ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
+    int frames_total = 0;
+    for (int b = 0; b < B; ++b) frames_total += F[b];
+    const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+    // the launches read the frame counts from F_dev when the persistent loop takes them all
+    const int* Fd = persistent && F_dev ? F_dev : g->F;  // (reassigned if the persistent launch falls back)
+    if (Fd == g->F) TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
     MagArgs ma{};
     ma.mode = mode;
     ma.spec = spec;
     ma.n_in = mode == TTS_GL_FROM_MEL ? g->cfg.num_mels : NB;
     ma.Fmax = Fmax;
-    ma.F = g->F;
+    ma.F = Fd;
     ma.pinv = g->pinv;
     ma.S = g->S;
     ma.min_db = g->cfg.min_level_db;
@@ -1659,16 +1687,9 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                        0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
-    // small batches: overlap-add fused into the iteration launch (one launch per iteration); at most
-    // 256 frames in all: the whole loop as one persistent launch (one workgroup per frame), whose
-    // iterations write slots of their own: a frame slot is never rewritten inside the launch, so no
-    // XCD's L2 can hold an earlier copy of the bytes an iteration reads
-    // (TTS_GL_FUSED=1 forces the fused form at any batch: measurement knob)
-    const char* fz = getenv("TTS_GL_FUSED");
-    const bool fused = ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
-    int frames_total = 0;
-    for (int b = 0; b < B; ++b) frames_total += F[b];
-    const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+    // the persistent loop (one workgroup per frame) writes every iteration to slots of its own: a
+    // frame slot is never rewritten inside the launch, so no XCD's L2 can hold an earlier copy of
+    // the bytes an iteration reads (TTS_GL_FUSED=1 forces the fused form at any batch: measurement knob)
     // frame storage: float64 for the small-batch fused / persistent loops, float32 for the batched
     // loop and for the forced fused form (TTS_GL_FUSED=1, whose waveform the tests compare bitwise
     // with the batched loop's)
@@ -1690,7 +1711,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     };
     IterArgs ia{};
     ia.S = g->S;
-    ia.F = g->F;
+    ia.F = Fd;
     ia.Fmax = Fmax;
     ia.B = B;
     ia.g = geo;
@@ -1723,7 +1744,7 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipGetLastError());
     TTS_HIP(hipEventRecord(g->ev_t0, s));
     FinArgs fa{};
-    fa.F = g->F;
+    fa.F = Fd;
     fa.Fmax = Fmax;
     fa.B = B;
     fa.g = geo;
@@ -1782,6 +1803,13 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             fprintf(stderr, "\n");
         }
     }
+    if (!persistent_ran && Fd != g->F) {
+        // the persistent loop could not be placed: its fallbacks replay graphs that bake the
+        // handle's own frame-count array in
+        TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+        Fd = g->F;
+        ia.F = fa.F = Fd;
+    }
     if (!persistent_ran && iters > 0) {
         // one iteration = overlap-add of the previous frames into the float32 signal (every
         // sample once) + one workgroup per frame for STFT -> phase -> iSTFT of that signal
@@ -1822,9 +1850,11 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     TTS_HIP(hipEventRecord(g->ev_t1, s));
     fa.frames = persistent_ran ? static_cast<void*>(g->pfr + (size_t)iters * fstride) : slot(iters);
     fa.status = persistent_ran ? g->pstatus : nullptr;
+    fa.host_status = persistent_ran ? g->host_status : nullptr;  // (no read-back copy launch)
     if (f64) hipLaunchKernelGGL(gl_ola_kernel<pframe_t>, ogrid, oblock, 0, s, fa);
     else hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, fa);
     fa.status = nullptr;
+    fa.host_status = nullptr;
     TTS_HIP(hipGetLastError());
     {
         // de-emphasis chunks: each starts `look` samples early, |c|^look <= 1e-22; one chunk per
@@ -1837,14 +1867,13 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             else chunk = Nmax;
         }
         const dim3 sgrid((unsigned)((Nmax + chunk - 1) / chunk), B);
-        hipLaunchKernelGGL(preemph_scan_kernel, sgrid, dim3(SCAN_THREADS), 0, s, g->y, Nmax, g->F, geo.hop, c,
+        hipLaunchKernelGGL(preemph_scan_kernel, sgrid, dim3(SCAN_THREADS), 0, s, g->y, Nmax, Fd, geo.hop, c,
                            c != 0.0 ? 1 : 0, chunk, look, wav);
     }
     TTS_HIP(hipGetLastError());
     g->last_persistent = persistent_ran;
     g->last_path = persistent_ran ? TTS_GL_PATH_PERSISTENT : fused ? TTS_GL_PATH_FUSED : TTS_GL_PATH_UNFUSED;
     g->last_launches = persistent_ran ? 1 : (fused ? 1 : 2) * iters;
-    if (persistent_ran) TTS_HIP(hipMemcpyAsync(g->host_status, g->pstatus, sizeof(int), hipMemcpyDeviceToHost, s));
     TTS_HIP(hipEventRecord(g->ev_done, s));
     if (s != cs) TTS_HIP(hipStreamWaitEvent(cs, g->ev_done, 0));
     g->pending = true;
@@ -1860,6 +1889,10 @@ tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     g->last_fstride = fstride;
     return TTS_OK;
 }
+
+}  // namespace tts
+
+extern "C" {
 
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) {
     TTS_CHECK(g && kernel_ms && n_kernels >= TTS_GL_KERNELS && reps >= 1, TTS_ERR_INVALID, "bad profile arguments");

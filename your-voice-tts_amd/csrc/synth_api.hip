@@ -265,7 +265,14 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
     // shorter sentences leave their waveform tail unwritten: zero it
     if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
-    if ((st = tts_gl_run(s->g, TTS_GL_FROM_MEL, spec, h_frames, B, Fmax, nullptr, seed, gl_iters, wav, gs))) return st;
+    // at r = 1 the decoder's device step counts are the frame counts: no upload
+    const float* hist_unused = nullptr;
+    int64_t sf_unused = 0;
+    const int* n_dev = nullptr;
+    tts::decoder_histories(s->d, &hist_unused, &sf_unused, &n_dev);
+    if ((st = tts::gl_run_dev(s->g, TTS_GL_FROM_MEL, spec, h_frames, s->r == 1 ? n_dev : nullptr, B, Fmax, nullptr, seed,
+                              gl_iters, wav, gs)))
+        return st;
     TTS_HIP(hipEventRecord(s->ev_out, gs));
     TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
     return TTS_OK;
