@@ -1105,17 +1105,21 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads),
         // straight into the first butterfly's registers
         double2 v[4];
+        // every contributor load of the thread's 8 samples is issued before the first sum (one
+        // memory round trip per iteration instead of one per sample; absent contributors load
+        // slot 0 of this frame's block and are masked to exact zeros)
+        double fv[PN][OLA_MAX];
 #pragma unroll
-        for (int i = 0; i < PN; ++i) {
-            double fv[OLA_MAX];
+        for (int i = 0; i < PN; ++i)
 #pragma unroll
             for (int k = 0; k < OLA_MAX; ++k)
-                fv[k] = off[i][k] >= 0 ? __longlong_as_double((long long)__hip_atomic_load(
-                                             (gu64_t*)(src + off[i][k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                                       : 0.0;
+                fv[i][k] = __longlong_as_double((long long)__hip_atomic_load(
+                    (gu64_t*)(src + (off[i][k] >= 0 ? off[i][k] : 0)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+        for (int i = 0; i < PN; ++i) {
             float y = 0.f;
 #pragma unroll
-            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + fv[k]);
+            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (off[i][k] >= 0 ? fv[i][k] : 0.0));
             const float yv = wssv[i] > 1.17549435e-38f ? y / wssv[i] : y;
             if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
             else v[i >> 1].x = wi[i] * (double)yv;
