@@ -92,12 +92,18 @@ def test_resident_deterministic_and_batches_unaffected(models):
     x = res.inference_batch([ids])
     y = res.inference_batch([ids])
     assert torch.equal(x["mel"], y["mel"]) and torch.equal(x["align"], y["align"])
-    # a batch of 2 on the same handle takes the multi-launch path and matches it
+    # a batch of 2 on the same handle takes the multi-launch decoder and matches it; its encoder is
+    # the batched resident BiLSTM (XCD-parallel, MFMA gate rows) where `ml` runs the per-step
+    # launches, so the two agree to fp32 reduction-order noise rather than bit for bit
     ids2 = w.synthetic_ids(40, 2)
     z = res.inference_batch([ids, ids2])
     assert not res.last_timing["resident"]
     zz = ml.inference_batch([ids, ids2])
-    assert torch.equal(z["mel"], zz["mel"])
+    assert list(z["frames"]) == list(zz["frames"])
+    for b, T in enumerate(z["frames"]):
+        a, r = z["mel"][b, :int(T)].double(), zz["mel"][b, :int(T)].double()
+        assert float((a - r).norm() / r.norm()) < 1e-4, b
+    assert torch.equal(res.inference_batch([ids, ids2])["mel"], z["mel"])  # deterministic
     # and a batch-1 call afterwards is resident again and unchanged
     x2 = res.inference_batch([ids])
     assert res.last_timing["resident"] and torch.equal(x2["mel"], x["mel"])

@@ -41,6 +41,11 @@ void decoder_set_pipeline(tts_decoder* d, bool on);
 // the decoder's mel history (sentence b at mel + b * sentence_floats, rows of nmel * r floats) and
 // its device step counts, where a pipeline-mode run (decoder_set_pipeline) leaves its output
 void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floats, const int** n_steps);
+// work to enqueue behind the batch-1 resident launch before the host waits for it (null: none;
+// cleared when pipeline mode ends); decoder_hook_ran: the last run enqueued it AND its result is the
+// resident launch's (false after a multi-launch rerun: the caller enqueues that work again)
+void decoder_set_post_hook(tts_decoder* d, void (*fn)(void*, hipStream_t), void* ctx);
+bool decoder_hook_ran(tts_decoder* d);
 // postnet.hip: tts_postnet_run with device frame counts (T_dev[b] * tmul) and input rows mel_tmax
 // frames apart (0 = Tmax); T holds the same counts on the host
 tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
@@ -70,6 +75,7 @@ int usable_cus();
 // record `ev` on `s` and wait for it by polling (runtime.hip: the blocking wait's wake-up latency
 // sits on the synthesis critical path)
 hipError_t spin_sync(hipStream_t s, hipEvent_t ev);
+hipError_t spin_wait(hipEvent_t ev);  // the same wait on an event already recorded
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 

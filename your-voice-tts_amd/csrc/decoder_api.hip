@@ -67,7 +67,12 @@ struct tts_decoder {
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
     float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
-    int* host_flags = nullptr;  // pinned
+    int* host_flags = nullptr;  // pinned: [0, 4) flags, [4, 4 + 64) step counts (read-back target)
+    // tts_synth_run: work enqueued behind a resident launch before the host waits for it (the
+    // postnet, reading the device step counts); hook_ran reports that it was enqueued
+    void (*post_hook)(void*, hipStream_t) = nullptr;
+    void* post_ctx = nullptr;
+    bool hook_ran = false;
     std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
     bool pipeline = false;  // tts_synth_run: work on the caller's stream
@@ -331,7 +336,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         hipEventCreateWithFlags(&d->ev_out, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&d->ev_t0) != hipSuccess || hipEventCreate(&d->ev_t1) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), 4 * sizeof(int)) != hipSuccess) {
+        hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), (4 + 64) * sizeof(int)) != hipSuccess) {
         set_error("stream/event creation failed");
         return fail(TTS_ERR_HIP);
     }
@@ -692,9 +697,16 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         } else {
         TTS_HIP(hipEventRecord(d->ev_t1, s));
         TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
-        TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
-        // a polling wait: the sentence's next stages are enqueued right after it
-        TTS_HIP(spin_sync(s, d->ev_sync));
+        TTS_HIP(hipMemcpyAsync(d->host_flags + 4, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        // a polling wait on the event after the read-backs; work that needs no host-side step count
+        // (the synthesis postnet) is enqueued before it, so the device does not idle while the host wakes
+        TTS_HIP(hipEventRecord(d->ev_sync, s));
+        if (d->post_hook) {
+            d->post_hook(d->post_ctx, s);
+            d->hook_ran = true;
+        }
+        TTS_HIP(spin_wait(d->ev_sync));
+        n_steps[0] = d->host_flags[4];
         if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
             // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
             // stopped before touching any state; use the multi-launch path from now on
@@ -761,8 +773,9 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         if (st) return st;
     }
     TTS_HIP(hipEventRecord(d->ev_t1, s));
-    TTS_HIP(hipMemcpyAsync(n_steps, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipMemcpyAsync(d->host_flags + 4, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     TTS_HIP(spin_sync(s, d->ev_sync));
+    std::copy(d->host_flags + 4, d->host_flags + 4 + B, n_steps);
     }
     int nmax = 0;
     for (int b = 0; b < B; ++b) nmax = std::max(nmax, (int)n_steps[b]);
@@ -882,7 +895,14 @@ namespace tts {
 void decoder_set_pipeline(tts_decoder* d, bool on) {
     d->pipeline = on;
     d->keep_hist = on;
+    if (!on) d->post_hook = nullptr;
 }
+void decoder_set_post_hook(tts_decoder* d, void (*fn)(void*, hipStream_t), void* ctx) {
+    d->post_hook = fn;
+    d->post_ctx = ctx;
+    d->hook_ran = false;
+}
+bool decoder_hook_ran(tts_decoder* d) { return d->hook_ran && d->last_resident; }
 void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floats, const int** n_steps) {
     *mel = d->mel_hist;
     *sentence_floats = (int64_t)d->hist_cap * d->nmel;

@@ -90,12 +90,17 @@ hipError_t launch_persistent(const void* fn, dim3 grid, dim3 block, void** args,
 // `ev` on `s` and polls it instead (one host core busy for the wait), falling back to the blocking
 // wait after TTS_SPIN_MS milliseconds (default 200; 0 = always block).
 hipError_t spin_sync(hipStream_t s, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, s);
+    if (e != hipSuccess) return e;
+    return spin_wait(ev);
+}
+
+hipError_t spin_wait(hipEvent_t ev) {
     static const long long spin_ns = [] {
         const char* v = std::getenv("TTS_SPIN_MS");
         return (long long)((v && v[0]) ? std::atof(v) * 1e6 : 200e6);
     }();
-    hipError_t e = hipEventRecord(ev, s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
     if (spin_ns > 0) {
         const auto t0 = std::chrono::steady_clock::now();
         for (unsigned k = 0;; ++k) {

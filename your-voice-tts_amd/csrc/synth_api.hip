@@ -213,12 +213,38 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     float* const enc = tts::encoder_out_buffer(s->e);
     TTS_HIP(hipMemcpyAsync(ids_dev, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
     s->steps.assign(B, 0);
+    // batch 1: the postnet is enqueued behind the resident decoder launch before the host waits for
+    // it (device step counts, tiles sized for the step cap: the tiles past the sentence exit), so
+    // the device goes from the decoder to the postnet without waiting for the host to wake up
+    const float* hist = nullptr;
+    int64_t sent_floats = 0;
+    const int* n_dev = nullptr;
+    tts::decoder_histories(s->d, &hist, &sent_floats, &n_dev);
+    float* const post = s->post[par];
+    struct Hook {
+        tts_synth* s;
+        const float* hist;
+        int mel_tmax;
+        const int* n_dev;
+        float* post;
+        int T;
+        tts_status st;
+    } hook{s, hist, (int)(sent_floats / s->nmel), n_dev, post, (int)T, TTS_OK};
+    auto hook_fn = [](void* c, hipStream_t q) {
+        Hook* h = static_cast<Hook*>(c);
+        const int32_t Tcap[1] = {h->T};
+        h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
+    };
+    tts::decoder_set_post_hook(s->d, B == 1 ? +hook_fn : nullptr, &hook);
     for (int attempt = 0;; ++attempt) {
         if ((st = tts_encoder_run(s->e, ids_dev, h_lens, B, Lmax, enc, ss))) return st;
         // synchronises ss: the encoder's placement status is then readable
-        if ((st = tts_decoder_run(s->d, enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr,
-                                  s->steps.data(), ss)))
+        st = tts_decoder_run(s->d, enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr, s->steps.data(), ss);
+        if (!st) st = hook.st;
+        if (st) {
+            tts::decoder_set_post_hook(s->d, nullptr, nullptr);
             return st;
+        }
         int rerun = 0;
         if ((st = tts::encoder_pending_status(s->e, &rerun))) return st;
         if (!rerun) break;
@@ -232,14 +258,11 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_CHECK(Fmax >= 2, TTS_ERR_INVALID, "a sentence decoded to fewer than 2 frames");
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
     std::copy(h_frames, h_frames + B, frames);
-    float* const post = s->post[par];
-    {
+    const bool post_done = tts::decoder_hook_ran(s->d);
+    tts::decoder_set_post_hook(s->d, nullptr, nullptr);
+    if (!post_done) {
         // the postnet reads the decoder's mel history in place, with the step counts the decoder left
         // on the device (pipeline mode: no history copies, no frame-count upload)
-        const float* hist = nullptr;
-        int64_t sent_floats = 0;
-        const int* n_dev = nullptr;
-        tts::decoder_histories(s->d, &hist, &sent_floats, &n_dev);
         if ((st = tts::postnet_run_dev(s->p, hist, (int)(sent_floats / s->nmel), n_dev, s->r, h_frames, B, (int)T, post, ss)))
             return st;
     }
@@ -266,10 +289,6 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     // shorter sentences leave their waveform tail unwritten: zero it
     if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
     // at r = 1 the decoder's device step counts are the frame counts: no upload
-    const float* hist_unused = nullptr;
-    int64_t sf_unused = 0;
-    const int* n_dev = nullptr;
-    tts::decoder_histories(s->d, &hist_unused, &sf_unused, &n_dev);
     if ((st = tts::gl_run_dev(s->g, TTS_GL_FROM_MEL, spec, h_frames, s->r == 1 ? n_dev : nullptr, B, Fmax, nullptr, seed,
                               gl_iters, wav, gs)))
         return st;
