@@ -9,8 +9,15 @@ namespace tts {
 
 // ------------------------------------------------------------------ init (per call)
 __global__ void decoder_init_kernel(const InitArgs a) {
+    if ((int)blockIdx.x >= a.B) {  // the extra workgroups zero the resident hand-off granules
+        for (int i = (blockIdx.x - a.B) * blockDim.x + threadIdx.x; i < a.nzero; i += INIT_ZERO_BLOCKS * blockDim.x)
+            a.zero[i] = 0ull;
+        return;
+    }
     const int b = blockIdx.x;
     const int L = a.lens[b];
+    if (a.pre1_go && !a.keep)
+        for (int k = threadIdx.x; k < PRE; k += blockDim.x) a.pre1[(int64_t)b * PRE + k] = a.pre1_go[k];
     // step 0 reads the "previous" ping-pong slot (parity 1) for h_att / h_dec and xa[0] for ctx.
     float* ha = a.h_att + a.h_pstride + (int64_t)b * HATT;
     float* hd = a.h_dec + a.h_pstride + (int64_t)b * HDEC;
@@ -48,7 +55,7 @@ __global__ void decoder_init_kernel(const InitArgs a) {
 }
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B + (a.zero ? INIT_ZERO_BLOCKS : 0)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

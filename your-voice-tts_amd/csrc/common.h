@@ -46,15 +46,32 @@ void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floa
 // resident launch's (false after a multi-launch rerun: the caller enqueues that work again)
 void decoder_set_post_hook(tts_decoder* d, void (*fn)(void*, hipStream_t), void* ctx);
 bool decoder_hook_ran(tts_decoder* d);
+// the next batch-1 resident runs read the sentence length from this device array (the encoder's own,
+// encoder_lens_buffer) instead of uploading it, and one more status word is read back with the
+// decoder's own (src -> pinned dst; the pipeline's deferred encoder status); clamp_dst (or null)
+// receives the speculative Griffin-Lim frame counts (Readback below); cleared when pipeline mode ends
+void decoder_set_pipeline_io(tts_decoder* d, const int* lens_dev, const int* rb_src, int* rb_dst, int* clamp_dst,
+                             int clamp_max);
+// the encoder's device length array, and its batch-1 resident status word with the pinned word the
+// host reads it from; defer: a pipeline-mode batch-1 resident run leaves that read-back to the caller
+const int* encoder_lens_buffer(tts_encoder* e);
+void encoder_status_words(tts_encoder* e, const int** dev, int** host);
+void encoder_set_defer_status(tts_encoder* e, bool defer);
+// the next pipeline-mode run's lengths are already in encoder_lens_buffer (stage_ids): no upload
+void encoder_set_lens_staged(tts_encoder* e, bool staged);
 // postnet.hip: tts_postnet_run with device frame counts (T_dev[b] * tmul) and input rows mel_tmax
 // frames apart (0 = Tmax); T holds the same counts on the host
 tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
                            int B, int Tmax, float* out, hipStream_t s);
 void gl_set_pipeline(tts_gl* g, bool on);
-// griffin_lim.hip: tts_gl_run with the frame counts also on the device (F_dev, or null)
+// griffin_lim.hip: tts_gl_run with the frame counts also on the device (F_dev, or null); F_bound:
+// F holds upper bounds only, F_dev (on the same stream) the counts
 tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, const int* F_dev, int B, int Fmax,
-                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream);
+                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream,
+                      bool F_bound = false);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
+// whether gl_run_dev takes the persistent loop for this shape (host values only)
+bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters);
 
 // Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent
 // Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This checks
@@ -76,6 +93,33 @@ int usable_cus();
 // sits on the synthesis critical path)
 hipError_t spin_sync(hipStream_t s, hipEvent_t ev);
 hipError_t spin_wait(hipEvent_t ev);  // the same wait on an event already recorded
+// Small device -> pinned-host read-back in ONE launch (runtime.hip: readback_kernel) instead of one
+// copy launch per array: up to 4 int arrays (system-scope stores, visible to the host once an
+// event recorded after the launch has completed), plus an optional clamp of frame counts for a
+// Griffin-Lim enqueued before they are known: clamp_dst[b] = src[b] if 2 <= src[b] <= clamp_max,
+// else 0 (every launch of that run exits at once; the caller redoes the sentence).
+struct Readback {
+    const int* src[4];
+    int n[4];
+    int* dst[4];
+    int count;
+    const int* clamp_src;
+    int* clamp_dst;
+    int clamp_n, clamp_max;
+};
+hipError_t readback(const Readback& r, hipStream_t s);
+// A batch-1 sentence's ids (and its length) written to device arrays by one kernel whose argument
+// block carries them (runtime.hip), in place of two host-to-device copies: on this runtime a small
+// pageable-or-pinned H2D copy was measured to hold the host until its stream drained (~50 µs of
+// idle device at every pipelined sentence boundary).
+constexpr int STAGE_IDS_MAX = 512;
+struct StageIds {
+    int32_t* ids;
+    int* lens;
+    int n, len;  // ids to write, the length value
+    int32_t v[STAGE_IDS_MAX];
+};
+hipError_t stage_ids(const StageIds& a, hipStream_t s);
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 

@@ -74,7 +74,12 @@ struct InitArgs {
     float* mem;
     float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; int* nidx; float* tail;
     int* flag1; int* count; int* done; int* n_steps; int* step; int* n_active;
+    // batch-1 resident runs: the cached go-frame prenet row copied into pre1 (null: the prenet GEMM
+    // runs), and a granule array zeroed by INIT_ZERO_BLOCKS extra workgroups (null: none)
+    const float* pre1_go; float* pre1;
+    unsigned long long* zero; int nzero;
 };
+constexpr int INIT_ZERO_BLOCKS = 16;
 
 // Processed query + energy partials (one workgroup per (16 attention dims, sentence)):
 //   q[b][d] = W_q h_att[b]  (query_layer, common_layers.py:170/179)

@@ -73,6 +73,18 @@ struct tts_decoder {
     void (*post_hook)(void*, hipStream_t) = nullptr;
     void* post_ctx = nullptr;
     bool hook_ran = false;
+    // tts_synth_run (decoder_set_pipeline_io): device length array, one extra status word to read
+    // back, the speculative Griffin-Lim frame-count clamp target
+    const int* io_lens = nullptr;
+    const int* io_rb_src = nullptr;
+    int* io_rb_dst = nullptr;
+    int* io_clamp = nullptr;
+    int io_clamp_max = 0;
+    // relu(W_pre1 go): the step-0 prenet layer 1 of a fresh batch-1 resident run, copied by
+    // decoder_init instead of a GEMM launch per sentence (computed by the first such run)
+    float* pre1_go = nullptr;
+    bool pre1_go_ok = false;
+    const float* last_enc_direct = nullptr;  // the last direct run's encoder output (profiling re-runs)
     std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
     bool pipeline = false;  // tts_synth_run: work on the caller's stream
@@ -334,7 +346,8 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_out, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreate(&d->ev_t0) != hipSuccess || hipEventCreate(&d->ev_t1) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_t0, hipEventReleaseToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&d->ev_t1, hipEventReleaseToDevice) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), (4 + 64) * sizeof(int)) != hipSuccess) {
         set_error("stream/event creation failed");
@@ -490,6 +503,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     CK(dmalloc(d, &d->xa, (size_t)2 * Bc * XA));
     CK(dmalloc(d, &d->mem, (size_t)Bc * nmel));
     CK(dmalloc(d, &d->pre1, (size_t)Bc * PRE));
+    CK(dmalloc(d, &d->pre1_go, (size_t)PRE));
     CK(dmalloc(d, &d->q, (size_t)Bc * ADIM));
     if (Bc > 16) {
         d->ntf = (Bc + 15) / 16;
@@ -634,12 +648,20 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         TTS_HIP(hipEventRecord(d->ev_in, cs));
         TTS_HIP(hipStreamWaitEvent(s, d->ev_in, 0));
     }
-    TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4, B,
-                             hipMemcpyDeviceToDevice, s));
-    TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
-    TTS_HIP(launch_project_inputs(d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
+    // A fresh batch-1 resident run ("direct") reads the caller's encoder output in place, the length
+    // from the pipeline's device array when it has one, zeroes its hand-off granules and takes the
+    // cached go-frame prenet row inside decoder_init: two launches before the resident one instead
+    // of six.  A fallback to the multi-launch path stages the copies first (stage_fallback).
+    const bool direct = d->resident && B == 1 && lens[0] <= RES_LMAX && !keep;
+    if (!direct)
+        TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4,
+                                 B, hipMemcpyDeviceToDevice, s));
+    const int* lens_dev = direct && d->io_lens ? d->io_lens : d->lens;
+    if (lens_dev == d->lens) TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    TTS_HIP(launch_project_inputs(direct ? enc : d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
+    d->last_enc_direct = direct ? enc : nullptr;
     InitArgs ia{};
-    ia.B = B; ia.Lcap = d->Lcap; ia.nmel = d->nmel; ia.lens = d->lens;
+    ia.B = B; ia.Lcap = d->Lcap; ia.nmel = d->nmel; ia.lens = lens_dev;
     ia.att_init = d->att_init; ia.dec_init = d->dec_init; ia.go = d->go;
     ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
     ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
@@ -663,9 +685,35 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                                    hipMemcpyDeviceToDevice, s));
         ia.keep = 1;
     }
+    if (direct) {
+        ia.zero = d->gran;
+        ia.nzero = 2 * GR_TOTAL + 2;
+        ia.pre1 = d->pre1;
+        ia.pre1_go = d->pre1_go_ok ? d->pre1_go : nullptr;
+    }
     TTS_HIP(launch_decoder_init(ia, s));
     if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
-    if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
+    if (!keep && !ia.pre1_go) {
+        tts_status st = enqueue_prenet_go(d, B, s);
+        if (st) return st;
+        if (direct) {
+            TTS_HIP(hipMemcpyAsync(d->pre1_go, d->pre1, PRE * sizeof(float), hipMemcpyDeviceToDevice, s));
+            d->pre1_go_ok = true;
+        }
+    }
+    // a direct run falling back to the multi-launch path: the staged inputs the step graphs read
+    auto stage_fallback = [&]() -> tts_status {
+        if (!direct) return TTS_OK;
+        TTS_HIP(hipMemcpy2DAsync(d->enc, (size_t)d->Lcap * ENC * 4, enc, (size_t)Lmax * ENC * 4, (size_t)Lmax * ENC * 4,
+                                 B, hipMemcpyDeviceToDevice, s));
+        if (ia.lens != d->lens) TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+        ia.lens = d->lens;
+        ia.zero = nullptr;
+        ia.nzero = 0;
+        ia.pre1_go = nullptr;
+        d->last_enc_direct = nullptr;
+        return TTS_OK;
+    };
     int run = 0;  // steps enqueued; the next step has parity run & 1
     d->last_resident = 0;
     bool res_done = false;
@@ -675,7 +723,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.w = d->rw;
         ra.L = lens[0]; ra.Lcap = d->Lcap; ra.nmel = d->nmel; ra.nrows = d->nmel + PRE + 1;
         ra.max_steps = max_steps; ra.hist_cap = d->hist_cap; ra.Lalign = Lmax; ra.timeout_ticks = d->res_ticks;
-        ra.v = d->v; ra.v_b = d->v_b; ra.Pt = d->Pt; ra.enc = d->enc;
+        ra.v = d->v; ra.v_b = d->v_b; ra.Pt = d->Pt; ra.enc = direct ? enc : d->enc;
         ra.h_att = d->h_att; ra.c_att = d->c_att; ra.h_dec = d->h_dec; ra.c_dec = d->c_dec; ra.xa = d->xa;
         ra.hps = (int64_t)d->Bcap * HATT; ra.xps = (int64_t)d->Bcap * XA;
         ra.pre1 = d->pre1; ra.alpha = d->alpha; ra.nidx = d->nidx; ra.u = d->u; ra.flag1 = d->flag1; ra.count = d->count;
@@ -686,7 +734,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         d->res_salt = (d->res_salt + 1) & 0x3FFFF;
         ra.salt = d->res_salt;
         d->last_ra = ra;
-        TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
+        if (!direct) TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
         TTS_HIP(hipEventRecord(d->ev_t0, s));
         bool launched = false;
         TTS_HIP(launch_resident(ra, s, &launched));
@@ -694,10 +742,23 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             // the grid cannot be co-resident on this device (launch_persistent): nothing ran and the
             // initial state is untouched; the multi-launch path takes over for the life of the handle
             d->resident = false;
+            if (tts_status st = stage_fallback()) return st;
+            TTS_HIP(launch_decoder_init(ia, s));
+            if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
         } else {
         TTS_HIP(hipEventRecord(d->ev_t1, s));
-        TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
-        TTS_HIP(hipMemcpyAsync(d->host_flags + 4, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+        {
+            // status, step counts (and the pipeline's extra word / GL clamp) in one launch
+            Readback rb{};
+            rb.src[0] = ra.status; rb.n[0] = 1; rb.dst[0] = d->host_flags;
+            rb.src[1] = d->n_steps; rb.n[1] = B; rb.dst[1] = d->host_flags + 4;
+            rb.count = 2;
+            if (d->io_rb_src) { rb.src[2] = d->io_rb_src; rb.n[2] = 1; rb.dst[2] = d->io_rb_dst; rb.count = 3; }
+            if (d->io_clamp) {
+                rb.clamp_src = d->n_steps; rb.clamp_dst = d->io_clamp; rb.clamp_n = B; rb.clamp_max = d->io_clamp_max;
+            }
+            TTS_HIP(readback(rb, s));
+        }
         // a polling wait on the event after the read-backs; work that needs no host-side step count
         // (the synthesis postnet) is enqueued before it, so the device does not idle while the host wakes
         TTS_HIP(hipEventRecord(d->ev_sync, s));
@@ -711,6 +772,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
             // stopped before touching any state; use the multi-launch path from now on
             d->resident = false;
+            if (tts_status st = stage_fallback()) return st;
             TTS_HIP(launch_decoder_init(ia, s));
             if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
         } else if (d->host_flags[0] != 0 && d->host_flags[0] != 100 && !keep) {
@@ -720,6 +782,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             // path (same results within the resident tests' tolerance); the handle stays resident.
             // (inference_truncated's carried state may already be overwritten: that case raises.)
             ++d->res_timeouts;
+            if (tts_status st = stage_fallback()) return st;
             TTS_HIP(launch_decoder_init(ia, s));
             if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
             tts_status st = enqueue_prenet_go(d, B, s);
@@ -774,6 +837,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     }
     TTS_HIP(hipEventRecord(d->ev_t1, s));
     TTS_HIP(hipMemcpyAsync(d->host_flags + 4, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
+    if (d->io_rb_src) TTS_HIP(hipMemcpyAsync(d->io_rb_dst, d->io_rb_src, sizeof(int), hipMemcpyDeviceToHost, s));
     TTS_HIP(spin_sync(s, d->ev_sync));
     std::copy(d->host_flags + 4, d->host_flags + 4 + B, n_steps);
     }
@@ -870,6 +934,9 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
     for (int i = 0; i <= K; ++i) TTS_HIP(hipEventCreate(&ev[i]));
     TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
     hipStream_t s = d->stream;
+    if (d->last_enc_direct)  // the last run read its encoder output in place: stage it for the step graphs
+        TTS_HIP(hipMemcpyAsync(d->enc, d->last_enc_direct, (size_t)d->last_Lmax * ENC * sizeof(float),
+                               hipMemcpyDeviceToDevice, s));
     TTS_HIP(launch_decoder_init(d->last_init, s));
     tts_status st = enqueue_prenet_go(d, d->last_B, s);
     std::vector<double> acc(K, 0.0);
@@ -895,7 +962,18 @@ namespace tts {
 void decoder_set_pipeline(tts_decoder* d, bool on) {
     d->pipeline = on;
     d->keep_hist = on;
-    if (!on) d->post_hook = nullptr;
+    if (!on) {
+        d->post_hook = nullptr;
+        decoder_set_pipeline_io(d, nullptr, nullptr, nullptr, nullptr, 0);
+    }
+}
+void decoder_set_pipeline_io(tts_decoder* d, const int* lens_dev, const int* rb_src, int* rb_dst, int* clamp_dst,
+                             int clamp_max) {
+    d->io_lens = lens_dev;
+    d->io_rb_src = rb_src;
+    d->io_rb_dst = rb_dst;
+    d->io_clamp = clamp_dst;
+    d->io_clamp_max = clamp_max;
 }
 void decoder_set_post_hook(tts_decoder* d, void (*fn)(void*, hipStream_t), void* ctx) {
     d->post_hook = fn;

@@ -53,6 +53,8 @@ struct tts_encoder {
     int* host_status = nullptr;  // pinned
     bool pipeline = false;        // tts_synth_run: caller's stream, placement status left pending
     bool status_pending = false;
+    bool defer_status = false;  // pipeline, batch-1 resident: the caller reads the status word back
+    bool lens_staged = false;   // pipeline: the caller wrote T on the stream already (stage_ids)
     bool skip_resident_once = false;  // a pipelined resident run timed out: its rerun goes per-step
     int res_timeouts = 0;             // resident runs that timed out a hand-off and re-ran per-step
     std::map<int, hipGraphExec_t> rgraphs;  // by Lmax (B = 1)
@@ -324,7 +326,7 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
     }
     // (tts_synth_run uploads the ids straight into this handle's buffer: encoder_ids_buffer)
     if (ids != e->ids) TTS_HIP(hipMemcpyAsync(e->ids, ids, sizeof(int) * (size_t)B * Lmax, hipMemcpyDeviceToDevice, s));
-    TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
+    if (!(e->pipeline && e->lens_staged)) TTS_HIP(hipMemcpyAsync(e->T, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
     // initial state (h_0, c_0) of both directions: step 0 reads the parity-1 h slots
     const size_t hs = (size_t)e->Bcap * EH;  // per-direction stride
     const size_t row = (size_t)B * EH * sizeof(float);
@@ -380,8 +382,9 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
             e->last_resident = 1;
             e->rsalt_pending = e->rsalt;
             e->pending_batch = false;
-            TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
-                                   hipMemcpyDeviceToHost, s));
+            if (!(e->pipeline && e->defer_status))
+                TTS_HIP(hipMemcpyAsync(e->host_status, e->rgran + encoder_resident_granules() - 2, sizeof(int),
+                                       hipMemcpyDeviceToHost, s));
             if (e->pipeline) {  // the pipeline reads the status at its next synchronisation point
                 e->status_pending = true;
                 goto done;
@@ -500,11 +503,21 @@ done:
 }  // extern "C"
 
 namespace tts {
-void encoder_set_pipeline(tts_encoder* e, bool on) { e->pipeline = on; }
+void encoder_set_pipeline(tts_encoder* e, bool on) {
+    e->pipeline = on;
+    if (!on) e->defer_status = e->lens_staged = false;
+}
+void encoder_set_lens_staged(tts_encoder* e, bool staged) { e->lens_staged = staged; }
 int32_t* encoder_ids_buffer(tts_encoder* e, int B, int Lmax) {
     return (size_t)B * Lmax <= (size_t)e->Bcap * e->Lcap ? e->ids : nullptr;
 }
 float* encoder_out_buffer(tts_encoder* e) { return e->out; }
+const int* encoder_lens_buffer(tts_encoder* e) { return e->T; }
+void encoder_status_words(tts_encoder* e, const int** dev, int** host) {
+    *dev = e->rgran ? reinterpret_cast<const int*>(e->rgran + encoder_resident_granules() - 2) : nullptr;
+    *host = e->host_status;
+}
+void encoder_set_defer_status(tts_encoder* e, bool defer) { e->defer_status = defer; }
 
 tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
     *placement_failed = 0;

@@ -987,9 +987,11 @@ typedef __attribute__((address_space(1))) int gi32_t;
 __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArgs p) {
     const IterArgs& a = p.it;
     const int b = blockIdx.y;
-    const int f = xcd_remap(blockIdx.x, gridDim.x);
     const int Fb = a.F[b];
-    if (f >= Fb) return;
+    // frames -> XCDs in contiguous runs over the sentence's own frame count rather than the grid's
+    // (a speculative batch-1 run sizes the grid as an upper bound): the placement of a grid of Fb
+    if ((int)blockIdx.x >= Fb) return;
+    const int f = xcd_remap(blockIdx.x, Fb);
     const Geo g = a.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ __align__(16) double2 buf0[NH];
@@ -1506,8 +1508,8 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if ((e = hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_out, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
-    if ((e = hipEventCreate(&g->ev_t0)) != hipSuccess) return fail(e, "event");
-    if ((e = hipEventCreate(&g->ev_t1)) != hipSuccess) return fail(e, "event");
+    if ((e = hipEventCreateWithFlags(&g->ev_t0, hipEventReleaseToDevice)) != hipSuccess) return fail(e, "event");
+    if ((e = hipEventCreateWithFlags(&g->ev_t1, hipEventReleaseToDevice)) != hipSuccess) return fail(e, "event");
     if ((e = hipMalloc(&g->win, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&g->win2, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
     if ((e = hipMalloc(&g->tw, NFFT * sizeof(double2))) != hipSuccess) return fail(e, "hipMalloc");
@@ -1571,6 +1573,8 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     {
         int dev = 0, ncu = 0, rate_khz = 0;
         if ((e = hipMalloc(&g->pstatus, 16)) != hipSuccess) return fail(e, "hipMalloc");
+        // (an empty speculative run leaves the word as it is: it must start out clean)
+        if ((e = hipMemset(g->pstatus, 0, 16)) != hipSuccess) return fail(e, "hipMemset");
         if ((e = hipHostMalloc(reinterpret_cast<void**>(&g->host_status), sizeof(int))) != hipSuccess)
             return fail(e, "hipHostMalloc");
         if (hipGetDevice(&dev) == hipSuccess &&
@@ -1589,6 +1593,16 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
 
 namespace tts {
 void gl_set_pipeline(tts_gl* g, bool on) { g->pipeline = on; }
+
+// small batches fuse the overlap-add into the iteration launch; at most 256 frames in all run the
+// whole loop as one persistent launch (host values only)
+static bool gl_fused_path(const tts_gl* g, int B, int Fmax) {
+    const char* fz = getenv("TTS_GL_FUSED");
+    return ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (g->g.win + g->g.hop - 1) / g->g.hop <= OLA_MAX;
+}
+bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters) {
+    return gl_fused_path(g, B, Fmax) && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+}
 
 tts_status gl_collect(tts_gl* g) {
     if (!g->pending) return TTS_OK;
@@ -1613,10 +1627,13 @@ namespace tts {
 // tts_gl_run, optionally with the frame counts also on the device (F_dev, the same values as F:
 // tts_synth_run passes the decoder's step counts at r = 1): the persistent loop's launches then
 // read them there and the upload is skipped (the graph-replayed fallbacks still upload into the
-// handle's own array, which their graphs bake in).
+// handle's own array, which their graphs bake in).  F_bound: F holds only upper bounds of the
+// device counts (a run enqueued before the decoder's step counts reach the host, same stream):
+// the fallbacks then copy F_dev into the handle's array on the device.
 tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, const int* F_dev, int B, int Fmax,
-                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream) {
+                      const double* phase_u, uint64_t seed, int iters, double* wav, hipStream_t stream, bool F_bound) {
     TTS_CHECK(g && spec && F && wav && B >= 1 && Fmax >= 2 && iters >= 0, TTS_ERR_INVALID, "bad gl_run arguments");
+    TTS_CHECK(!F_bound || F_dev, TTS_ERR_INVALID, "F_bound needs device frame counts");
     TTS_CHECK(mode == TTS_GL_FROM_MEL || mode == TTS_GL_FROM_LINEAR, TTS_ERR_INVALID, "bad mode");
     TTS_CHECK(mode == TTS_GL_FROM_LINEAR || g->pinv, TTS_ERR_INVALID, "mel mode needs inv_mel_basis at create");
     for (int b = 0; b < B; ++b) TTS_CHECK(F[b] >= 2 && F[b] <= Fmax, TTS_ERR_INVALID, "F[b] out of range [2, Fmax]");
@@ -1665,13 +1682,18 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     // path choice (host values only): small batches fuse the overlap-add into the iteration launch;
     // at most 256 frames in all run the whole loop as one persistent launch
     const char* fz = getenv("TTS_GL_FUSED");
-    const bool fused = ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (geo.win + geo.hop - 1) / geo.hop <= OLA_MAX;
+    const bool fused = gl_fused_path(g, B, Fmax);
     int frames_total = 0;
     for (int b = 0; b < B; ++b) frames_total += F[b];
-    const bool persistent = fused && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
-    // the launches read the frame counts from F_dev when the persistent loop takes them all
+    const bool persistent = gl_persistent_path(g, B, Fmax, frames_total, iters);
+    // the launches read the frame counts from F_dev when the persistent loop takes them all; the
+    // graph-replayed loops read the handle's own array, filled from F_dev when there is one (a
+    // speculative run's host F is only an upper bound: tts_synth_run)
     const int* Fd = persistent && F_dev ? F_dev : g->F;  // (reassigned if the persistent launch falls back)
-    if (Fd == g->F) TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+    if (Fd == g->F) {
+        if (F_bound) TTS_HIP(hipMemcpyAsync(g->F, F_dev, B * sizeof(int), hipMemcpyDeviceToDevice, s));
+        else TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+    }
     MagArgs ma{};
     ma.mode = mode;
     ma.spec = spec;
@@ -1810,7 +1832,8 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     if (!persistent_ran && Fd != g->F) {
         // the persistent loop could not be placed: its fallbacks replay graphs that bake the
         // handle's own frame-count array in
-        TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+        if (F_bound) TTS_HIP(hipMemcpyAsync(g->F, F_dev, B * sizeof(int), hipMemcpyDeviceToDevice, s));
+        else TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
         Fd = g->F;
         ia.F = fa.F = Fd;
     }

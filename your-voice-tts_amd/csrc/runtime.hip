@@ -114,6 +114,34 @@ hipError_t spin_wait(hipEvent_t ev) {
     return hipEventSynchronize(ev);
 }
 
+__global__ void readback_kernel(const Readback r) {
+    for (int i = 0; i < r.count; ++i)
+        for (int j = threadIdx.x; j < r.n[i]; j += blockDim.x)
+            __hip_atomic_store(r.dst[i] + j, r.src[i][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (r.clamp_dst)
+        for (int j = threadIdx.x; j < r.clamp_n; j += blockDim.x) {
+            const int v = r.clamp_src[j];
+            r.clamp_dst[j] = v >= 2 && v <= r.clamp_max ? v : 0;
+        }
+}
+
+hipError_t readback(const Readback& r, hipStream_t s) {
+    if (r.count < 0 || r.count > 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(readback_kernel, dim3(1), dim3(64), 0, s, r);
+    return hipGetLastError();
+}
+
+__global__ void stage_ids_kernel(const StageIds a) {
+    for (int i = threadIdx.x; i < a.n; i += blockDim.x) a.ids[i] = a.v[i];
+    if (threadIdx.x == 0) a.lens[0] = a.len;
+}
+
+hipError_t stage_ids(const StageIds& a, hipStream_t s) {
+    if (a.n < 1 || a.n > STAGE_IDS_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(stage_ids_kernel, dim3(1), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 __global__ void frag_mirror_kernel(const float* src, int64_t ld, int B, int K, float* dst, int ntf) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B * K) return;

@@ -43,6 +43,7 @@ struct tts_synth {
     int32_t* pin[2] = {nullptr, nullptr};
     size_t pin_n[2] = {0, 0};
     unsigned calls = 0;
+    int* fspec = nullptr;  // [dev] frame count of a speculative batch-1 Griffin-Lim (synth_stages)
 };
 
 namespace {
@@ -94,7 +95,8 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
         hipStreamCreateWithPriority(&s->gl_stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_post, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&s->fspec, 4 * sizeof(int)) != hipSuccess) {
         tts_synth_destroy(s);
         tts::set_error("tts_synth_create: stream / event creation failed");
         return TTS_ERR_HIP;
@@ -110,7 +112,7 @@ void tts_synth_destroy(tts_synth* s) {
     if (tts::gl_collect(s->g) != TTS_OK)  // the last pipelined run's status was never collected
         std::fprintf(stderr, "tts_synth_destroy: the last run failed: %s\n", tts_last_error());
     for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post[0],
-                    (void*)s->post[1], (void*)s->spec[0], (void*)s->spec[1]})
+                    (void*)s->post[1], (void*)s->spec[0], (void*)s->spec[1], (void*)s->fspec})
         if (q) (void)hipFree(q);
     for (int32_t* q : s->pin)
         if (q) (void)hipHostFree(q);
@@ -211,7 +213,20 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     int32_t* ids_dev = tts::encoder_ids_buffer(s->e, B, Lmax);
     if (!ids_dev) ids_dev = s->ids;
     float* const enc = tts::encoder_out_buffer(s->e);
-    TTS_HIP(hipMemcpyAsync(ids_dev, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
+    if (B == 1 && Lmax <= tts::STAGE_IDS_MAX && ids_dev != s->ids) {
+        // batch 1: ids and length through one kernel's arguments (common.h: stage_ids)
+        tts::StageIds sa;
+        sa.ids = ids_dev;
+        sa.lens = const_cast<int*>(tts::encoder_lens_buffer(s->e));
+        sa.n = Lmax;
+        sa.len = h_lens[0];
+        std::copy(h_ids, h_ids + Lmax, sa.v);
+        TTS_HIP(tts::stage_ids(sa, ss));
+        tts::encoder_set_lens_staged(s->e, true);
+    } else {
+        TTS_HIP(hipMemcpyAsync(ids_dev, h_ids, sizeof(int32_t) * (size_t)B * Lmax, hipMemcpyHostToDevice, ss));
+        tts::encoder_set_lens_staged(s->e, false);
+    }
     s->steps.assign(B, 0);
     // batch 1: the postnet is enqueued behind the resident decoder launch before the host waits for
     // it (device step counts, tiles sized for the step cap: the tiles past the sentence exit), so
@@ -221,6 +236,12 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     const int* n_dev = nullptr;
     tts::decoder_histories(s->d, &hist, &sent_floats, &n_dev);
     float* const post = s->post[par];
+    // ... and, when its frame count can only take the persistent Griffin-Lim (<= 256 frames, r = 1),
+    // Griffin-Lim too: sized for Ts = min(256, T) frames, reading the count the decoder's read-back
+    // launch clamps into fspec (a longer sentence makes it an empty run, redone below)
+    const int Ts = (int)std::min<size_t>(256, T);
+    const bool spec_gl = B == 1 && s->r == 1 && wav_cap >= (int64_t)s->hop * (Ts - 1) &&
+                         tts::gl_persistent_path(s->g, 1, Ts, Ts, gl_iters);
     struct Hook {
         tts_synth* s;
         const float* hist;
@@ -229,12 +250,39 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         float* post;
         int T;
         tts_status st;
-    } hook{s, hist, (int)(sent_floats / s->nmel), n_dev, post, (int)T, TTS_OK};
+        bool spec_gl;
+        int Ts;
+        uint64_t seed;
+        int iters;
+        double* wav;
+        hipStream_t cs;
+        bool gl_done;
+    } hook{s, hist, (int)(sent_floats / s->nmel), n_dev, post, (int)T, TTS_OK, spec_gl, Ts, seed, gl_iters, wav, cs, false};
     auto hook_fn = [](void* c, hipStream_t q) {
         Hook* h = static_cast<Hook*>(c);
         const int32_t Tcap[1] = {h->T};
         h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
+        if (h->st || !h->spec_gl) return;
+        // Griffin-Lim writes the caller's waveform: after the caller's stream
+        if (hipEventRecord(h->s->ev_in, h->cs) != hipSuccess || hipStreamWaitEvent(q, h->s->ev_in, 0) != hipSuccess) {
+            h->st = TTS_ERR_HIP;
+            tts::set_error("tts_synth_run: event hand-off failed");
+            return;
+        }
+        const int32_t Fb[1] = {h->Ts};
+        h->st = tts::gl_run_dev(h->s->g, TTS_GL_FROM_MEL, h->post, Fb, h->s->fspec, 1, h->Ts, nullptr, h->seed, h->iters,
+                                h->wav, q, true);
+        h->gl_done = h->st == TTS_OK;
     };
+    // batch 1: the sentence length from the encoder's device copy, the encoder's status word read back
+    // with the decoder's (one launch), the speculative Griffin-Lim's frame count clamped by it
+    if (B == 1) {
+        const int* est = nullptr;
+        int* ehost = nullptr;
+        tts::encoder_status_words(s->e, &est, &ehost);
+        tts::encoder_set_defer_status(s->e, est != nullptr);
+        tts::decoder_set_pipeline_io(s->d, tts::encoder_lens_buffer(s->e), est, ehost, spec_gl ? s->fspec : nullptr, Ts);
+    }
     tts::decoder_set_post_hook(s->d, B == 1 ? +hook_fn : nullptr, &hook);
     for (int attempt = 0;; ++attempt) {
         if ((st = tts_encoder_run(s->e, ids_dev, h_lens, B, Lmax, enc, ss))) return st;
@@ -259,6 +307,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
     std::copy(h_frames, h_frames + B, frames);
     const bool post_done = tts::decoder_hook_ran(s->d);
+    const bool gl_done = post_done && hook.gl_done && Fmax <= Ts;
     tts::decoder_set_post_hook(s->d, nullptr, nullptr);
     if (!post_done) {
         // the postnet reads the decoder's mel history in place, with the step counts the decoder left
@@ -280,6 +329,11 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     for (int b = 0; b < B; ++b) frames_total += h_frames[b];
     const bool same = frames_total <= 256;
     hipStream_t gs = same ? ss : s->gl_stream;
+    if (gl_done) {  // enqueued behind the decoder already (hook_fn)
+        TTS_HIP(hipEventRecord(s->ev_out, ss));
+        TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+        return TTS_OK;
+    }
     TTS_HIP(hipEventRecord(s->ev_in, cs));
     if (!same) {
         TTS_HIP(hipEventRecord(s->ev_post, ss));

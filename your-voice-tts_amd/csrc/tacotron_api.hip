@@ -945,7 +945,8 @@ tts_status tts_tacotron_create(const tts_tacotron_config* cfg, const tts_tensor*
     if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_out, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreate(&t->ev_t0) != hipSuccess || hipEventCreate(&t->ev_t1) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_t0, hipEventReleaseToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_t1, hipEventReleaseToDevice) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&t->host_flags), 4 * sizeof(int)) != hipSuccess) {
         set_error("stream/event creation failed");
         return fail(TTS_ERR_HIP);
