@@ -118,6 +118,26 @@ def test_synthesize_native_timeout_surfaces(audio_cfg):
         assert torch.isfinite(wav).all()
 
 
+def test_long_sentence_after_griffin_lim_timeout(audio_cfg):
+    """after a persistent Griffin-Lim timeout, a batch-1 sentence above 256 frames (its
+    speculative Griffin-Lim in the decoder hook becomes an empty run, then the host redoes it) must
+    not report the earlier run's failure: the empty run clears the status word too.  Its waveform
+    equals the same sentence on a fresh handle."""
+    audio = load_pkg("audio")
+    z = golden("t2_fwdmask_L12")
+    ids_long = load_pkg("weights").synthetic_ids(130, 7)  # 2L + 22 = 282 frames under the mask
+    m = _t2()
+    with _env(TTS_GL_WAIT_TICKS=20000):
+        ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
+        with _env(TTS_GL_INJECT_DROP=2):
+            with pytest.raises(RuntimeError, match="timed out"):
+                m.synthesize_native([z["ids"]], ap, seed=1, sync=True)
+        wav, frames = m.synthesize_native([ids_long], ap, seed=1, sync=True)
+        assert frames[0] > 256 and torch.isfinite(wav).all()
+        ref, _ = _t2().synthesize_native([ids_long], ap, seed=1, sync=True)
+    assert torch.equal(wav, ref)
+
+
 def test_resident_decoder_timeout_reruns_multilaunch():
     """Fault injection: every hand-off wait of the resident decoder times out at once
     (TTS_DEC_WAIT_TICKS=1), as when a workgroup cannot become resident beside another stream's work.

@@ -297,6 +297,22 @@ def test_synthesize_native_matches_staged(audio_cfg, cases):
     assert torch.equal(wav, ref)
 
 
+def test_synthesize_native_server_cap(audio_cfg):
+    """at the server's max_decoder_steps=3000 (Synthesizer, server/synthesizer.py) the
+    batch-1 postnet enqueued behind the decoder is sized by the small-kernel bound, not by the
+    3021-frame cap; waveforms (222 frames: persistent Griffin-Lim in the hook; 322 frames:
+    redone after the wait) are bitwise inference_batch + griffin_lim_batch."""
+    fl = dict(golden_flags(golden("t2_fwdmask_L100")), max_decoder_steps=3000)
+    m = _model(fl)
+    ap = load_pkg("audio").AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
+    for k, ids in enumerate((golden("t2_fwdmask_L100")["ids"], weights_mod().synthetic_ids(150, 7))):
+        wav, frames = m.synthesize_native([ids], ap, seed=30 + k)
+        out = m.inference_batch([ids])
+        ref = ap.griffin_lim_batch(out["mel_post"], out["frames"], seed=30 + k)
+        assert frames == out["frames"]
+        assert torch.equal(wav, ref), k
+
+
 def test_synthesize_native_back_to_back(audio_cfg):
     """tts_synth_run returns once Griffin-Lim is enqueued (the next call's host work and encoder
     overlap it; its stages run on the synth handle's stream): back-to-back calls with alternating

@@ -24,7 +24,7 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 EXPORTS = (
     "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state", "tts_encoder_last_path",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue", "tts_decoder_run_teacher",
-    "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases",
+    "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases", "tts_decoder_resident_trace",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_last_path", "tts_gl_profile",
@@ -90,6 +90,7 @@ def _declare(lib):
     lib.tts_gl_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     lib.tts_synth_sync.argtypes = [vp]
     lib.tts_decoder_resident_phases.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    lib.tts_decoder_resident_trace.argtypes = [vp, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int64]
     lib.tts_postnet_create.argtypes = [ctypes.POINTER(TensorView), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
     lib.tts_postnet_destroy.argtypes = [vp]
     lib.tts_postnet_destroy.restype = None

@@ -85,6 +85,8 @@ struct tts_decoder {
     float* pre1_go = nullptr;
     bool pre1_go_ok = false;
     const float* last_enc_direct = nullptr;  // the last direct run's encoder output (profiling re-runs)
+    int last_len_direct = 0;                 // ... and its length (the device copy it read may be reused)
+    std::vector<long long> res_trace;        // the last tts_decoder_resident_phases run's event trace
     std::map<std::tuple<int, int, int>, Graphs> graphs;
     float last_ms = 0.f;
     bool pipeline = false;  // tts_synth_run: work on the caller's stream
@@ -413,11 +415,11 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     // packed GEMM weights
     const int nfused = nmel + PRE + 1;
     {
-        // the resident decoder needs one workgroup per CU on >= 256 CUs and fits the fused rows in
-        // two rows per CU; TTS_RESIDENT=0 disables it (multi-launch path for every batch)
+        // the resident decoder needs one workgroup per CU on >= 256 CUs and one mel row per CU;
+        // TTS_RESIDENT=0 disables it (multi-launch path for every batch)
         const char* env = getenv("TTS_RESIDENT");
         int dev = 0, ncu = 0, rate_khz = 0;
-        if (d->fast_attention && nfused < 2 * RES_CUS && !(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
+        if (d->fast_attention && nmel <= RES_CUS && !(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= RES_CUS &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0 &&
             resident_prepare() == hipSuccess) {
@@ -452,19 +454,19 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         if (e == hipSuccess) e = dmalloc(d, &d->b_melf, (nfused + 15) / 16 * 16) ? hipErrorOutOfMemory : hipSuccess;
         if (e == hipSuccess) e = sgemm_pack_bias(bf, nullptr, nfused, ROWMAP_IDENTITY, 0, d->b_melf, s);
         if (e == hipSuccess && d->resident) {
-            size_t nwa, nwdl, nwdc, nws;
-            resident_weight_floats(&nwa, &nwdl, &nwdc, &nws);
-            float *pa = nullptr, *pdl = nullptr, *pdc = nullptr, *pws = nullptr;
-            if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) || dmalloc(d, &pws, nws) ||
+            size_t nwa, nwdl, nwdc;
+            resident_weight_floats(&nwa, &nwdl, &nwdc);
+            float *pa = nullptr, *pdl = nullptr, *pdc = nullptr;
+            if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) ||
+                dmalloc(d, &d->rw.wf, (size_t)nfused * (HDEC + ENC)) || dmalloc(d, &d->rw.bf, nfused) ||
                 dmalloc(d, &d->rw.ba, RES_CUS * 16) || dmalloc(d, &d->rw.bd, RES_CUS * 16) ||
-                dmalloc(d, &d->rw.bs, RES_CUS * 2) || dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) || dmalloc(d, &d->rw.wq, (size_t)ADIM * HATT) ||
+                dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) || dmalloc(d, &d->rw.wq, (size_t)ADIM * HATT) ||
                 dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
                 e = hipErrorOutOfMemory;
             if (e == hipSuccess) {
                 d->rw.wa = reinterpret_cast<float4*>(pa);
                 d->rw.wdl = reinterpret_cast<float4*>(pdl);
                 d->rw.wdc = reinterpret_cast<float4*>(pdc);
-                d->rw.ws = reinterpret_cast<float4*>(pws);
                 ResSrc src{a_wih, a_whh, a_bih, a_bhh, d_wih, d_whh, d_bih, d_bhh, pre1, wq, wf, bf, nfused};
                 e = resident_pack(src, d->rw, s);
             }
@@ -660,6 +662,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     if (lens_dev == d->lens) TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
     TTS_HIP(launch_project_inputs(direct ? enc : d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
     d->last_enc_direct = direct ? enc : nullptr;
+    d->last_len_direct = lens[0];
     InitArgs ia{};
     ia.B = B; ia.Lcap = d->Lcap; ia.nmel = d->nmel; ia.lens = lens_dev;
     ia.att_init = d->att_init; ia.dec_init = d->dec_init; ia.go = d->go;
@@ -872,6 +875,45 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
 }
 }  // namespace
 
+namespace {
+// Measurement only: re-run the last batch-1 resident sentence with timers (marks: per-phase tick
+// sums of CU 0 and the logging attention CU; always: the per-CU event trace, kept in d->res_trace).
+tts_status res_rerun(tts_decoder* d, bool marks, long long* h) {
+    TTS_CHECK(d->last_resident && d->last_steps > 0, TTS_ERR_INVALID,
+              "the resident decoder profile needs a previous resident tts_decoder_run");
+    TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
+    hipStream_t s = d->stream;
+    long long* prof = nullptr;
+    TTS_HIP(hipMalloc(&prof, sizeof(long long) * RES_PROF_LL));
+    TTS_HIP(hipMemsetAsync(prof, 0, sizeof(long long) * RES_PROF_LL, s));
+    TTS_HIP(launch_decoder_init(d->last_init, s));
+    tts_status st = enqueue_prenet_go(d, 1, s);
+    ResArgs ra = d->last_ra;
+    ra.prof = prof;
+    ra.prof_marks = marks ? 1 : 0;
+    if (!st) {
+        TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
+        bool launched = false;
+        TTS_HIP(launch_resident(ra, s, &launched));
+        if (!launched) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(prof);
+            TTS_CHECK(false, TTS_ERR_UNSUPPORTED, "resident decoder cannot be co-resident on this device now");
+        }
+    }
+    TTS_HIP(hipMemcpyAsync(h, prof, sizeof(long long) * 2 * RES_PHASES, hipMemcpyDeviceToHost, s));
+    d->res_trace.resize(RES_PROF_LL - 2 * RES_PHASES);
+    TTS_HIP(hipMemcpyAsync(d->res_trace.data(), prof + 2 * RES_PHASES, sizeof(long long) * d->res_trace.size(),
+                           hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
+    TTS_HIP(hipStreamSynchronize(s));
+    (void)hipFree(prof);
+    if (st) return st;
+    TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP, "resident decoder: a hand-off wait timed out (internal error)");
+    return TTS_OK;
+}
+}  // namespace
+
 extern "C" {
 
 tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_run) {
@@ -889,38 +931,20 @@ tts_status tts_decoder_last_path(tts_decoder* d, int* resident) {
 
 tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n) {
     TTS_CHECK(d && us && n >= 2 * RES_PHASES, TTS_ERR_INVALID, "bad arguments");
-    TTS_CHECK(d->last_resident && d->last_steps > 0, TTS_ERR_INVALID,
-              "tts_decoder_resident_phases needs a previous resident tts_decoder_run");
-    TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
-    hipStream_t s = d->stream;
-    long long* prof = nullptr;
-    TTS_HIP(hipMalloc(&prof, sizeof(long long) * 2 * RES_PHASES));
-    TTS_HIP(hipMemsetAsync(prof, 0, sizeof(long long) * 2 * RES_PHASES, s));
-    TTS_HIP(launch_decoder_init(d->last_init, s));
-    tts_status st = enqueue_prenet_go(d, 1, s);
-    ResArgs ra = d->last_ra;
-    ra.prof = prof;
-    if (!st) {
-        TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
-        bool launched = false;
-        TTS_HIP(launch_resident(ra, s, &launched));
-        if (!launched) {
-            (void)hipStreamSynchronize(s);
-            (void)hipFree(prof);
-            TTS_CHECK(false, TTS_ERR_UNSUPPORTED, "resident decoder cannot be co-resident on this device now");
-        }
-    }
     long long h[2 * RES_PHASES];
-    TTS_HIP(hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s));
-    TTS_HIP(hipMemcpyAsync(d->host_flags, ra.status, sizeof(int), hipMemcpyDeviceToHost, s));
-    TTS_HIP(hipStreamSynchronize(s));
-    (void)hipFree(prof);
-    if (st) return st;
-    TTS_CHECK(d->host_flags[0] == 0, TTS_ERR_HIP, "resident decoder: a hand-off wait timed out (internal error)");
+    if (tts_status st = res_rerun(d, true, h)) return st;
     int dev = 0, rate_khz = 1;
     TTS_HIP(hipGetDevice(&dev));
     TTS_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));
     for (int i = 0; i < 2 * RES_PHASES; ++i) us[i] = (float)(1e3 * (double)h[i] / rate_khz / d->last_steps);
+    return TTS_OK;
+}
+
+tts_status tts_decoder_resident_trace(tts_decoder* d, long long* ticks, int64_t n) {
+    TTS_CHECK(d && ticks && n >= (int64_t)(RES_PROF_LL - 2 * RES_PHASES), TTS_ERR_INVALID, "bad arguments");
+    long long h[2 * RES_PHASES];
+    if (tts_status st = res_rerun(d, false, h)) return st;  // no phase marks: only the event stamps
+    std::copy(d->res_trace.begin(), d->res_trace.end(), ticks);
     return TTS_OK;
 }
 
@@ -934,10 +958,21 @@ tts_status tts_decoder_profile(tts_decoder* d, int reps, float* kernel_ms, int n
     for (int i = 0; i <= K; ++i) TTS_HIP(hipEventCreate(&ev[i]));
     TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
     hipStream_t s = d->stream;
-    if (d->last_enc_direct)  // the last run read its encoder output in place: stage it for the step graphs
+    InitArgs init = d->last_init;
+    if (d->last_enc_direct) {
+        // the last run read its encoder output and length in place: stage copies for the step
+        // graphs.  The length is the run's own (host record: the device word it read may hold a later
+        // sentence's by now, possibly longer than this shape); the encoder rows are read from the
+        // caller's buffer as it is now (the caller keeps it alive; the step timings do not depend on
+        // its contents)
+        const int len = d->last_len_direct;
         TTS_HIP(hipMemcpyAsync(d->enc, d->last_enc_direct, (size_t)d->last_Lmax * ENC * sizeof(float),
                                hipMemcpyDeviceToDevice, s));
-    TTS_HIP(launch_decoder_init(d->last_init, s));
+        TTS_HIP(hipMemcpyAsync(d->lens, &len, sizeof(int), hipMemcpyHostToDevice, s));
+        TTS_HIP(hipStreamSynchronize(s));  // `len` is a stack copy
+        init.lens = d->lens;
+    }
+    TTS_HIP(launch_decoder_init(init, s));
     tts_status st = enqueue_prenet_go(d, d->last_B, s);
     std::vector<double> acc(K, 0.0);
     for (int r = 0; r < reps && st == TTS_OK; ++r) {

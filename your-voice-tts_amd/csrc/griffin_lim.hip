@@ -437,13 +437,15 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     const int b = blockIdx.y;
     const int f = xcd_remap(blockIdx.x, gridDim.x);
     const int Fb = a.F[b];
+    // the persistent loop's status word is cleared by block (0, 0) even when the run is empty
+    // (a speculative batch-1 run whose frame count was clamped to 0): its final overlap-add launch
+    // copies the word to the host, which must not see an earlier run's failure
+    if (INIT && a.zero_status && threadIdx.x == 0 && (blockIdx.x | blockIdx.y) == 0) *a.zero_status = 0;
     if (f >= Fb) return;
     const Geo g = a.g;
     const int tid = threadIdx.x;
-    if (INIT && tid == 0) {  // the persistent loop that follows reads tags of frames < F[b] only
-        if (a.zero_flags) a.zero_flags[(int64_t)b * a.Fmax + f] = 0u;
-        if (a.zero_status && (b | f) == 0) *a.zero_status = 0;
-    }
+    if (INIT && tid == 0 && a.zero_flags)  // the persistent loop that follows reads tags of frames < F[b] only
+        a.zero_flags[(int64_t)b * a.Fmax + f] = 0u;
     __shared__ __align__(16) double2 buf0[NH];
     __shared__ __align__(16) double2 buf1[NH];
     // the spectrum X[0, 1024) reuses buf0 (free once the forward FFT's last pass has read it; the

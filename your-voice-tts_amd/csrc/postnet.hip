@@ -102,7 +102,8 @@ namespace tts {
 // tts_postnet_run, optionally with the frame counts already on the device (T_dev[b] * tmul frames:
 // the decoder's step counts) and the input rows mel_tmax frames apart (0 = Tmax): the synthesis
 // path feeds the decoder's mel history in place, with no copy and no host-to-device transfer.
-// T still gives the host-side counts (tile sizes); both must agree.
+// T gives the host-side counts that size the tiles: with T_dev, an upper bound of the device counts
+// (frames past T[b] are not computed; the caller redoes a sentence whose device count exceeds it).
 tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const int* T_dev, int tmul, const int32_t* T,
                            int B, int Tmax, float* out, hipStream_t s) {
     TTS_CHECK(p && mel && T && out && B >= 1 && Tmax >= 1, TTS_ERR_INVALID, "bad postnet_run arguments");

@@ -2,19 +2,23 @@
 // Decoder.inference (layers/tacotron2.py:249-285) as ONE launch whose 256 workgroups (one per
 // compute unit) keep every step weight on chip — 16 gate rows of both LSTMs per CU (the
 // attention LSTM's in VGPRs, the decoder LSTM's recurrent/attention half in LDS, its context
-// half in VGPRs) plus a prenet-2 row, a query row and up to two fused mel/prenet-1/stop rows.
-// A step then streams no weights at all; its cost is the six dependent hand-offs
+// half in VGPRs) plus a prenet-2 row, a query row and one mel row (LDS).
+// A step then streams no weights from HBM; its cost is the six dependent hand-offs
 //   pre1 -> prenet2 -> h_att -> query -> [attention] -> ctx -> h_dec -> pre1
-// of which prenet2, query and ctx stay inside one XCD: every XCD computes its own copy of
-// prenet-2, the query and the attention step (one attention CU per XCD; identical results).
-// carried by 8-byte {tag, value} granules (agent-scope relaxed atomics, sc1: the hand-off form
-// that needs no fences, MI355X_MICROARCH.md "Valid forms").  Every wait is bounded: a wave
-// that does not see its data within the timeout flags an error and the grid drains.
+// of which pre1, prenet2, query and ctx stay inside one XCD: every XCD computes its own copy of
+// the folded prenet-1 rows + stopnet (round 4: those 1.5 MB of rows are read from the XCD's L2
+// every step, prefetched during the context and h_dec gathers; the register file and LDS are full), prenet-2,
+// the query and the attention step (one attention CU per XCD; identical results), so only the
+// two LSTM outputs cross XCDs.  Hand-offs are 8-byte {tag, value} granules (agent-scope relaxed
+// atomics, sc1: the hand-off form that needs no fences, MI355X_MICROARCH.md "Valid forms").
+// Every wait is bounded: a wave that does not see its data within the timeout flags an error
+// and the grid drains.
 //
 // Scope: B = 1, the synthesis attention configuration (forward attention + eval mask,
 // sigmoid norm, no location / windowing / transition agent — attention_uses_epart()), L <= 256,
-// nmel + 257 <= 512 (r <= 3).  Reads its initial state from, and leaves its final state in,
-// the multi-launch path's buffers (same slots), so continuous mode and profiling interoperate.
+// nmel <= 256 (one mel row per CU; r <= 3).  Reads its initial state from, and leaves its final
+// state in, the multi-launch path's buffers (same slots), so continuous mode and profiling
+// interoperate.
 #pragma once
 #include "decoder.h"
 
@@ -28,10 +32,12 @@ constexpr int RES_LMAX = 256;
 // granule slots (u64 {tag << 32 | float bits}) per step parity
 // (GR_PRE2X: per-XCD prenet-2 vectors, [8 XCDs][256], written and read inside one XCD; GR_SETUP:
 // each CU's XCD id, parity 0 only)
-// GR_QX: per-XCD query half-rows [8][128 rows][2]; GR_CTXX: per-XCD context + tail [8][528].
-constexpr int GR_PRE1 = 0, GR_CTRL = 256, GR_HATT = 576, GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376,
-              GR_QX = 5632, GR_CTXX = 7680, GR_CTXX_STRIDE = ENC + 16, GR_TOTAL = 11904;
-constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-2 rows 8 per CU
+// GR_QX: per-XCD query half-rows [8][128 rows][2]; GR_CTXX: per-XCD context + tail [8][528];
+// GR_P1X: per-XCD prenet-1 rows + continue flag [8][264] (slot 256 = flag).
+constexpr int GR_HATT = 576, GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376, GR_QX = 5632, GR_CTXX = 7680,
+              GR_CTXX_STRIDE = ENC + 16, GR_P1X = 11904, GR_P1X_STRIDE = PRE + 8, GR_TOTAL = GR_P1X + 8 * GR_P1X_STRIDE;
+constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-1/2 rows 8 per CU
+static_assert(RES_MIN_CUS_PER_XCD * 8 >= PRE, "at most one prenet row per wave");
 constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
 // the failure code of launch `salt` from its status word (salt << 8 | code; anything else: none)
 inline int res_status_code(int word, unsigned salt) {
@@ -49,10 +55,11 @@ struct ResWeights {
     float4* wa;   // [256 CU][14 i4][512 thr]   attention LSTM rows over [prenet | ctx | h_att]
     float4* wdl;  // [256 CU][16 i4][16 row][32 ks]  decoder LSTM rows over [h_att | h_dec] (LDS image)
     float4* wdc;  // [256 CU][4 i4][512 thr]    decoder LSTM rows over ctx
-    float4* ws;   // [256 CU][8 wave][6 i4][64 lane]  waves 2/3: fused rows c, c + 256
+    float* wf;    // folded rows [nrows][1536] = [mel | W1 W_mel (prenet-1) | stop] over [h_dec | ctx],
+                  // reference layout: mel row c -> LDS of CU c; prenet-1 rows and the stop row per XCD
+    float* bf;    // [nrows] folded biases
     float* ba;    // [256][16] attention LSTM bias (b_ih + b_hh), logical row g*4 + u
     float* bd;    // [256][16] decoder LSTM bias
-    float* bs;    // [256][2] fused-row biases (rows c, c + 256)
     float* w2;    // prenet layer-2 weight, reference layout [256][256] (rows picked per XCD rank)
     float* wq;    // query_layer weight, reference layout [128][1024] (rows picked per XCD rank)
 };
@@ -87,10 +94,15 @@ struct ResArgs {
     float* align_hist;
     unsigned long long* gran;  // [2][GR_TOTAL], zeroed before every launch
     int* status;               // [0]: 0 ok, else the id of the wait that timed out
-    long long* prof;           // null, or [2][RES_PHASES] wall-clock ticks summed over steps per phase
-                               // (CU 0, attention CU) — measurement only
+    long long* prof;           // null, or RES_PROF_LL: [2][RES_PHASES] wall-clock ticks summed over steps
+                               // per phase (CU 0, attention CU), then the event trace — measurement only
+    int prof_marks;            // with prof: also the per-phase marks (they perturb the two CUs that take them)
 };
 constexpr int RES_PHASES = 16;
+// profiling re-run only: prof also holds [256 CU][RES_TRACE_STEPS][RES_TRACE_EV] event ticks
+// (P1, B1, h_att published, B3, B4, h_dec published, B6, pre1 row published)
+constexpr int RES_TRACE_STEPS = 64, RES_TRACE_EV = 8;
+constexpr size_t RES_PROF_LL = 2 * RES_PHASES + (size_t)RES_CUS * RES_TRACE_STEPS * RES_TRACE_EV;
 
 // Pack the reference-layout weights (device pointers) into ResWeights (allocated by the caller,
 // sizes from resident_weight_floats).
@@ -102,7 +114,7 @@ struct ResSrc {
     const float *wf, *bf;                        // folded [nrows][1536] + [nrows]
     int nrows;
 };
-void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc, size_t* ws);
+void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc);
 hipError_t resident_pack(const ResSrc& src, const ResWeights& w, hipStream_t s);
 size_t resident_smem_bytes();
 hipError_t resident_prepare();

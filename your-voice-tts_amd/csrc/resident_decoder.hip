@@ -10,9 +10,11 @@
 //   7. CU 255: energies, sigmoid, forward attention + mask, context, publish ctx_t and the tail
 //      (common_layers.py:178-182, 199-223, 239-253)
 //   8. gather ctx_t; 9. context part, cell, publish h_dec_t               (tacotron2.py:206-208)
-//  10. gather h_dec_t; 11. waves 2/3: fused rows c, c+256 = [mel | prenet-1 of t+1 | stop]:
-//      mel -> history, prenet-1 -> publish, stop -> sigmoid + stop rule -> publish continue flag
-//      (tacotron2.py:214-224, 256-277)
+//  10. gather h_dec_t (the prenet-1 row weights of step 11 in flight from the XCD's L2);
+//  11. every wave: one folded prenet-1 row of this XCD's copy -> XCD-local publish; the XCD's
+//      stop CU (rank 0), wave 3: the stop row -> sigmoid + stop rule -> XCD-local continue flag
+//      (tacotron2.py:214-224, 256-277).  Mel row c of step t is written by wave 4 during step
+//      t+1's h_att gather (after the loop for the last step).
 // Reductions keep fixed orders (bitwise run-to-run deterministic).
 #include "resident.h"
 
@@ -23,13 +25,9 @@ typedef unsigned long long u64;
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) int gint;
 
-#ifndef RES_GW
-#define RES_GW 4
-#endif
 #ifndef RES_SLEEP
 #define RES_SLEEP 0  // s_sleep between polls: 0 measured 11.03 -> 10.70 us per step (tools/dec_ab.sh)
 #endif
-constexpr int GW = RES_GW;  // waves that sweep the 1024- and 512-granule vectors
 
 __device__ __forceinline__ void publish(u64* g, unsigned tag, float v) {
     __hip_atomic_store((gu64*)g, ((u64)tag << 32) | (u64)__float_as_uint(v), __ATOMIC_RELAXED,
@@ -78,6 +76,38 @@ __device__ __forceinline__ bool sweep2(u64* g, F idx, T tag, float (&v)[N], long
 template <int N, typename F>
 __device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo) {
     return sweep2<N>(g, idx, [&](int) { return tag; }, v, tmo);
+}
+
+// Granule pairs: every gather of the step loop reads ONE 16-byte pair (2 granules) per lane, an
+// sc1 buffer load (L1-bypassing; volatile, so every poll re-issues it).  A poll's latency grows
+// with the loads per lane (tools/microbench/edge.hip, round 4: device-wide 1024 granules 2.31 us per
+// edge with 4 x 8-byte loads per lane on 4 waves, 1.60-1.63 with one pair or two granules per lane
+// on 8 waves; XCD-local 256 granules 1.14 us with 4 per lane on one wave, 0.47 with one pair per
+// lane on 2 waves).  Each 8-byte half is written whole by one store, so a pair is never torn
+// within a half (MI355X_MICROARCH.md "Valid forms", R2's granule); both tags are checked.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int SC1_VOLATILE = (int)0x80000010u;  // buffer aux: sc1 (bit 4) | volatile (bit 31)
+// One wave polls one pair per lane at granule slot `slot` (even; < 0: none) until its tags equal
+// `tag` (the second half only when `both`); v0/v1 = the two values.  false after `tmo` ticks.
+__device__ __forceinline__ bool sweep_pair(__amdgpu_buffer_rsrc_t r, int slot, bool both, unsigned tag, float& v0,
+                                           float& v1, long long tmo) {
+    long long t_end = 0;
+    for (int spin = 0;; ++spin) {
+        bool ok = true;
+        if (slot >= 0) {
+            const u32x4 x = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, slot * 8, 0, SC1_VOLATILE));
+            v0 = __uint_as_float(x.x);
+            v1 = __uint_as_float(x.z);
+            ok = x.y == tag && (!both || x.w == tag);
+        }
+        if (__all(ok)) return true;
+        if (spin == 0) {
+            t_end = (long long)wall_clock64() + tmo;
+        } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
+            return false;
+        }
+        if (RES_SLEEP) __builtin_amdgcn_s_sleep(RES_SLEEP);
+    }
 }
 
 // LSTM cell of units 4c..4c+3 from the 16 gate sums (row g*4 + u, torch order i, f, g, o): lanes
@@ -138,7 +168,7 @@ __device__ __forceinline__ int res_candidate(int s, int nn, int np, int L) {
 constexpr int SM_WDL = 16 * 16 * 32 * 4;  // floats of the decoder-LSTM LDS weight image (128 KiB)
 constexpr int SM_ST = 64;                  // biases, cell states, stop-rule state
 constexpr int SM_RQ = 4 * 64 * 4;          // query row [4 i4][64 lanes] float4 | attention CU scratch
-constexpr int SM_RM = 2 * 6 * 64 * 4 + 2 * 256;  // fused rows [2][6][64] float4 | row 0 + energy partials
+constexpr int SM_RM = 2 * 6 * 64 * 4 + 2 * 256;  // mel row c, stop row: [2][6][64] float4 | row c + energy partials
 constexpr int SM_PROF = 2 * 16;            // RES_PHASES tick accumulators (long long)
 constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 16 + SM_ST + SM_RQ + SM_RM + SM_PROF + PRE;
 static_assert(SM_RM >= 6 * 64 * 4 + RES_WAVES * RES_LMAX, "attention CU partials");
@@ -159,10 +189,10 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     float* gates = xq + ADIM;  // [16]
     int* flags = reinterpret_cast<int*>(gates + 16);  // [0] stop seen, [1] abort
     float* st = gates + 32;    // [0,16) b_att, [16,32) b_dec (row g*4+u), [32,36) c_att, [36,40) c_dec,
-                               // [40,44) h_att, [44,48) h_dec of units 4c+u, [48,50) fused biases,
-                               // [50] flag1, [51] count (int bits, stop lane)
+                               // [40,44) h_att, [44,48) h_dec of units 4c+u, [48] mel bias, [49] stop
+                               // bias, [50] flag1, [51] count (int bits, stop lane)
     float* rq = st + SM_ST;    // query row (CUs < 128) | attention CU: aold, an, scr, v
-    float* rm = rq + SM_RQ;    // fused rows c, c+256 | attention CU: row c + energy partials
+    float* rm = rq + SM_RQ;    // mel row c, stop row (stop CU) | attention CU: row c + energy partials
     float* abuf = rq;                 // [2][RES_LMAX] previous alpha, ping-pong by step parity
     float* an = abuf + 2 * RES_LMAX;  // unnormalised forward weights of this step
     float* scr = an + RES_LMAX;       // [2 * RES_WAVES] + candidate values [16]
@@ -173,6 +203,11 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     // optional phase timing (thread 0 of CU 0 and of the logging attention CU)
     bool prof = false;
     long long plast = 0;
+    // event trace of the profiling re-run (RES_TRACE_STEPS steps x RES_TRACE_EV events per CU,
+    // wall_clock64 ticks): measurement only
+    long long* trace = a.prof ? a.prof + 2 * RES_PHASES + (size_t)c * RES_TRACE_STEPS * RES_TRACE_EV : nullptr;
+#define RES_EV(t, k)                                                                                \
+    if (trace && (t) < RES_TRACE_STEPS) trace[(t) * RES_TRACE_EV + (k)] = (long long)wall_clock64();
 #define RES_MARK(k)                                     \
     if (prof && tid == 0) {                             \
         const long long now = (long long)wall_clock64(); \
@@ -182,8 +217,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
 
     // ---- weights (loaded once per call) and initial state
     float4 wa[14], wdc[4];
-    // fused rows c, c + 256 (waves 2/3) in LDS
-    const float4* wsp = a.w.ws + ((size_t)c * RES_WAVES + wave) * 6 * 64 + lane;
+    constexpr int KF = HDEC + ENC;  // folded-row length
     {
         const float4* p = a.w.wa + (size_t)c * 14 * RES_THREADS + tid;
 #pragma unroll
@@ -191,8 +225,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         const float4* q = a.w.wdc + (size_t)c * 4 * RES_THREADS + tid;
 #pragma unroll
         for (int i = 0; i < 4; ++i) wdc[i] = q[(size_t)i * RES_THREADS];
-        if ((wave == 2 || wave == 3) && (c + 256 * (wave - 2)) < a.nrows)
-            for (int i = 0; i < 6; ++i) reinterpret_cast<float4*>(rm)[((wave - 2) * 6 + i) * 64 + lane] = wsp[i * 64];
+        if (wave == 2 && c < a.nmel)  // mel row c in LDS
+            for (int i = 0; i < 6; ++i) reinterpret_cast<float4*>(rm)[i * 64 + lane] = ld4(a.w.wf + (size_t)c * KF + i * 256 + lane * 4);
         const float4* l = a.w.wdl + (size_t)c * (SM_WDL / 4);
         for (int i = tid; i < SM_WDL / 4; i += RES_THREADS) wdl[i] = l[i];
     }
@@ -204,7 +238,8 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         st[32 + tid] = a.c_att[4 * c + tid];
         st[36 + tid] = a.c_dec[4 * c + tid];
     }
-    if (tid < 2) st[48 + tid] = a.w.bs[c * 2 + tid];
+    if (tid == 0) st[48] = c < a.nmel ? a.w.bf[c] : 0.f;
+    if (tid == 1) st[49] = a.w.bf[a.nmel + PRE];
     for (int k = tid; k < HATT; k += RES_THREADS) {
         xh_att[k] = a.h_att[a.hps + k];  // step 0 reads slot 1 (decoder_init_kernel)
         xh_dec[k] = a.h_dec[a.hps + k];
@@ -254,17 +289,27 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     if (flags[1]) return;
     const int rank = flags[2], nx = flags[3];
     const int p2lo = rank * PRE / nx, p2hi = (rank + 1) * PRE / nx;
-    const int r0 = p2lo + wave, r1 = p2lo + wave + RES_WAVES;  // this wave's prenet-2 rows (< p2hi)
-    const float4 wp0 = r0 < p2hi ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
-    const float4 wp1 = r1 < p2hi ? ld4(a.w.w2 + r1 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    // this wave's prenet-2 row and prenet-1 row of the XCD's copies (nx >= 32: at most one per wave)
+    const int r0 = p2lo + wave;
+    const bool has_row = r0 < p2hi;
+    const float4 wp0 = has_row ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
+    const float bp1 = has_row ? a.w.bf[a.nmel + r0] : 0.f;
+    // folded prenet-1 row (re-read from the XCD's L2 every step: no register or LDS room); a wave
+    // without a row loads row 0 and discards it (no branch around the loads)
+    const float* w1p = a.w.wf + (size_t)(a.nmel + (has_row ? r0 : 0)) * KF + lane * 4;
+    const bool stop_cu = rank == 0;  // this XCD's stopnet + stop rule
+    if (stop_cu && wave == 3)
+        for (int i = 0; i < 6; ++i)
+            reinterpret_cast<float4*>(rm)[(6 + i) * 64 + lane] = ld4(a.w.wf + (size_t)(a.nmel + PRE) * KF + i * 256 + lane * 4);
     // query rows 4 rank .. 4 rank + 3 of this XCD's copy: wave w holds half (w & 1) of row 4 rank + w / 2
     const int qrow = 4 * rank + (wave >> 1), qhalf = wave & 1;
     const float4 wq0 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + lane * 4);
     const float4 wq1 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + 256 + lane * 4);
     const int L = a.L;
     const bool att_cu = rank == nx - 1;               // the last CU of each XCD runs its attention copy
-    const bool att_log = att_cu && xcc == flags[4];  // ... and one of them writes the alignment rows
-    prof = a.prof != nullptr && (c == 0 || att_log);
+    const bool xlog = xcc == flags[4];                // the XCD whose copies write the outputs
+    const bool att_log = att_cu && xlog;              // ... alignment rows
+    prof = a.prof != nullptr && a.prof_marks && (c == 0 || att_log);
     if (prof && tid == 0) plast = (long long)wall_clock64();
     int n = 0, n_prev = 0;
     float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f}, ptc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -283,8 +328,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         if (tid < ADIM) xv[tid] = a.v[tid];
         prefetch_rows(n);
     }
-    const int srow = a.nmel + PRE;  // the stop row of the fused GEMM
-    const bool stop_lane = c == (srow & 255) && wave == 2 + (srow >> 8) && lane == 0;
+    const bool stop_lane = stop_cu && wave == 3 && lane == 0;
     if (stop_lane) {
         reinterpret_cast<int*>(st)[50] = a.flag1[0];
         reinterpret_cast<int*>(st)[51] = a.count[0];
@@ -292,19 +336,28 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     u64* Gx = a.gran + GR_PRE2X + xcc * PRE;  // this XCD's prenet-2 slots (parity offset added below)
     u64* Gq = a.gran + GR_QX + xcc * 2 * ADIM;   // this XCD's query half-rows
     u64* Gc = a.gran + GR_CTXX + xcc * GR_CTXX_STRIDE;  // this XCD's context + tail
+    u64* G1 = a.gran + GR_P1X + xcc * GR_P1X_STRIDE;    // this XCD's prenet-1 rows + continue flag
+    // the gathers' pair loads: one buffer resource over both parities' granules, slot offsets
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc(a.gran, (short)0, 2 * GR_TOTAL * 8, 0x00020000);
+    const int s_x = GR_PRE2X + xcc * PRE, s_q = GR_QX + xcc * 2 * ADIM, s_c = GR_CTXX + xcc * GR_CTXX_STRIDE,
+              s_1 = GR_P1X + xcc * GR_P1X_STRIDE;
+    const int pk = wave * 64 + lane;  // this lane's pair of a gather over all waves
+    // mel row c of step tt from xh_dec / xctx (= h_dec_tt, ctx_tt), by one wave
+    auto mel_row = [&](int tt) {
+        if (c >= a.nmel) return;
+        const float4* wm = reinterpret_cast<const float4*>(rm) + lane;
+        float sm_ = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sm_ = dot4(wm[i * 64], ld4(xh_dec + i * 256 + lane * 4), sm_);
+#pragma unroll
+        for (int i = 4; i < 6; ++i) sm_ = dot4(wm[i * 64], ld4(xctx + (i - 4) * 256 + lane * 4), sm_);
+        sm_ = wave_sum_dpp(sm_);
+        if (lane == 0 && tt < a.hist_cap) a.mel_hist[(int64_t)tt * a.nmel + c] = sm_ + st[48];
+    };
     int t = 0;
     for (;; ++t) {
         u64* G = a.gran + (t & 1) * GR_TOTAL;          // this step's granules
-        u64* Gp = a.gran + ((t & 1) ^ 1) * GR_TOTAL;   // the previous step's (pre1, continue flag)
         const unsigned E = (a.salt << 14) | ((unsigned)t * 8u);  // tags E+1 .. E+6, never 0
-        if (att_cu && t > 0) {
-            // the next attention step's operands, in flight while pre1 is awaited: the encoder rows
-            // the mask can keep and P at the candidate positions
-            prefetch_rows(n);
-            const int pos = res_candidate(tid >> 5, n, n_prev, L);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) ptc[m] = pos >= 0 ? a.Pt[(int64_t)((tid & 31) + 32 * m) * a.Lcap + pos] : 0.f;
-        }
         // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}]
         float acc_a = 0.f;
 #pragma unroll
@@ -319,49 +372,52 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
 #pragma unroll 2
         for (int i = 8; i < 16; ++i)
             acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
-        // 2) prenet layer 2: wave 0 gathers pre1_t (+ the previous step's continue flag); every
-        //    wave computes its rows of this XCD's copy, publishes them XCD-locally; wave 0 gathers
-        if (wave == 0) {
-            const int gp = ((t & 1) ^ 1) * GR_TOTAL;
-            float p[5];
+        // 2) prenet layer 2: wave 0 gathers this XCD's pre1_t (+ the previous step's continue flag);
+        //    every wave computes its row of this XCD's copy, publishes it XCD-locally; wave 0 gathers
+        // (waves 0, 1: the 256 rows as pairs; wave 2, lane 0: the flag)
+        if (wave < 3) {
+            const int gp = s_1 + ((t & 1) ^ 1) * GR_TOTAL;
             bool ok = true;
             if (t == 0) {
-                const float4 v = ld4(a.pre1 + lane * 4);  // go frame's layer 1 (enqueue_prenet_go)
-                p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w; p[4] = 1.f;
+                if (wave == 0) {
+                    const float4 v = ld4(a.pre1 + lane * 4);  // go frame's layer 1 (enqueue_prenet_go)
+                    xp1[lane * 4] = v.x; xp1[lane * 4 + 1] = v.y; xp1[lane * 4 + 2] = v.z; xp1[lane * 4 + 3] = v.w;
+                }
             } else {
-                ok = sweep<5>(a.gran, E - 2, p, [&](int i) { return gp + (i < 4 ? GR_PRE1 + lane * 4 + i : GR_CTRL); }, tmo);
+                float p0 = 0.f, p1 = 0.f;
+                if (wave < 2) {
+                    ok = sweep_pair(rg, gp + 2 * pk, true, E - 2, p0, p1, tmo);
+                    xp1[2 * pk] = p0;
+                    xp1[2 * pk + 1] = p1;
+                } else {
+                    ok = sweep_pair(rg, lane == 0 ? gp + PRE : -1, false, E - 2, p0, p1, tmo);
+                    if (lane == 0 && ok && p0 == 0.f) flags[0] = 1;
+                }
             }
             RES_MARK(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) xp1[lane * 4 + i] = p[i];
-            if (lane == 0) {
-                if (!ok) { flags[1] = 1; fail(a.status, 1); }
-                if (ok && p[4] == 0.f) flags[0] = 1;
-            }
+            if (lane == 0 && !ok) { flags[1] = 1; fail(a.status, 1); }
         }
         __syncthreads();  // P1
+        if (tid == 0) { RES_EV(t, 0) }
         if (flags[0] | flags[1]) break;
         {
             const float4 x = ld4(xp1 + lane * 4);
             u64* gx = Gx + (t & 1) * GR_TOTAL;
-            if (r0 < p2hi) {
+            if (has_row) {
                 const float s0 = wave_sum_dpp(dot4(wp0, x, 0.f));
                 if (lane == 0) publish_xcd(gx + r0, E + 1, fmaxf(s0, 0.f));
             }
-            if (r1 < p2hi) {
-                const float s1 = wave_sum_dpp(dot4(wp1, x, 0.f));
-                if (lane == 0) publish_xcd(gx + r1, E + 1, fmaxf(s1, 0.f));
-            }
             RES_MARK(1);
-            if (wave == 0) {
-                float q4[4];
-                const bool ok = sweep<4>(gx, E + 1, q4, [&](int i) { return lane * 4 + i; }, tmo);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) xpre[lane * 4 + i] = q4[i];
+            if (wave < 2) {
+                float q0, q1;
+                const bool ok = sweep_pair(rg, s_x + (t & 1) * GR_TOTAL + 2 * pk, true, E + 1, q0, q1, tmo);
+                xpre[2 * pk] = q0;
+                xpre[2 * pk + 1] = q1;
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7); }
             }
         }
         __syncthreads();  // B1
+        if (tid == 0) { RES_EV(t, 1) }
         if (flags[1]) break;
         RES_MARK(2);
         // 3) prenet part, cell
@@ -378,18 +434,31 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 st[32 + tid] = cs;
                 st[40 + tid] = h;
                 publish(G + GR_HATT + 4 * c + tid, E + 2, h);
+                if (tid == 0) { RES_EV(t, 2) }
             }
         }
-        // 4) gather h_att_t
-        if (wave < GW) {
-            constexpr int PER = HATT / (64 * GW);
-            float v4[PER];
-            const bool ok = sweep<PER>(G, E + 2, v4, [&](int i) { return GR_HATT + wave * 64 * PER + i * 64 + lane; }, tmo);
+        // 4) gather h_att_t (all waves); first wave 4 writes the mel row c of step t-1 (xh_dec, xctx
+        //    still hold h_dec_{t-1}, ctx_{t-1}): off the critical path of step t-1's pre1 rows.  The
+        //    attention CU first issues this step's attention operands (the encoder rows the mask can
+        //    keep, P at the candidate positions): in flight while h_att is awaited (a load issued
+        //    before the pre1 poll instead held that poll up by its latency, vmcnt being in order, and
+        //    with it the XCD's prenet-2 rows: 1.2 us per step, round-4 trace)
+        if (att_cu && t > 0) {
+            prefetch_rows(n);
+            const int pos = res_candidate(tid >> 5, n, n_prev, L);
 #pragma unroll
-            for (int i = 0; i < PER; ++i) xh_att[wave * 64 * PER + i * 64 + lane] = v4[i];
+            for (int m = 0; m < 4; ++m) ptc[m] = pos >= 0 ? a.Pt[(int64_t)((tid & 31) + 32 * m) * a.Lcap + pos] : 0.f;
+        }
+        {
+            if (wave == 4 && t > 0) mel_row(t - 1);
+            float h0, h1;
+            const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HATT + 2 * pk, true, E + 2, h0, h1, tmo);
+            xh_att[2 * pk] = h0;
+            xh_att[2 * pk + 1] = h1;
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2); }
         }
         __syncthreads();  // B3
+        if (tid == 0) { RES_EV(t, 3) }
         if (flags[1]) break;
         RES_MARK(4);
         // 5) query half-rows of this XCD's copy (common_layers.py:179), published XCD-locally
@@ -399,12 +468,11 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             s = wave_sum_dpp(s);
             if (lane == 0) publish_xcd(Gq + (t & 1) * GR_TOTAL + 2 * qrow + qhalf, E + 3, s);
         }
-        // 6) decoder LSTM over h_att_t (its h_dec_{t-1} half ran at the loop top); the attention
-        //    CU does this after its attention step, which is on the critical path
-        if (!att_cu) {
+        // 6) decoder LSTM over h_att_t (its h_dec_{t-1} half ran at the loop top); on the attention
+        //    CU too, while the query is still in flight (after the attention step it would delay
+        //    that CU's h_dec publish, which every CU waits for)
 #pragma unroll 2
-            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
-        }
+        for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
         RES_MARK(5);
         // 7) attention step.  After the forward mask the previous alpha is nonzero only on the
         //    previous window S' = W(n') = {(n'-2) mod L} + [n'-1, n'+2], so every position outside
@@ -425,11 +493,10 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
 #pragma unroll
             for (int m = 0; m < 4; ++m) xvd[m] = xv[sub + 32 * m];
             const float a_pos = pos >= 0 ? aold[pos] : 0.f, a_prev = pos > 0 ? aold[pos - 1] : 0.f;
-            if (wave == 0) {
-                float q4[4];
-                const bool ok = sweep<4>(Gq + (t & 1) * GR_TOTAL, E + 3, q4, [&](int i) { return lane * 4 + i; }, tmo);
-                xq[2 * lane] = q4[0] + q4[1];
-                xq[2 * lane + 1] = q4[2] + q4[3];
+            if (wave < 2) {  // query row pk = its two half-rows
+                float q0, q1;
+                const bool ok = sweep_pair(rg, s_q + (t & 1) * GR_TOTAL + 2 * pk, true, E + 3, q0, q1, tmo);
+                xq[pk] = q0 + q1;
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3); }
             }
             __syncthreads();  // A1
@@ -544,23 +611,29 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (att_log && t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
             n_prev = n;
             n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: loop top)
-#pragma unroll 2
-            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
             RES_MARK(9);
         }
-        // 8) gather ctx_t and the tail
-        if (wave < GW && !att_cu) {
-            constexpr int PER = ENC / (64 * GW);
-            float v3[PER + 1];
-            const bool ok = sweep<PER + 1>(Gc + (t & 1) * GR_TOTAL, E + 4, v3, [&](int i) {
-                return i < PER ? wave * 64 * PER + i * 64 + lane : (wave == 0 && lane == 0 ? ENC : -1);
-            }, tmo);
+        // this wave's prenet-1 row weights (step 11) from the XCD's L2, in flight while the context
+        // (and then h_dec) is awaited
+        float4 w1[6];
 #pragma unroll
-            for (int i = 0; i < PER; ++i) xctx[wave * 64 * PER + i * 64 + lane] = v3[i];
-            if (wave == 0 && lane == 0) xctx[ENC] = v3[PER];
+        for (int i = 0; i < 6; ++i) w1[i] = ld4(w1p + i * 256);
+        // 8) gather ctx_t and the tail
+        if (wave < 5 && !att_cu) {  // waves 0-3: the 512 context values as pairs; wave 4, lane 0: the tail
+            const int gc = s_c + (t & 1) * GR_TOTAL;
+            float c0 = 0.f, c1 = 0.f;
+            const bool ok = wave < 4 ? sweep_pair(rg, gc + 2 * pk, true, E + 4, c0, c1, tmo)
+                                     : sweep_pair(rg, lane == 0 ? gc + ENC : -1, false, E + 4, c0, c1, tmo);
+            if (wave < 4) {
+                xctx[2 * pk] = c0;
+                xctx[2 * pk + 1] = c1;
+            } else if (lane == 0) {
+                xctx[ENC] = c0;
+            }
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4); }
         }
         __syncthreads();  // B4
+        if (tid == 0) { RES_EV(t, 4) }
         if (flags[1]) break;
         RES_MARK(10);
         // 9) context part, cell
@@ -577,72 +650,83 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 st[36 + tid] = cs;
                 st[44 + tid] = h;
                 publish(G + GR_HDEC + 4 * c + tid, E + 5, h);
+                if (tid == 0) { RES_EV(t, 5) }
             }
         }
         // 10) gather h_dec_t
-        if (wave < GW) {
-            constexpr int PER = HDEC / (64 * GW);
-            float v4[PER];
-            const bool ok = sweep<PER>(G, E + 5, v4, [&](int i) { return GR_HDEC + wave * 64 * PER + i * 64 + lane; }, tmo);
-#pragma unroll
-            for (int i = 0; i < PER; ++i) xh_dec[wave * 64 * PER + i * 64 + lane] = v4[i];
+        {
+            float h0, h1;
+            const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HDEC + 2 * pk, true, E + 5, h0, h1, tmo);
+            xh_dec[2 * pk] = h0;
+            xh_dec[2 * pk + 1] = h1;
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5); }
         }
         __syncthreads();  // B6
+        if (tid == 0) { RES_EV(t, 6) }
         if (flags[1]) break;
         RES_MARK(12);
-        long long m0 = 0;  // fused-row phase timing (wave 2, lane 0)
+        long long m0 = 0;  // prenet-1 / mel / stop row phase timing (wave 2, lane 0)
         if (prof && tid == 128) m0 = (long long)wall_clock64();
-        // 11) fused rows [mel | prenet-1 of step t+1 | stop]
-        if (wave == 2 || wave == 3) {
-            const int row = c + 256 * (wave - 2);
-            if (row < a.nrows) {
-                float s = 0.f;
-                const float4* wm = reinterpret_cast<const float4*>(rm) + (wave - 2) * 6 * 64 + lane;
+        // 11) this wave's folded prenet-1 row of step t+1 (XCD copy) and, on the stop CU's wave 3,
+        //     the stop row in the same pass
+        {
+            const bool stw = stop_cu && wave == 3;
+            const float4* wsr = reinterpret_cast<const float4*>(rm) + 6 * 64 + lane;
+            float s = 0.f, ss = 0.f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) s = dot4(wm[i * 64], ld4(xh_dec + i * 256 + lane * 4), s);
+            for (int i = 0; i < 4; ++i) {
+                const float4 x = ld4(xh_dec + i * 256 + lane * 4);
+                s = dot4(w1[i], x, s);
+                if (stw) ss = dot4(wsr[i * 64], x, ss);
+            }
 #pragma unroll
-                for (int i = 4; i < 6; ++i) s = dot4(wm[i * 64], ld4(xctx + (i - 4) * 256 + lane * 4), s);
-                s = wave_sum_dpp(s);
-                const float v = s + st[48 + wave - 2];
+            for (int i = 4; i < 6; ++i) {
+                const float4 x = ld4(xctx + (i - 4) * 256 + lane * 4);
+                s = dot4(w1[i], x, s);
+                if (stw) ss = dot4(wsr[i * 64], x, ss);
+            }
+            s = wave_sum_dpp(s);
+            u64* g1 = G1 + (t & 1) * GR_TOTAL;
+            if (has_row && lane == 0) {
+                const float p = fmaxf(s + bp1, 0.f);
+                publish_xcd(g1 + r0, E + 6, p);
+                if (wave == 0) { RES_EV(t, 7) }
+                if (xlog) a.pre1[r0] = p;  // the next step's layer 1 (continuous mode reads it)
+            }
+            if (stw) {
+                ss = wave_sum_dpp(ss);
                 if (lane == 0) {
-                    if (row < a.nmel) {
-                        if (t < a.hist_cap) a.mel_hist[(int64_t)t * a.nmel + row] = v;
-                    } else if (row < a.nmel + PRE) {
-                        const float p = fmaxf(v, 0.f);
-                        a.pre1[row - a.nmel] = p;
-                        publish(G + GR_PRE1 + row - a.nmel, E + 6, p);
-                    } else {
-                        // stopnet + stop rule (tacotron2.py:219-224, 257-277), as EPI_MEL_FUSED rule 0
-                        const float stv = sigmoidf_(v);
-                        if (t < a.hist_cap) a.stop_hist[t] = stv;
-                        const float tail = xctx[ENC];
-                        int* sst = reinterpret_cast<int*>(st);
-                        const int f1 = sst[50] | ((tail > 0.8f && t > L) ? 1 : 0);
-                        sst[50] = f1;
-                        int nd = 0;
-                        if (f1 && t > 2 * L) {
-                            sst[51] += 1;
-                            if (sst[51] > 20) nd = 1;
-                        } else if (t + 1 == a.max_steps) {
-                            nd = 1;
-                        }
-                        if (!nd && t + 1 >= a.hist_cap) {  // cannot happen: the rule stops by max_steps + 20
-                            nd = 1;
-                            fail(a.status, 100);
-                        }
-                        if (nd) {
-                            a.done[0] = 1;
-                            a.n_steps[0] = t + 1;
-                        }
-                        publish(G + GR_CTRL, E + 6, nd ? 0.f : 1.f);
+                    // stopnet + stop rule (tacotron2.py:219-224, 257-277), as EPI_MEL_FUSED rule 0;
+                    // every XCD's stop CU decides identically, the logging XCD writes the outputs
+                    const float stv = sigmoidf_(ss + st[49]);
+                    if (xlog && t < a.hist_cap) a.stop_hist[t] = stv;
+                    const float tail = xctx[ENC];
+                    int* sst = reinterpret_cast<int*>(st);
+                    const int f1 = sst[50] | ((tail > 0.8f && t > L) ? 1 : 0);
+                    sst[50] = f1;
+                    int nd = 0;
+                    if (f1 && t > 2 * L) {
+                        sst[51] += 1;
+                        if (sst[51] > 20) nd = 1;
+                    } else if (t + 1 == a.max_steps) {
+                        nd = 1;
                     }
+                    if (!nd && t + 1 >= a.hist_cap) {  // cannot happen: the rule stops by max_steps + 20
+                        nd = 1;
+                        fail(a.status, 100);
+                    }
+                    if (nd && xlog) {
+                        a.done[0] = 1;
+                        a.n_steps[0] = t + 1;
+                    }
+                    publish_xcd(g1 + PRE, E + 6, nd ? 0.f : 1.f);
                 }
             }
         }
         if (prof && tid == 128) pacc[13] += (long long)wall_clock64() - m0;
     }
     if (flags[1]) return;
+    if (wave == 4 && t > 0) mel_row(t - 1);  // the last step's mel row (its h_att gather never came)
     if (prof && tid == 0)
         for (int k = 0; k < RES_PHASES; ++k) a.prof[(c == 0 ? 0 : 1) * RES_PHASES + k] = pacc[k];
     // the last step t-1 leaves its state where the multi-launch path's would be
@@ -691,40 +775,22 @@ __global__ void res_pack_wd(const float* wih, const float* whh, float4* wdl, flo
         wdc[((int64_t)c * 4 + i4) * RES_THREADS + tid] = float4{v[0], v[1], v[2], v[3]};
     }
 }
-__global__ void res_pack_ws(const float* w2, const float* wq, const float* wf, int nrows, float4* out) {
-    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (int64_t)RES_CUS * RES_WAVES * 6 * 64) return;
-    const int lane = idx % 64, i4 = (idx / 64) % 6, w = (idx / 384) % RES_WAVES, c = idx / (384 * RES_WAVES);
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < 4; ++j) {
-        if (w == 2 || w == 3) {
-            const int row = c + 256 * (w - 2);
-            if (row < nrows) v[j] = wf[(int64_t)row * (HDEC + ENC) + i4 * 256 + lane * 4 + j];
-        }
-    }
-    out[idx] = float4{v[0], v[1], v[2], v[3]};
-}
-__global__ void res_pack_bias(const float* abih, const float* abhh, const float* dbih, const float* dbhh,
-                              const float* bf, int nrows, float* ba, float* bd, float* bs) {
+__global__ void res_pack_bias(const float* abih, const float* abhh, const float* dbih, const float* dbhh, float* ba,
+                              float* bd) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx < RES_CUS * 16) {
         const int c = idx / 16, r = idx % 16, row = (r >> 2) * HATT + 4 * c + (r & 3);
         ba[idx] = abih[row] + abhh[row];
         bd[idx] = dbih[row] + dbhh[row];
     }
-    if (idx < RES_CUS * 2) {
-        const int row = idx / 2 + 256 * (idx % 2);
-        bs[idx] = row < nrows ? bf[row] : 0.f;
-    }
 }
 
 }  // namespace
 
-void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc, size_t* ws) {
+void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc) {
     *wa = (size_t)RES_CUS * 14 * RES_THREADS * 4;
     *wdl = (size_t)RES_CUS * 16 * 16 * 32 * 4;
     *wdc = (size_t)RES_CUS * 4 * RES_THREADS * 4;
-    *ws = (size_t)RES_CUS * RES_WAVES * 6 * 64 * 4;
 }
 
 hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
@@ -735,10 +801,10 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
                        s.d_whh, w.wdl, w.wdc);
     (void)hipMemcpyAsync(w.w2, s.w_pre2, sizeof(float) * PRE * PRE, hipMemcpyDeviceToDevice, st);
     (void)hipMemcpyAsync(w.wq, s.w_q, sizeof(float) * ADIM * HATT, hipMemcpyDeviceToDevice, st);
-    hipLaunchKernelGGL(res_pack_ws, blocks((int64_t)RES_CUS * RES_WAVES * 6 * 64), dim3(256), 0, st, s.w_pre2, s.w_q,
-                       s.wf, s.nrows, w.ws);
-    hipLaunchKernelGGL(res_pack_bias, blocks(RES_CUS * 16), dim3(256), 0, st, s.a_bih, s.a_bhh, s.d_bih, s.d_bhh, s.bf,
-                       s.nrows, w.ba, w.bd, w.bs);
+    (void)hipMemcpyAsync(w.wf, s.wf, sizeof(float) * s.nrows * (HDEC + ENC), hipMemcpyDeviceToDevice, st);
+    (void)hipMemcpyAsync(w.bf, s.bf, sizeof(float) * s.nrows, hipMemcpyDeviceToDevice, st);
+    hipLaunchKernelGGL(res_pack_bias, blocks(RES_CUS * 16), dim3(256), 0, st, s.a_bih, s.a_bhh, s.d_bih, s.d_bhh, w.ba,
+                       w.bd);
     return hipGetLastError();
 }
 
@@ -751,7 +817,7 @@ hipError_t resident_prepare() {
 
 hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched) {
     *launched = false;
-    if (a.L < 2 || a.L > RES_LMAX || a.nrows >= 2 * RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
+    if (a.L < 2 || a.L > RES_LMAX || a.nmel > RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
     ResArgs arg = a;
     void* args[] = {&arg};
     return launch_persistent(reinterpret_cast<const void*>(&resident_decoder_kernel), dim3(RES_CUS), dim3(RES_THREADS),

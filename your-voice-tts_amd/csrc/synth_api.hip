@@ -229,8 +229,10 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     }
     s->steps.assign(B, 0);
     // batch 1: the postnet is enqueued behind the resident decoder launch before the host waits for
-    // it (device step counts, tiles sized for the step cap: the tiles past the sentence exit), so
-    // the device goes from the decoder to the postnet without waiting for the host to wake up
+    // it (device step counts; tiles sized for Tp = min(T, 1024) frames, the tiles past the sentence
+    // exit), so the device goes from the decoder to the postnet without waiting for the host to wake
+    // up.  Tp bounds the frames that run gives (the small-batch conv kernel's limit, independent of
+    // the step cap): a longer sentence is redone after the wait, like the speculative Griffin-Lim.
     const float* hist = nullptr;
     int64_t sent_floats = 0;
     const int* n_dev = nullptr;
@@ -240,6 +242,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     // Griffin-Lim too: sized for Ts = min(256, T) frames, reading the count the decoder's read-back
     // launch clamps into fspec (a longer sentence makes it an empty run, redone below)
     const int Ts = (int)std::min<size_t>(256, T);
+    const int Tp = (int)std::min<size_t>(1024, T);
     const bool spec_gl = B == 1 && s->r == 1 && wav_cap >= (int64_t)s->hop * (Ts - 1) &&
                          tts::gl_persistent_path(s->g, 1, Ts, Ts, gl_iters);
     struct Hook {
@@ -248,7 +251,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         int mel_tmax;
         const int* n_dev;
         float* post;
-        int T;
+        int T, Tp;
         tts_status st;
         bool spec_gl;
         int Ts;
@@ -257,10 +260,10 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         double* wav;
         hipStream_t cs;
         bool gl_done;
-    } hook{s, hist, (int)(sent_floats / s->nmel), n_dev, post, (int)T, TTS_OK, spec_gl, Ts, seed, gl_iters, wav, cs, false};
+    } hook{s, hist, (int)(sent_floats / s->nmel), n_dev, post, (int)T, Tp, TTS_OK, spec_gl, Ts, seed, gl_iters, wav, cs, false};
     auto hook_fn = [](void* c, hipStream_t q) {
         Hook* h = static_cast<Hook*>(c);
-        const int32_t Tcap[1] = {h->T};
+        const int32_t Tcap[1] = {h->Tp};
         h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
         if (h->st || !h->spec_gl) return;
         // Griffin-Lim writes the caller's waveform: after the caller's stream
@@ -306,7 +309,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     TTS_CHECK(Fmax >= 2, TTS_ERR_INVALID, "a sentence decoded to fewer than 2 frames");
     TTS_CHECK(wav_cap >= (int64_t)B * s->hop * (Fmax - 1), TTS_ERR_INVALID, "wav buffer too small");
     std::copy(h_frames, h_frames + B, frames);
-    const bool post_done = tts::decoder_hook_ran(s->d);
+    const bool post_done = tts::decoder_hook_ran(s->d) && Fmax <= Tp;
     const bool gl_done = post_done && hook.gl_done && Fmax <= Ts;
     tts::decoder_set_post_hook(s->d, nullptr, nullptr);
     if (!post_done) {

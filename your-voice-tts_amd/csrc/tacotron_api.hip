@@ -33,6 +33,7 @@
 #include "conv1d.h"
 #include "decoder.h"
 #include "sgemm.h"
+#include "resident.h"
 #include "tacotron.h"
 
 using namespace tts;
@@ -1084,8 +1085,14 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
         a.done = t->done; a.n_steps = t->n_steps;
         a.gran = t->tr_gran;
         a.status = reinterpret_cast<int*>(t->tr_gran + tres_granules());
-        t->res_salt = (t->res_salt + 1) & 0x3FFFF;
-        if (t->res_salt == 0) t->res_salt = 1;
+        {
+            // 18-bit tag salt: after a wrap a granule left by the launch 2^18 back could match a
+            // current wait (an XCD group a smaller batch left idle), so clear them on a wrap
+            bool wrapped = false;
+            t->res_salt = res_next_salt(t->res_salt, &wrapped);
+            if (wrapped)
+                TTS_HIP(hipMemsetAsync(t->tr_gran, 0, sizeof(unsigned long long) * (tres_granules() + 2), s));
+        }
         a.salt = t->res_salt;
         a.timeout_ticks = t->res_ticks;
         a.prof = nullptr;
@@ -1245,8 +1252,11 @@ tts_status tts_tacotron_resident_phases(tts_tacotron* t, float* us, int n) {
     tts_status st = enqueue_prenet_go(t, t->last_B, s);
     TResArgs a = t->last_ra;
     a.prof = prof;
-    t->res_salt = (t->res_salt + 1) & 0x3FFFF;
-    if (t->res_salt == 0) t->res_salt = 1;
+    {
+        bool wrapped = false;  // as in the decode path: clear the granules on a salt wrap
+        t->res_salt = res_next_salt(t->res_salt, &wrapped);
+        if (wrapped) TTS_HIP(hipMemsetAsync(t->tr_gran, 0, sizeof(unsigned long long) * (tres_granules() + 2), s));
+    }
     a.salt = t->res_salt;
     if (!st) {
         TTS_HIP(hipMemsetAsync(a.status, 0, sizeof(int), s));

@@ -232,6 +232,7 @@ class Tacotron2:
                           max_steps, cap, ctypes.c_void_p(mel.data_ptr()),
                           ctypes.c_void_p(stop.data_ptr()), ctypes.c_void_p(align.data_ptr()),
                           n_steps, stream), "tts_decoder_run")
+        self._dec_enc = enc  # a batch-1 run reads it in place; profile_step_kernels re-reads it
         steps = [int(n_steps[b]) for b in range(B)]
         for s in steps:
             if s >= max_steps:
@@ -394,6 +395,16 @@ class Tacotron2:
         k = len(self.RESIDENT_PHASES)
         return {"cu0": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[:k]])),
                 "attention_cu": dict(zip(self.RESIDENT_PHASES, [float(v) for v in us[k:]]))}
+
+    def profile_resident_trace(self):
+        """Per-CU event trace of the last resident sentence, re-run with event stamps only
+        (measurement only): int64 numpy [256 CU, 64 steps, 8 events] of wall-clock ticks (P1, B1,
+        h_att published, B3, B4, h_dec published, B6, pre1 row published; 0 = not reached)."""
+        lib, hdec, _ = self._handles(1, 1)
+        n = 256 * 64 * 8
+        buf = (ctypes.c_longlong * n)()
+        _native.check(lib.tts_decoder_resident_trace(hdec, buf, n), "tts_decoder_resident_trace")
+        return np.frombuffer(buf, dtype=np.int64).reshape(256, 64, 8).copy()
 
     def profile_step_kernels(self, reps=50):
         """Mean duration (ms) of each decoder-step kernel, HIP events on its own stream, for the
