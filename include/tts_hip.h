@@ -147,8 +147,9 @@ tts_status tts_decoder_last_path(tts_decoder* d, int* resident);
 #define TTS_RESIDENT_PHASES 16
 tts_status tts_decoder_resident_phases(tts_decoder* d, float* us, int n);
 // Measurement only: re-runs the last resident sentence with per-CU event stamps (no phase marks) and
-// returns n >= 256*64*8 wall-clock ticks [CU][step < 64][event]: P1, B1, h_att published, B3, B4,
-// h_dec published, B6, pre1 row published (0 = not reached).
+// returns n >= 256*64*12 wall-clock ticks [CU][step < 64][event]: P1, B1, h_att published, B3, B4,
+// h_dec published, B6, pre1 row published, query row published, and on the attention CUs A1 (query
+// gathered), A2 (candidate energies), context published (0 = not reached).
 tts_status tts_decoder_resident_trace(tts_decoder* d, long long* ticks, int64_t n);
 
 /* Measurement only (no reference counterpart): re-runs up to `reps` steps of the last

@@ -22,7 +22,7 @@ sys.path.insert(0, REPO)
 gu = importlib.import_module("your-voice-tts_amd.generic_utils")
 weights = importlib.import_module("your-voice-tts_amd.weights")
 
-EV = ("P1", "B1", "hatt_pub", "B3", "B4", "hdec_pub", "B6", "pre1_pub")
+EV = ("P1", "B1", "hatt_pub", "B3", "B4", "hdec_pub", "B6", "pre1_pub", "q_pub", "att_A1", "att_A2", "att_ctx_pub")
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=100)
@@ -47,8 +47,7 @@ for t in steps:
     period.append(tr[:, t + 1, 0].min() - t0)
     for k, name in enumerate(EV):
         v = tr[:, t, k]
-        if name == "pre1_pub":
-            v = v[v > 0]
+        v = v[v > 0]
         r = v - t0
         rel[name].append((r.min(), np.median(r), r.max()))
         if name in last:

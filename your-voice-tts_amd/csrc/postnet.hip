@@ -6,6 +6,7 @@
 
 #include <algorithm>
 
+#include <cstdlib>
 #include "conv1d.h"
 
 using namespace tts;
@@ -99,6 +100,16 @@ tts_status tts_postnet_run(tts_postnet* p, const float* mel, const int32_t* T, i
 }  // extern "C"
 
 namespace tts {
+namespace {
+__global__ void postnet_pad_kernel() {}
+bool pad_kernel() {  // TTS_PAD_KERNEL=1: a trivial launch after every layer (dispatch-position diagnostic)
+    static const bool on = [] {
+        const char* v = getenv("TTS_PAD_KERNEL");
+        return v && v[0] == '1';
+    }();
+    return on;
+}
+}  // namespace
 // tts_postnet_run, optionally with the frame counts already on the device (T_dev[b] * tmul frames:
 // the decoder's step counts) and the input rows mel_tmax frames apart (0 = Tmax): the synthesis
 // path feeds the decoder's mel history in place, with no copy and no host-to-device transfer.
@@ -152,6 +163,7 @@ tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const
         a.tickets = reinterpret_cast<int*>(p->part + CONV_SPLITK_FLOATS);
         a.Ttile = Tlong;
         TTS_HIP(conv_launch(a, 5, B, frames, s));
+        if (pad_kernel()) hipLaunchKernelGGL(postnet_pad_kernel, dim3(1), dim3(64), 0, s);  // measurement only
         in = a.out;
     }
     return TTS_OK;

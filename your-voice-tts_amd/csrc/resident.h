@@ -100,8 +100,9 @@ struct ResArgs {
 };
 constexpr int RES_PHASES = 16;
 // profiling re-run only: prof also holds [256 CU][RES_TRACE_STEPS][RES_TRACE_EV] event ticks
-// (P1, B1, h_att published, B3, B4, h_dec published, B6, pre1 row published)
-constexpr int RES_TRACE_STEPS = 64, RES_TRACE_EV = 8;
+// (P1, B1, h_att published, B3, B4, h_dec published, B6, pre1 row published, query row published;
+// attention CUs: A1 (query gathered), A2 (candidate energies), context published)
+constexpr int RES_TRACE_STEPS = 64, RES_TRACE_EV = 12;
 constexpr size_t RES_PROF_LL = 2 * RES_PHASES + (size_t)RES_CUS * RES_TRACE_STEPS * RES_TRACE_EV;
 
 // Pack the reference-layout weights (device pointers) into ResWeights (allocated by the caller,

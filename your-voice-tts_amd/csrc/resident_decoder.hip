@@ -467,12 +467,15 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             s = dot4(wq1, ld4(xh_att + qhalf * 512 + 256 + lane * 4), s);
             s = wave_sum_dpp(s);
             if (lane == 0) publish_xcd(Gq + (t & 1) * GR_TOTAL + 2 * qrow + qhalf, E + 3, s);
+            if (tid == 0) { RES_EV(t, 8) }
         }
-        // 6) decoder LSTM over h_att_t (its h_dec_{t-1} half ran at the loop top); on the attention
-        //    CU too, while the query is still in flight (after the attention step it would delay
-        //    that CU's h_dec publish, which every CU waits for)
+        // 6) decoder LSTM over h_att_t (its h_dec_{t-1} half ran at the loop top); the attention
+        //    CU does this after its attention step, which is on the critical path (there it runs
+        //    while the other CUs' context gather waits out the XCD-local edge)
+        if (!att_cu) {
 #pragma unroll 2
-        for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
+            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
+        }
         RES_MARK(5);
         // 7) attention step.  After the forward mask the previous alpha is nonzero only on the
         //    previous window S' = W(n') = {(n'-2) mod L} + [n'-1, n'+2], so every position outside
@@ -500,6 +503,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3); }
             }
             __syncthreads();  // A1
+            if (tid == 0) { RES_EV(t, 9) }
             if (flags[1]) break;
             RES_MARK(6);
             bool full = t == 0;
@@ -520,6 +524,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                     candv[sl] = v;
                 }
                 __syncthreads();  // A2
+                if (tid == 0) { RES_EV(t, 10) }
                 RES_MARK(14);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -603,6 +608,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (tid == 0) publish_xcd(Gc + (t & 1) * GR_TOTAL + ENC, E + 4, tail);
             xctx[tid] = ctx;  // this CU skips the gather
             if (tid == 0) xctx[ENC] = tail;
+            if (tid == 0) { RES_EV(t, 11) }
             RES_MARK(8);
             // off the critical path: this step's alpha (next step's prev_alpha) and alignment row
             const int j = tid;
@@ -610,7 +616,9 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (j < L) anew[j] = w;
             if (att_log && t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
             n_prev = n;
-            n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: loop top)
+            n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: h_att wait)
+#pragma unroll 2
+            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
             RES_MARK(9);
         }
         // this wave's prenet-1 row weights (step 11) from the XCD's L2, in flight while the context

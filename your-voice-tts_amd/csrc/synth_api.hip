@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -30,8 +31,8 @@ struct tts_synth {
     float *post[2] = {nullptr, nullptr}, *spec[2] = {nullptr, nullptr};
     size_t ids_n = 0, enc_n = 0, mel_n = 0, stop_n = 0, spec_n = 0;
     std::vector<int32_t> steps;
-    // encoder -> decoder -> postnet on `stream` (higher priority: its launches are latency-bound
-    // and leave most CUs idle), Griffin-Lim on `gl_stream`.  Neither front stage touches caller
+    // encoder -> decoder -> postnet on `stream`, Griffin-Lim on `gl_stream` (default priorities: see
+    // tts_synth_create).  Neither front stage touches caller
     // memory, so `stream` does not wait for the caller's; Griffin-Lim waits for the caller's
     // stream (it writes the caller's waveform buffer) and for the postnet, and the caller's stream
     // waits for Griffin-Lim.
@@ -89,8 +90,14 @@ tts_status tts_synth_create(tts_encoder* e, tts_decoder* d, tts_postnet* p, tts_
     s->r = r;
     s->nmel = n_mel;
     s->hop = hop;
+    // both streams at the default priority: with a high-priority front stream (round 3) every few
+    // launches after the resident decoder waited ~35 us for its waves to be dispatched (postnet
+    // layers, the Griffin-Lim magnitude / initial iSTFT / overlap-add / de-emphasis launches:
+    // +0.2 ms per configs[1] sentence; rocprofv3 SQ counters showed the same busy cycles at 3x the
+    // wall time).  TTS_STREAM_PRIO=1 restores the priorities (measurement only).
     int prio_lo = 0, prio_hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
+    if (const char* v = getenv("TTS_STREAM_PRIO"); v && v[0] == '1')
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_lo = prio_hi = 0;
     if (hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipStreamCreateWithPriority(&s->gl_stream, hipStreamNonBlocking, prio_lo) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming) != hipSuccess ||
@@ -266,8 +273,14 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         const int32_t Tcap[1] = {h->Tp};
         h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
         if (h->st || !h->spec_gl) return;
-        // Griffin-Lim writes the caller's waveform: after the caller's stream
-        if (hipEventRecord(h->s->ev_in, h->cs) != hipSuccess || hipStreamWaitEvent(q, h->s->ev_in, 0) != hipSuccess) {
+        // Griffin-Lim writes the caller's waveform: after the caller's stream (TTS_HOOK_NO_XWAIT=1:
+        // measurement only, for a caller whose stream is idle)
+        static const bool no_xwait = [] {
+            const char* v = getenv("TTS_HOOK_NO_XWAIT");
+            return v && v[0] == '1';
+        }();
+        if (!no_xwait &&
+            (hipEventRecord(h->s->ev_in, h->cs) != hipSuccess || hipStreamWaitEvent(q, h->s->ev_in, 0) != hipSuccess)) {
             h->st = TTS_ERR_HIP;
             tts::set_error("tts_synth_run: event hand-off failed");
             return;
@@ -286,7 +299,11 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         tts::encoder_set_defer_status(s->e, est != nullptr);
         tts::decoder_set_pipeline_io(s->d, tts::encoder_lens_buffer(s->e), est, ehost, spec_gl ? s->fspec : nullptr, Ts);
     }
-    tts::decoder_set_post_hook(s->d, B == 1 ? +hook_fn : nullptr, &hook);
+    static const bool no_hook = [] {  // measurement only: postnet and Griffin-Lim after the host's wait
+        const char* v = getenv("TTS_NO_HOOK");
+        return v && v[0] == '1';
+    }();
+    tts::decoder_set_post_hook(s->d, B == 1 && !no_hook ? +hook_fn : nullptr, &hook);
     for (int attempt = 0;; ++attempt) {
         if ((st = tts_encoder_run(s->e, ids_dev, h_lens, B, Lmax, enc, ss))) return st;
         // synchronises ss: the encoder's placement status is then readable

@@ -398,13 +398,14 @@ class Tacotron2:
 
     def profile_resident_trace(self):
         """Per-CU event trace of the last resident sentence, re-run with event stamps only
-        (measurement only): int64 numpy [256 CU, 64 steps, 8 events] of wall-clock ticks (P1, B1,
-        h_att published, B3, B4, h_dec published, B6, pre1 row published; 0 = not reached)."""
+        (measurement only): int64 numpy [256 CU, 64 steps, 12 events] of wall-clock ticks (P1, B1,
+        h_att published, B3, B4, h_dec published, B6, pre1 row published, query row published;
+        attention CUs: A1, A2, context published; 0 = not reached)."""
         lib, hdec, _ = self._handles(1, 1)
-        n = 256 * 64 * 8
+        n = 256 * 64 * 12
         buf = (ctypes.c_longlong * n)()
         _native.check(lib.tts_decoder_resident_trace(hdec, buf, n), "tts_decoder_resident_trace")
-        return np.frombuffer(buf, dtype=np.int64).reshape(256, 64, 8).copy()
+        return np.frombuffer(buf, dtype=np.int64).reshape(256, 64, 12).copy()
 
     def profile_step_kernels(self, reps=50):
         """Mean duration (ms) of each decoder-step kernel, HIP events on its own stream, for the
