@@ -106,8 +106,21 @@ struct Readback {
     const int* clamp_src;
     int* clamp_dst;
     int clamp_n, clamp_max;
+    int* seq_dst;  // pinned coherent host word written `seq` after every other word (release), or null
+    int seq;
 };
 hipError_t readback(const Readback& r, hipStream_t s);
+// Host wait for a pinned coherent word that a kernel on `s` sets to `want` with a system-scope release
+// (Readback::seq_dst, the Griffin-Lim overlap-add's status sequence): polled for up to TTS_SPIN_MS,
+// then the stream is synchronised.  Replaces an event record + query: each event marker in a stream
+// was measured to hold the GPU ~5.8 us between the kernels around it (round-4 kernel trace).
+hipError_t spin_word(const int* p, int want, hipStream_t s);
+// the device side of spin_word: thread 0 of the launch, after every thread's earlier stores
+__device__ __forceinline__ void release_word_system(int* p, int v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // A batch-1 sentence's ids (and its length) written to device arrays by one kernel whose argument
 // block carries them (runtime.hip), in place of two host-to-device copies: on this runtime a small
 // pageable-or-pinned H2D copy was measured to hold the host until its stream drained (~50 µs of

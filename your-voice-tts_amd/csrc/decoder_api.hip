@@ -67,7 +67,8 @@ struct tts_decoder {
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr;  // state: [2][2] = {step, n_active} per parity
     float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
-    int* host_flags = nullptr;  // pinned: [0, 4) flags, [4, 4 + 64) step counts (read-back target)
+    int* host_flags = nullptr;  // pinned coherent: [0, 3) flags, [3] read-back sequence, [4, 4 + 64) step counts
+    int rb_seq = 0;             // the resident run's read-back sequence number (host_flags[3])
     // tts_synth_run: work enqueued behind a resident launch before the host waits for it (the
     // postnet, reading the device step counts); hook_ran reports that it was enqueued
     void (*post_hook)(void*, hipStream_t) = nullptr;
@@ -351,7 +352,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         hipEventCreateWithFlags(&d->ev_t0, hipEventReleaseToDevice) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_t1, hipEventReleaseToDevice) != hipSuccess ||
         hipEventCreateWithFlags(&d->ev_sync, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), (4 + 64) * sizeof(int)) != hipSuccess) {
+        hipHostMalloc(reinterpret_cast<void**>(&d->host_flags), (4 + 64) * sizeof(int), hipHostMallocCoherent) != hipSuccess) {
         set_error("stream/event creation failed");
         return fail(TTS_ERR_HIP);
     }
@@ -719,6 +720,9 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     };
     int run = 0;  // steps enqueued; the next step has parity run & 1
     d->last_resident = 0;
+    // stage timers (tts_decoder_last_timing) outside pipeline mode only: every event marker holds
+    // the GPU ~5.8 us between the kernels around it
+    const bool timed = !d->pipeline;
     bool res_done = false;
     if (d->resident && B == 1 && lens[0] <= RES_LMAX) {
         // one persistent launch runs every step (resident.h); same state / history buffers
@@ -738,7 +742,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.salt = d->res_salt;
         d->last_ra = ra;
         if (!direct) TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
-        TTS_HIP(hipEventRecord(d->ev_t0, s));
+        if (timed) TTS_HIP(hipEventRecord(d->ev_t0, s));
         bool launched = false;
         TTS_HIP(launch_resident(ra, s, &launched));
         if (!launched) {
@@ -749,9 +753,11 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             TTS_HIP(launch_decoder_init(ia, s));
             if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
         } else {
-        TTS_HIP(hipEventRecord(d->ev_t1, s));
+        if (timed) TTS_HIP(hipEventRecord(d->ev_t1, s));
+        const int seq = ++d->rb_seq;
         {
-            // status, step counts (and the pipeline's extra word / GL clamp) in one launch
+            // status, step counts (and the pipeline's extra word / GL clamp) in one launch, then the
+            // sequence word the host polls
             Readback rb{};
             rb.src[0] = ra.status; rb.n[0] = 1; rb.dst[0] = d->host_flags;
             rb.src[1] = d->n_steps; rb.n[1] = B; rb.dst[1] = d->host_flags + 4;
@@ -760,16 +766,18 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             if (d->io_clamp) {
                 rb.clamp_src = d->n_steps; rb.clamp_dst = d->io_clamp; rb.clamp_n = B; rb.clamp_max = d->io_clamp_max;
             }
+            rb.seq_dst = d->host_flags + 3;
+            rb.seq = seq;
             TTS_HIP(readback(rb, s));
         }
-        // a polling wait on the event after the read-backs; work that needs no host-side step count
-        // (the synthesis postnet) is enqueued before it, so the device does not idle while the host wakes
-        TTS_HIP(hipEventRecord(d->ev_sync, s));
+        // a polling wait on the read-back's sequence word (no event marker); work that needs no
+        // host-side step count (the synthesis postnet, Griffin-Lim) is enqueued before it, so the
+        // device does not idle while the host wakes
         if (d->post_hook) {
             d->post_hook(d->post_ctx, s);
             d->hook_ran = true;
         }
-        TTS_HIP(spin_wait(d->ev_sync));
+        TTS_HIP(spin_word(d->host_flags + 3, seq, s));
         n_steps[0] = d->host_flags[4];
         if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
             // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
@@ -812,7 +820,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         it = d->graphs.emplace(key, g).first;
     }
     const Graphs& g = it->second;
-    TTS_HIP(hipEventRecord(d->ev_t0, s));
+    if (timed) TTS_HIP(hipEventRecord(d->ev_t0, s));
     auto launch_steps = [&](int n) -> tts_status {
         while (n > 0) {
             if ((run & 1) == 0 && n >= CHUNK) {
@@ -838,7 +846,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         st = launch_steps(CHUNK);
         if (st) return st;
     }
-    TTS_HIP(hipEventRecord(d->ev_t1, s));
+    if (timed) TTS_HIP(hipEventRecord(d->ev_t1, s));
     TTS_HIP(hipMemcpyAsync(d->host_flags + 4, d->n_steps, sizeof(int) * B, hipMemcpyDeviceToHost, s));
     if (d->io_rb_src) TTS_HIP(hipMemcpyAsync(d->io_rb_dst, d->io_rb_src, sizeof(int), hipMemcpyDeviceToHost, s));
     TTS_HIP(spin_sync(s, d->ev_sync));
@@ -862,7 +870,8 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         TTS_HIP(hipEventRecord(d->ev_out, s));
         TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
     }
-    TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
+    d->last_ms = 0.f;  // (pipeline mode: not timed)
+    if (timed) TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
     d->last_steps = run;
     d->last_B = B;
     d->last_Lmax = Lmax;

@@ -1198,6 +1198,8 @@ struct FinArgs {
     int64_t Nmax;
     const int* status;  // the persistent loop's status word, or null: nonzero poisons the signal (NaN)
     int* host_status;   // pinned host word the status is copied to by thread 0 of block (0, 0), or null
+    int* host_seq;      // ... then (pipeline mode) this pinned word is set to `seq` (release), or null
+    int seq;
     const float* wssp;  // [hop] float32 window sum-square of a sample whose every contributing frame
                         // exists, by (q - woff) mod hop (summed on the host in ola_sample's order)
 };
@@ -1208,8 +1210,10 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     const int Fb = a.F[b];
     const int N = a.g.hop * (Fb - 1);
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a.host_status && p == 0 && b == 0)  // the persistent loop's status, for the host's collect
+    if (a.host_status && p == 0 && b == 0) {  // the persistent loop's status, for the host's collect
         __hip_atomic_store(a.host_status, *a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.host_seq) release_word_system(a.host_seq, a.seq);
+    }
     if (p >= N) return;
     // a persistent loop whose hand-off wait timed out left frames unwritten: never hand out a
     // plausible-looking waveform for it (the run's error status is raised when it is collected)
@@ -1448,13 +1452,16 @@ struct tts_gl {
     pframe_t* pfr = nullptr;    // persistent loop: one frame slot per iteration
     size_t pfr_n = 0;
     int* pstatus = nullptr;     // [dev] status of the persistent loop
-    int* host_status = nullptr; // pinned
+    int* host_status = nullptr; // pinned coherent: [0] status of the last persistent loop, [1] its sequence
+    int seq = 0;                // pipeline mode: the sequence the last persistent run's overlap-add sets
+    hipStream_t seq_stream = nullptr;
     unsigned salt = 0;
     long long tmo = 0;
     bool have_last = false;
     IterArgs last_iter{};
     bool pipeline = false;        // tts_synth_run: caller's stream, completion collected later
     bool pending = false;         // a pipeline run whose timing / status is not collected yet
+    bool last_timed = true;       // the last run recorded its events (not in pipeline mode)
     FinArgs last_fin{};
     size_t last_fstride = 0;
 };
@@ -1577,7 +1584,7 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
         if ((e = hipMalloc(&g->pstatus, 16)) != hipSuccess) return fail(e, "hipMalloc");
         // (an empty speculative run leaves the word as it is: it must start out clean)
         if ((e = hipMemset(g->pstatus, 0, 16)) != hipSuccess) return fail(e, "hipMemset");
-        if ((e = hipHostMalloc(reinterpret_cast<void**>(&g->host_status), sizeof(int))) != hipSuccess)
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&g->host_status), 2 * sizeof(int), hipHostMallocCoherent)) != hipSuccess)
             return fail(e, "hipHostMalloc");
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256 &&
@@ -1609,8 +1616,13 @@ bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int 
 tts_status gl_collect(tts_gl* g) {
     if (!g->pending) return TTS_OK;
     g->pending = false;
-    TTS_HIP(hipEventSynchronize(g->ev_done));
-    TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
+    if (g->last_timed) {
+        TTS_HIP(hipEventSynchronize(g->ev_done));
+        TTS_HIP(hipEventElapsedTime(&g->last_ms, g->ev_t0, g->ev_t1));
+    } else if (g->last_persistent) {
+        // pipeline mode: no event markers; the overlap-add launch set the status, then the sequence
+        TTS_HIP(spin_word(g->host_status + 1, g->seq, g->seq_stream));
+    }
     if (g->last_persistent)
         TTS_CHECK(g->host_status[0] == 0, TTS_ERR_HIP, "persistent Griffin-Lim: a hand-off wait timed out (internal error)");
     return TTS_OK;
@@ -1770,7 +1782,10 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.zero_flags = nullptr;
     ia.zero_status = nullptr;
     TTS_HIP(hipGetLastError());
-    TTS_HIP(hipEventRecord(g->ev_t0, s));
+    // loop timers and the completion event outside pipeline mode only (each event marker holds the
+    // GPU ~5.8 us between the kernels around it); a pipeline run's status travels by sequence word
+    const bool timed = !g->pipeline;
+    if (timed) TTS_HIP(hipEventRecord(g->ev_t0, s));
     FinArgs fa{};
     fa.F = Fd;
     fa.Fmax = Fmax;
@@ -1876,14 +1891,20 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         }
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
-    TTS_HIP(hipEventRecord(g->ev_t1, s));
+    if (timed) TTS_HIP(hipEventRecord(g->ev_t1, s));
     fa.frames = persistent_ran ? static_cast<void*>(g->pfr + (size_t)iters * fstride) : slot(iters);
     fa.status = persistent_ran ? g->pstatus : nullptr;
     fa.host_status = persistent_ran ? g->host_status : nullptr;  // (no read-back copy launch)
+    if (persistent_ran && !timed) {
+        fa.host_seq = g->host_status + 1;
+        fa.seq = ++g->seq;
+        g->seq_stream = s;
+    }
     if (f64) hipLaunchKernelGGL(gl_ola_kernel<pframe_t>, ogrid, oblock, 0, s, fa);
     else hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, fa);
     fa.status = nullptr;
     fa.host_status = nullptr;
+    fa.host_seq = nullptr;
     TTS_HIP(hipGetLastError());
     {
         // de-emphasis chunks: each starts `look` samples early, |c|^look <= 1e-22; one chunk per
@@ -1903,8 +1924,13 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     g->last_persistent = persistent_ran;
     g->last_path = persistent_ran ? TTS_GL_PATH_PERSISTENT : fused ? TTS_GL_PATH_FUSED : TTS_GL_PATH_UNFUSED;
     g->last_launches = persistent_ran ? 1 : (fused ? 1 : 2) * iters;
-    TTS_HIP(hipEventRecord(g->ev_done, s));
-    if (s != cs) TTS_HIP(hipStreamWaitEvent(cs, g->ev_done, 0));
+    if (timed) {
+        TTS_HIP(hipEventRecord(g->ev_done, s));
+        if (s != cs) TTS_HIP(hipStreamWaitEvent(cs, g->ev_done, 0));
+    } else {
+        g->last_ms = 0.f;  // (pipeline mode: not timed)
+    }
+    g->last_timed = timed;
     g->pending = true;
     if (!g->pipeline) {
         tts_status cst = gl_collect(g);

@@ -123,6 +123,28 @@ __global__ void readback_kernel(const Readback r) {
             const int v = r.clamp_src[j];
             r.clamp_dst[j] = v >= 2 && v <= r.clamp_max ? v : 0;
         }
+    if (r.seq_dst) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's stores have landed
+        __syncthreads();
+        if (threadIdx.x == 0) release_word_system(r.seq_dst, r.seq);
+    }
+}
+
+hipError_t spin_word(const int* p, int want, hipStream_t s) {
+    static const long long spin_ns = [] {
+        const char* v = std::getenv("TTS_SPIN_MS");
+        return (long long)((v && v[0]) ? std::atof(v) * 1e6 : 200e6);
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned k = 0;; ++k) {
+        if (__atomic_load_n(p, __ATOMIC_ACQUIRE) == want) return hipSuccess;
+        if ((k & 63) == 63 &&
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count() > spin_ns)
+            break;
+    }
+    hipError_t e = hipStreamSynchronize(s);  // a long run (or a fault): block, then look again
+    if (e != hipSuccess) return e;
+    return __atomic_load_n(p, __ATOMIC_ACQUIRE) == want ? hipSuccess : hipErrorUnknown;
 }
 
 hipError_t readback(const Readback& r, hipStream_t s) {

@@ -273,13 +273,16 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
         const int32_t Tcap[1] = {h->Tp};
         h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
         if (h->st || !h->spec_gl) return;
-        // Griffin-Lim writes the caller's waveform: after the caller's stream (TTS_HOOK_NO_XWAIT=1:
-        // measurement only, for a caller whose stream is idle)
-        static const bool no_xwait = [] {
-            const char* v = getenv("TTS_HOOK_NO_XWAIT");
-            return v && v[0] == '1';
-        }();
-        if (!no_xwait &&
+        // Griffin-Lim writes the caller's waveform: after the caller's stream.  An idle caller stream
+        // needs no cross-stream wait (its marker would hold the GPU ~5.8 us before the first
+        // Griffin-Lim launch)
+        const hipError_t idle = hipStreamQuery(h->cs);
+        if (idle != hipSuccess && idle != hipErrorNotReady) {
+            h->st = TTS_ERR_HIP;
+            tts::set_error("tts_synth_run: caller stream query failed");
+            return;
+        }
+        if (idle == hipErrorNotReady &&
             (hipEventRecord(h->s->ev_in, h->cs) != hipSuccess || hipStreamWaitEvent(q, h->s->ev_in, 0) != hipSuccess)) {
             h->st = TTS_ERR_HIP;
             tts::set_error("tts_synth_run: event hand-off failed");
