@@ -211,6 +211,47 @@ def test_griffin_lim_batched_ragged_60_iters(audio_cfg):
         assert np.all(wav[b, n:] == 0)
 
 
+def device_phases(seed, F, nb=1025):
+    """numpy restatement of griffin_lim.hip hash_uniform (sentence 0): U[k, f] of the device phases."""
+    idx = (np.arange(nb, dtype=np.uint64)[:, None] * np.uint64(1048576) + np.arange(F, dtype=np.uint64)[None, :])
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * (idx + np.uint64(1))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def test_griffin_lim_configs1_persistent_vs_oracle(audio_cfg):
+    """the exact configs[1] Griffin-Lim — the reference's own mel_post of the L=100
+    sentence (T = 222 frames), 60 iterations, on the persistent loop — against the oracle's
+    inv_mel_spectrogram with the same phases."""
+    z = golden("t2_fwdmask_L100")
+    mel = z["mel_post"].astype(np.float32)
+    F = mel.shape[0]
+    assert F == 222
+    ap = load_pkg("audio").AudioProcessor(**audio_cfg)  # 60 iterations
+    pu = np.random.Generator(np.random.PCG64(11)).uniform(0, 1, size=(1, 1025, F))
+    wav = ap.griffin_lim_batch(torch.from_numpy(mel[None]).cuda(), [F], phase_u=pu).cpu().numpy()[0]
+    assert ap.last_gl_path() == "persistent"
+    ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(mel.T, pu[0])
+    assert rel_rms(wav, ref) < WAV_RTOL
+
+
+def test_synthesize_native_configs1_vs_oracle(audio_cfg):
+    """configs[1] end to end on the benched path (tts_synth_run: resident decoder, postnet and the
+    persistent Griffin-Lim enqueued behind it, device phases) against the oracle chain: the
+    reference's mel_post through inv_mel_spectrogram with the device's phases (hash restated)."""
+    z = golden("t2_fwdmask_L100")
+    m = _model(golden_flags(z))
+    ap = load_pkg("audio").AudioProcessor(**audio_cfg)
+    wav, frames = m.synthesize_native([z["ids"]], ap, seed=21)
+    F = z["mel"].shape[0]
+    assert frames == [F]
+    ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(z["mel_post"].T, device_phases(21, F))
+    assert rel_rms(wav.cpu().numpy()[0], ref) < WAV_RTOL
+
+
 def test_end_to_end_synthesis_vs_oracle(audio_cfg):
     """ids -> wav through the whole HIP path vs the oracle chain (L=12, 60 GL iterations)."""
     z = golden("t2_fwdmask_L12")

@@ -42,8 +42,19 @@ using namespace tts;
 namespace {
 
 typedef float spec_t;    // |S|^power storage
-typedef float frame_t;   // windowed iSTFT frame storage of the batched (unfused) loop
-typedef double pframe_t; // ... of the fused and persistent loops
+typedef float frame_t;   // windowed iSTFT frame storage (every loop: rounded once before librosa's
+                         // float32 overlap-add, which adds each float64 frame into a float32 signal)
+// the persistent loop's frame storage: one 8-byte granule per sample, {tag : 32 | float32 sample},
+// the tag naming the iteration that wrote it (round 4; replaces float64 slots + per-frame flags)
+struct gran_t {
+    unsigned long long v;
+};
+__device__ __forceinline__ double fval(float x) { return (double)x; }
+__device__ __forceinline__ double fval(gran_t x) { return (double)__uint_as_float((unsigned)x.v); }
+__device__ __forceinline__ void fstore(float* p, double v, unsigned) { *p = (float)v; }
+__device__ __forceinline__ void fstore(gran_t* p, double v, unsigned tag) {
+    p->v = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint((float)v);
+}
 
 constexpr int NFFT = 2048;
 constexpr int NB = 1025;  // bins
@@ -262,7 +273,7 @@ __device__ __forceinline__ float ola_sample(const FT* __restrict__ fr, int q, in
     float y = 0.f, wss = 0.f;
     for (int i = ilo; i <= ihi; ++i) {
         const int o = q - i * g.hop;  // offset inside frame i (0..2047)
-        y = (float)((double)y + (double)fr[(int64_t)i * g.winp + (o - g.fb)]);
+        y = (float)((double)y + fval(fr[(int64_t)i * g.winp + (o - g.fb)]));
         wss = (float)((double)wss + win2[o]);
     }
     return wss > 1.17549435e-38f ? y / wss : y;
@@ -285,7 +296,7 @@ __device__ __forceinline__ float ola_sample_unrolled(const FT* __restrict__ fr, 
         const int i = ilo + k;
         const int o = q - i * g.hop;
         const bool ok = i <= ihi;
-        fv[k] = ok ? (double)fr[(int64_t)i * g.winp + (o - g.fb)] : 0.0;
+        fv[k] = ok ? fval(fr[(int64_t)i * g.winp + (o - g.fb)]) : 0.0;
         wv[k] = ok ? win2[o] : 0.0;
     }
     float y = 0.f, wss = 0.f;
@@ -404,7 +415,7 @@ struct IterArgs {
     const float* y;       // [B][Nmax] the previous iteration's float32 signal (gl_ola_kernel)
     const void* prev;     // FUSED: the previous iteration's frames (overlap-added here instead)
     int64_t Nmax;
-    void* next;           // frames written by this iteration (frame_t or pframe_t: see the kernels)
+    void* next;           // frames written by this iteration (frame_t; gran_t for the initial iSTFT of the persistent loop)
     const int* F;
     int Fmax;
     int B;
@@ -417,6 +428,7 @@ struct IterArgs {
     const double2* wt;      // gl_iter_wave_kernel: [16][4] pass-2 twiddles
     const double2* winc;    // gl_iter_wave_kernel: [4][64] window cosine seeds (see tts_gl_create)
     double wrot;            // ... and the recurrence factor 2 cos(2 pi 128 / win)
+    unsigned gtag;          // initial iSTFT into granules (gran_t): the tag of iteration 0
 };
 
 __device__ __forceinline__ double hash_uniform(unsigned long long seed, unsigned long long idx) {
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i) - g.woff;
         const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-        if (n >= 0 && n < g.win) out[n + g.woff - g.fb] = (FT)(wo[i] * (zv * (1.0 / NH)));
+        if (n >= 0 && n < g.win) fstore(out + (n + g.woff - g.fb), wo[i] * (zv * (1.0 / NH)), a.gtag);
     }
 }
 
@@ -954,33 +966,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 }
 
 // ---------------------------------------------------------------- persistent GL loop (small batches)
-// Every GL iteration after the initial one, for all frames, in ONE launch: workgroup (sentence,
-// frame) keeps its iteration-invariant operands (|S| row, window, twiddles, and the overlap-add
-// geometry of its 2048 STFT input samples: contributor offsets and the window sum-square) in
-// registers, and per iteration
-//   waits until every frame it overlap-adds from has published the previous iteration (one
-//   tag word per frame, polled by one wave), overlap-adds its input samples from their frames
-//   (agent-scope loads: the data was written by other CUs in this launch), runs the same
-//   STFT -> S X/|X| -> iSTFT as gl_iter_kernel, stores its frame write-through (sc1) and, after
-//   every storing wave drained, publishes its tag.
-// Every iteration writes a frame slot of its own (never rewritten in the launch): with parity
-// ping-pong, a consumer on another XCD read its L2's copy of the line from two iterations before
-// (sc1 loads bypass L1 but are L2-served; an acquire only drops L1) -- measured nondeterministic
-// 1e-4..1e-2 rel RMS errors.  Every wait is bounded.
+// Every GL iteration after the initial one, for all frames (<= 256 in all), in ONE launch: one
+// workgroup per (sentence, frame) keeps its iteration-invariant operands (|S| row, window,
+// twiddles, and the overlap-add geometry of its 2048 STFT input samples: contributor offsets and
+// the window sum-square) in registers.  Frames are 8-byte granules {tag | float32 sample} (gran_t)
+// in two ping-pong slots: iteration it reads slot it & 1 (tag it), writes slot (it + 1) & 1.
+// Per iteration each thread re-reads the granules of its 8 input samples' <= 5 contributors until
+// every tag is the iteration's (the neighbour wait and the overlap-add loads are one), then
+// STFT -> S X/|X| -> iSTFT as gl_iter_kernel, and stores its frame's samples: no flag words, no
+// per-frame publish.  Overwriting slot (it + 1) & 1 is safe because the contributor relation is
+// symmetric (checked on the host for the geometry and frame count, gl_persistent_path): every
+// reader of this frame's iteration it - 1 output is one of its own contributors, whose iteration
+// it output this frame has read - so that reader has finished its iteration it - 1 gather.
+// Placement: every workgroup publishes its XCD; frames map to XCDs in contiguous runs over the
+// runtime placement.  A frame whose consumers (frames within 4; sentence edges excepted, where
+// the STFT's reflection reaches further) share its XCD stores with workgroup scope (the line stays
+// in that XCD's L2, where the consumers' sc1 loads read it); others write through (agent scope).
+// A stale copy of a cross-XCD granule carries an old tag and is read again.  Waits are bounded.
 struct PersArgs {
     IterArgs it;        // S, F, Fmax, B, geometry, constants (y / next / prev unused)
-    pframe_t* frames;   // [iters + 1][B][Fmax][winp]: iteration k reads slot k, writes slot k + 1
-    int64_t fstride;
+    gran_t* frames;     // [2][B][Fmax][winp]
+    int64_t fstride;    // granules per slot
     int iters;          // iterations after the initial one
-    int it0;            // first iteration index of this launch (parity of the frames it reads)
-    unsigned* flags;    // [B][Fmax] tag of the last iteration each frame published
-    unsigned salt;      // per launch (18 bits)
+    unsigned* xtab;     // [B][Fmax] each workgroup's XCD, salted (zeroed by the initial iSTFT)
+    unsigned salt;      // per launch (18 bits): tag(it) = salt << 14 | it
     long long tmo;      // wall_clock64 ticks per wait
     int* status;
     long long* prof;    // diagnostic (TTS_GL_PHASES): per-phase wall_clock64 ticks of frame prof_f, or null
     int prof_f;
     int drop_f;         // fault injection (tests, TTS_GL_INJECT_DROP): sentence 0's frame drop_f stops
-                        // after its first iteration without publishing (-1: none)
+                        // after its first iteration without storing it (-1: none)
 };
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned gu32_t;
@@ -990,16 +1005,69 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     const IterArgs& a = p.it;
     const int b = blockIdx.y;
     const int Fb = a.F[b];
-    // frames -> XCDs in contiguous runs over the sentence's own frame count rather than the grid's
-    // (a speculative batch-1 run sizes the grid as an upper bound): the placement of a grid of Fb
-    if ((int)blockIdx.x >= Fb) return;
-    const int f = xcd_remap(blockIdx.x, Fb);
+    if ((int)blockIdx.x >= Fb) return;  // (a speculative batch-1 run sizes the grid as an upper bound)
     const Geo g = a.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ __align__(16) double2 buf0[NH];
     __shared__ __align__(16) double2 buf1[NH];
     __shared__ __align__(16) double2 X[NB + 1];
-    __shared__ int rng[3];  // contributor frame range lo, hi; abort flag
+    __shared__ int sh[4];  // frame, local stores, abort
+    auto fail = [&](int code) {
+        __hip_atomic_store((gi32_t*)p.status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sh[2] = 1;
+    };
+    if (tid == 0) sh[2] = 0;
+    // ---- placement: frames -> XCDs in contiguous runs over where the workgroups actually run
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    unsigned* xt = p.xtab + (int64_t)b * a.Fmax;
+    if (tid == 0)
+        __hip_atomic_store((gu32_t*)(xt + blockIdx.x), (p.salt << 8) | (unsigned)xcc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) {
+        unsigned v[4];  // blocks 4 lane .. 4 lane + 3 (Fb <= 256)
+        long long t_end = 0;
+        bool ok = true;
+        for (int spin = 0;; ++spin) {
+            ok = true;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane * 4 + i;
+                v[i] = k < Fb ? __hip_atomic_load((gu32_t*)(xt + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                ok = ok && (k >= Fb || (v[i] >> 8) == p.salt);
+            }
+            if (__all(ok)) break;
+            if (spin == 0) {
+                t_end = (long long)wall_clock64() + p.tmo;
+            } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
+                break;
+            }
+        }
+        int base = 0, cnt = 0, rank = 0;
+        for (int x = 0; x < 8; ++x) {
+            int c = 0, r = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int k = lane * 4 + i;
+                const bool on = k < Fb && (int)(v[i] & 7) == x;
+                c += __popcll(__ballot(on));
+                r += __popcll(__ballot(on && k < (int)blockIdx.x));
+            }
+            if (x < xcc) base += c;
+            if (x == xcc) { cnt = c; rank = r; }
+        }
+        if (lane == 0) {
+            const int f = base + rank;
+            sh[0] = f;
+            sh[1] = f - 4 >= base && f + 4 < base + cnt && f >= 5 && f <= Fb - 6;
+            if (!__all(ok)) fail(2);
+        }
+    }
+    __syncthreads();
+    if (sh[2]) return;
+    const int f = sh[0];
+    const bool local = sh[1];
     constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;
     constexpr int PN = NFFT / GL_THREADS;
     // ---- iteration-invariant operands
@@ -1019,13 +1087,12 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         const int m = edge_sample(tid, i), n = m - g.woff;
         wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
     }
-    // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors (frame
-    // offsets into one parity's sentence block, -1 = none) and window sum-square, as ola_sample
+    // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors
+    // (granule offsets into one slot's sentence block, -1 = none) and window sum-square, as ola_sample
     const int N = g.hop * (Fb - 1);
     double wi[PN];
     int off[PN][OLA_MAX];
     float wssv[PN];
-    int flo = Fb, fhi = -1;
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i);
@@ -1045,22 +1112,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const bool ok = any && fi <= ihi;
             off[i][k] = ok ? fi * g.winp + (o - g.fb) : -1;
             wss = (float)((double)wss + (ok ? a.c.win2[o] : 0.0));
-            if (ok) { flo = min(flo, fi); fhi = max(fhi, fi); }
         }
         wssv[i] = wss;
     }
-    if (tid == 0) { rng[0] = Fb; rng[1] = -1; rng[2] = 0; }
-    __syncthreads();
-    if (fhi >= 0) { atomicMin(&rng[0], flo); atomicMax(&rng[1], fhi); }
-    __syncthreads();
-    const int clo = rng[0], chi = rng[1];
-    unsigned* flb = p.flags + (int64_t)b * a.Fmax;
-    if (tid == 0 && chi - clo >= 64) {  // wider than one polling wave (cannot happen for hop >= 64)
-        __hip_atomic_store((gi32_t*)p.status, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        rng[2] = 1;
-    }
-    __syncthreads();
-    if (rng[2]) return;
     const bool timed = p.prof && f == p.prof_f && b == 0 && tid == 0;
     long long ph[6] = {0, 0, 0, 0, 0, 0};
     long long tp = timed ? (long long)wall_clock64() : 0;
@@ -1070,60 +1124,54 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         ph[k] += tn - tp;                                \
         tp = tn;                                         \
     }
-    for (int it = p.it0; it < p.it0 + p.iters; ++it) {
-        const pframe_t* src = p.frames + it * p.fstride + (int64_t)b * a.Fmax * g.winp;
-        pframe_t* dst = p.frames + (it + 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
-        if (it > p.it0 && wave == 0) {
-            // the previous iteration of every contributor frame, one lane per frame: its tag is it
-            // or, when that frame already finished this iteration too, it + 1 (never further: the
-            // contributor relation is symmetric, so it waits for this frame before iteration it + 1)
-            const int fr = clo + lane;
+    const unsigned tag0 = p.salt << 14;
+    for (int it = 0; it < p.iters; ++it) {
+        const gran_t* src = p.frames + (it & 1) * p.fstride + (int64_t)b * a.Fmax * g.winp;
+        gran_t* dst = p.frames + ((it + 1) & 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
+        const unsigned want = tag0 | (unsigned)it;
+        // ---- gather: every contributor granule of the thread's 8 samples, read (all in flight at
+        // once; absent contributors read this frame's first granule and are masked) until every tag
+        // is this iteration's
+        float fv[PN][OLA_MAX];
+        {
             long long t_end = 0;
             for (int spin = 0;; ++spin) {
-                bool ok = fr > chi;
-                if (!ok) {
-                    const unsigned v =
-                        __hip_atomic_load((gu32_t*)(flb + fr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = (v >> 14) == p.salt && (int)(v & 0x3FFFu) >= it;
-                }
+                unsigned long long x[PN][OLA_MAX];
+#pragma unroll
+                for (int i = 0; i < PN; ++i)
+#pragma unroll
+                    for (int k = 0; k < OLA_MAX; ++k)
+                        x[i][k] = __hip_atomic_load((gu64_t*)&src[off[i][k] >= 0 ? off[i][k] : 0].v, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                bool ok = true;
+#pragma unroll
+                for (int i = 0; i < PN; ++i)
+#pragma unroll
+                    for (int k = 0; k < OLA_MAX; ++k) {
+                        ok = ok && (off[i][k] < 0 || (unsigned)(x[i][k] >> 32) == want);
+                        fv[i][k] = __uint_as_float((unsigned)x[i][k]);
+                    }
                 if (__all(ok)) break;
                 if (spin == 0) {
                     t_end = (long long)wall_clock64() + p.tmo;
                 } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
-                    if (lane == 0) {
-                        __hip_atomic_store((gi32_t*)p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        rng[2] = 1;
-                    }
+                    if (lane == 0) fail(1);
                     break;
                 }
                 if (GLP_SLEEP) __builtin_amdgcn_s_sleep(GLP_SLEEP);
             }
-#if GL_ACQUIRE
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
         }
-        __syncthreads();
-        if (rng[2]) return;
+        __syncthreads();  // every wave's gather (or a timeout) before the FFT's LDS passes
+        if (sh[2]) return;
         GL_PHASE(0)
-        // ---- overlap-add of the input samples (frames written by other CUs: agent-scope loads),
-        // straight into the first butterfly's registers
+        // ---- overlap-add sums (librosa istft: float64 contributions into a float32 signal, frame
+        // order) straight into the first butterfly's registers
         double2 v[4];
-        // every contributor load of the thread's 8 samples is issued before the first sum (one
-        // memory round trip per iteration instead of one per sample; absent contributors load
-        // slot 0 of this frame's block and are masked to exact zeros)
-        double fv[PN][OLA_MAX];
-#pragma unroll
-        for (int i = 0; i < PN; ++i)
-#pragma unroll
-            for (int k = 0; k < OLA_MAX; ++k)
-                fv[i][k] = __longlong_as_double((long long)__hip_atomic_load(
-                    (gu64_t*)(src + (off[i][k] >= 0 ? off[i][k] : 0)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             float y = 0.f;
 #pragma unroll
-            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (off[i][k] >= 0 ? fv[i][k] : 0.0));
+            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (off[i][k] >= 0 ? (double)fv[i][k] : 0.0));
             const float yv = wssv[i] > 1.17549435e-38f ? y / wssv[i] : y;
             if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
             else v[i >> 1].x = wi[i] * (double)yv;
@@ -1165,21 +1213,22 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         }
         fft1024_regs<true, true>(v, buf0, buf1, ftw);
         GL_PHASE(4)
+        if (b == 0 && f == p.drop_f) return;  // fault injection only: never stores iteration 1
+        // ---- the frame's samples, tagged with the next iteration: XCD-local (workgroup-scope store,
+        // the line stays in the XCD's L2) when every consumer shares this XCD, else written through
+        const unsigned nt = tag0 | (unsigned)(it + 1);
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             const int n = edge_sample(tid, i) - g.woff;
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-            if (n >= 0 && n < g.win)
-                __hip_atomic_store((gu64_t*)(dst + n + g.woff - g.fb),
-                                   (unsigned long long)__double_as_longlong(wo[i] * (zv * (1.0 / NH))),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long gv = ((unsigned long long)nt << 32) |
+                                          (unsigned long long)__float_as_uint((float)(wo[i] * (zv * (1.0 / NH))));
+            gu64_t* q = (gu64_t*)&dst[n + g.woff - g.fb].v;
+            if (n >= 0 && n < g.win) {
+                if (local) __hip_atomic_store(q, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else __hip_atomic_store(q, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-        __syncthreads();  // ... before one lane signals; the LDS buffers are reused next iteration
-        if (b == 0 && f == p.drop_f) return;  // fault injection only: never publishes
-        if (tid == 0)
-            __hip_atomic_store((gu32_t*)(flb + f), (p.salt << 14) | (unsigned)(it + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
         GL_PHASE(5)
     }
 #undef GL_PHASE
@@ -1187,9 +1236,16 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         for (int k = 0; k < 6; ++k) p.prof[k] = ph[k];
 }
 
+// the initial iSTFT's granules (slot 0) as float32 frames for the fused loop, when the persistent
+// launch could not be placed
+__global__ void gl_gran_to_frames_kernel(const gran_t* in, float* out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = __uint_as_float((unsigned)in[i].v);
+}
+
 // ---------------------------------------------------------------- final OLA + inverse pre-emphasis
 struct FinArgs {
-    const void* frames;  // frame_t (batched loop) or pframe_t (fused / persistent): gl_ola_kernel<FT>
+    const void* frames;  // frame_t (fused / batched loops) or gran_t (persistent): gl_ola_kernel<FT>
     const int* F;
     int Fmax, B;
     Geo g;
@@ -1236,7 +1292,7 @@ __global__ void gl_ola_kernel(const FinArgs a) {
 #pragma unroll
         for (int k = 0; k < OLA_MAX; ++k) {
             const int i = ilo + k;
-            fv[k] = i <= ihi ? (double)fr[(int64_t)i * g.winp + (q - i * g.hop - g.fb)] : 0.0;
+            fv[k] = i <= ihi ? fval(fr[(int64_t)i * g.winp + (q - i * g.hop - g.fb)]) : 0.0;
         }
         float y = 0.f, wss = 0.f;
 #pragma unroll
@@ -1436,7 +1492,7 @@ struct tts_gl {
     // workspace
     size_t S_n = 0, fr_n = 0, y_n = 0;
     spec_t* S = nullptr;
-    void* frames = nullptr;  // frame_t or pframe_t slots (sized for pframe_t)
+    void* frames = nullptr;  // frame_t ping-pong slots
     float* y = nullptr;
     int* F = nullptr;
     int Fcap_B = 0;
@@ -1444,13 +1500,12 @@ struct tts_gl {
     float last_ms = 0.f;
     int last_launches = 0;
     bool last_fused = false;
-    bool last_f64 = false;  // the last run stored its frames float64
     bool last_persistent = false;
     int last_path = TTS_GL_PATH_UNFUSED;
-    unsigned* flags = nullptr;  // persistent loop: [flags_n] tags
+    unsigned* flags = nullptr;  // persistent loop: [flags_n] the workgroups' XCD table
     size_t flags_n = 0;
-    pframe_t* pfr = nullptr;    // persistent loop: one frame slot per iteration
-    size_t pfr_n = 0;
+    gran_t* pgr = nullptr;      // persistent loop: two granule slots
+    size_t pgr_n = 0;
     int* pstatus = nullptr;     // [dev] status of the persistent loop
     int* host_status = nullptr; // pinned coherent: [0] status of the last persistent loop, [1] its sequence
     int seq = 0;                // pipeline mode: the sequence the last persistent run's overlap-add sets
@@ -1474,7 +1529,7 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
-                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pfr, (void*)g->wt, (void*)g->winc,
+                    (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pgr, (void*)g->wt, (void*)g->winc,
                     (void*)g->wssp})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
@@ -1609,8 +1664,48 @@ static bool gl_fused_path(const tts_gl* g, int B, int Fmax) {
     const char* fz = getenv("TTS_GL_FUSED");
     return ((int64_t)B * Fmax <= 1024 || (fz && fz[0] == '1')) && (g->g.win + g->g.hop - 1) / g->g.hop <= OLA_MAX;
 }
+// The persistent loop overwrites a frame's ping-pong slot once its own contributors have moved on:
+// safe when every reader of a frame is one of its contributors.  Frame f reads the signal at the
+// reflected positions R(W_f), W_f = [f hop - win/2, f hop + win/2) (centred STFT frames), and its
+// contributors are the frames fi whose windows W_fi hold one of them.  While one reflection
+// suffices (win/2 < hop (F - 1)), R maps the part of W_f outside [0, N) into W_f's own part inside,
+// so R(W_f) = W_f n [0, N) and "f reads fi" <=> W_f n W_fi n [0, N) != {} is symmetric.  Shorter
+// sentences are checked by brute force (host copy of the kernels' index maps).
+static int reflect_host(int p, int N) {
+    if ((unsigned)p < (unsigned)N) return p;
+    if (N == 1) return 0;
+    const int period = 2 * (N - 1);
+    int pp = p % period;
+    if (pp < 0) pp += period;
+    return pp < N ? pp : period - pp;
+}
+static bool contrib_symmetric(const Geo& g, int F) {
+    if (2 * g.hop * (F - 1) > g.win + 2) return true;
+    const int N = g.hop * (F - 1);
+    std::vector<char> c((size_t)F * F, 0);
+    for (int f = 0; f < F; ++f)
+        for (int n = g.woff; n < g.woff + g.win; ++n) {
+            const int q = reflect_host(f * g.hop + n - NFFT / 2, N) + NFFT / 2;
+            if (q < g.woff) continue;
+            int ilo = q - g.woff - g.win + 1;
+            ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
+            const int ihi = std::min((q - g.woff) / g.hop, F - 1);
+            for (int fi = ilo; fi <= ihi; ++fi) c[(size_t)f * F + fi] = 1;
+        }
+    for (int f = 0; f < F; ++f)
+        for (int fi = 0; fi < F; ++fi)
+            if (c[(size_t)f * F + fi] != c[(size_t)fi * F + f]) return false;
+    return true;
+}
 bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters) {
-    return gl_fused_path(g, B, Fmax) && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT");
+    if (!(gl_fused_path(g, B, Fmax) && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT")))
+        return false;
+    // every frame count the run may have (a speculative run knows only the upper bound Fmax)
+    for (int F = 2; F <= Fmax; ++F) {
+        if (2 * g->g.hop * (F - 1) > g->g.win + 2) break;  // symmetric from here on (above)
+        if (!contrib_symmetric(g->g, F)) return false;
+    }
+    return true;
 }
 
 tts_status gl_collect(tts_gl* g) {
@@ -1676,7 +1771,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     if (!g->pipeline) TTS_HIP(hipStreamSynchronize(s));
     tts_status st;
     if ((st = grow(reinterpret_cast<void**>(&g->S), g->S_n, needS, sizeof(spec_t)))) return st;
-    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, sizeof(pframe_t)))) return st;
+    if ((st = grow(reinterpret_cast<void**>(&g->frames), g->fr_n, needF, sizeof(frame_t)))) return st;
     if ((st = grow(reinterpret_cast<void**>(&g->y), g->y_n, needY, 4))) return st;
     if (B > g->Fcap_B) {
         if (g->F) TTS_HIP(hipFree(g->F));
@@ -1727,28 +1822,25 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                        0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
-    // the persistent loop (one workgroup per frame) writes every iteration to slots of its own: a
-    // frame slot is never rewritten inside the launch, so no XCD's L2 can hold an earlier copy of
-    // the bytes an iteration reads (TTS_GL_FUSED=1 forces the fused form at any batch: measurement knob)
-    // frame storage: float64 for the small-batch fused / persistent loops, float32 for the batched
-    // loop and for the forced fused form (TTS_GL_FUSED=1, whose waveform the tests compare bitwise
-    // with the batched loop's)
-    const bool f64 = fused && !(fz && fz[0] == '1');
-    if (persistent) {
-        const size_t need = fstride * (size_t)(iters + 1);
-        if (need > g->pfr_n) {
-            if (g->pfr) TTS_HIP(hipFree(g->pfr));
-            g->pfr = nullptr;
-            TTS_HIP(hipMalloc(&g->pfr, need * sizeof(pframe_t)));
-            g->pfr_n = need;
+    // the persistent loop reads and writes two slots of tagged granules (gl_persistent_kernel);
+    // the other loops two slots of float32 frames (TTS_GL_FUSED=1 forces the fused form at any
+    // batch: measurement knob)
+    if (persistent && 2 * fstride > g->pgr_n) {
+        if (g->pgr) TTS_HIP(hipFree(g->pgr));
+        g->pgr = nullptr;
+        TTS_HIP(hipMalloc(&g->pgr, 2 * fstride * sizeof(gran_t)));
+        g->pgr_n = 2 * fstride;
+    }
+    // frame slot i of the two ping-pong slots of the fused / batched loops
+    auto slot = [&](int i) -> void* { return static_cast<frame_t*>(g->frames) + (i & 1) * fstride; };
+    if (persistent) {  // the initial iSTFT tags its granules with the launch's salt
+        g->salt = (g->salt + 1) & 0x3FFFF;
+        if (g->salt == 0) {
+            // wrapped: a granule of the launch 2^18 back could carry a current tag
+            g->salt = 1;
+            TTS_HIP(hipMemsetAsync(g->pgr, 0, g->pgr_n * sizeof(gran_t), s));
         }
     }
-    void* const fr0 = persistent ? static_cast<void*>(g->pfr) : g->frames;
-    // frame slot i of the two ping-pong slots, in the loop's storage type
-    auto slot = [&](int i) -> void* {
-        return f64 ? static_cast<void*>(static_cast<pframe_t*>(g->frames) + (i & 1) * fstride)
-                   : static_cast<void*>(static_cast<frame_t*>(g->frames) + (i & 1) * fstride);
-    };
     IterArgs ia{};
     ia.S = g->S;
     ia.F = Fd;
@@ -1760,10 +1852,11 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ia.seed = seed;
     ia.y = g->y;
     ia.Nmax = Nmax;
-    ia.next = fr0;
+    ia.next = persistent ? static_cast<void*>(g->pgr) : slot(0);
     ia.wt = g->wt;
     ia.winc = g->winc;
     ia.wrot = g->wrot;
+    ia.gtag = g->salt << 14;
     if (persistent) {
         if ((size_t)B * Fmax > g->flags_n) {
             if (g->flags) TTS_HIP(hipFree(g->flags));
@@ -1771,13 +1864,13 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             TTS_HIP(hipMalloc(&g->flags, sizeof(unsigned) * (size_t)B * Fmax));
             g->flags_n = (size_t)B * Fmax;
         }
-        // tags are salted per handle, and a new handle can get a freed one's flag words: the
+        // table entries are salted per launch, and a new handle can get a freed one's words: the
         // initial iSTFT launch zeroes them and the status word
         ia.zero_flags = g->flags;
         ia.zero_status = g->pstatus;
     }
     const dim3 grid(Fmax, B), block(GL_THREADS);
-    if (f64) hipLaunchKernelGGL((gl_iter_kernel<true, false, pframe_t>), grid, block, 0, s, ia);
+    if (persistent) hipLaunchKernelGGL((gl_iter_kernel<true, false, gran_t>), grid, block, 0, s, ia);
     else hipLaunchKernelGGL((gl_iter_kernel<true, false, frame_t>), grid, block, 0, s, ia);
     ia.zero_flags = nullptr;
     ia.zero_status = nullptr;
@@ -1800,11 +1893,10 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     if (persistent) {
         PersArgs pa{};
         pa.it = ia;
-        pa.frames = g->pfr;
+        pa.frames = g->pgr;
         pa.fstride = (int64_t)fstride;
         pa.iters = iters;
-        pa.flags = g->flags;
-        g->salt = (g->salt + 1) & 0x3FFFF;
+        pa.xtab = g->flags;
         pa.salt = g->salt;
         pa.tmo = g->tmo;
         pa.status = g->pstatus;
@@ -1824,8 +1916,10 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(launch_persistent(reinterpret_cast<const void*>(&gl_persistent_kernel), grid, block, kargs, 0, s,
                                   &persistent_ran));
         if (!persistent_ran) {
-            // the initial iSTFT wrote slot 0 of the persistent frame buffer: hand it to the fused loop
-            TTS_HIP(hipMemcpyAsync(g->frames, g->pfr, fstride * sizeof(pframe_t), hipMemcpyDeviceToDevice, s));
+            // the initial iSTFT wrote slot 0 of the granule buffer: hand it to the fused loop
+            hipLaunchKernelGGL(gl_gran_to_frames_kernel, dim3((unsigned)((fstride + 255) / 256)), dim3(256), 0, s,
+                               g->pgr, static_cast<frame_t*>(g->frames), (int64_t)fstride);
+            TTS_HIP(hipGetLastError());
             if (prof) {
                 TTS_HIP(hipStreamSynchronize(s));
                 TTS_HIP(hipFree(prof));
@@ -1840,7 +1934,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             int rate_khz = 100000, dev = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev);
-            static const char* names[6] = {"wait", "ola_loads", "fwd_fft", "spectrum", "inv_fft", "store_publish"};
+            static const char* names[6] = {"gather", "ola_sums", "fwd_fft", "spectrum", "inv_fft", "store"};
             fprintf(stderr, "TTS_GL_PHASES frame %d, us per iteration:", pa.prof_f);
             for (int k = 0; k < 6; ++k) fprintf(stderr, " %s %.3f", names[k], h[k] * 1e3 / rate_khz / iters);
             fprintf(stderr, "\n");
@@ -1868,8 +1962,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                 a.next = slot(i + 1);
                 if (fused) {
                     a.prev = slot(i);
-                    if (f64) hipLaunchKernelGGL((gl_iter_kernel<false, true, pframe_t>), grid, block, 0, s, a);
-                    else hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
+                    hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
                 } else {
                     FinArgs o = fa;
                     o.frames = slot(i);
@@ -1892,7 +1985,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipGraphLaunch(it->second, s));
     }
     if (timed) TTS_HIP(hipEventRecord(g->ev_t1, s));
-    fa.frames = persistent_ran ? static_cast<void*>(g->pfr + (size_t)iters * fstride) : slot(iters);
+    fa.frames = persistent_ran ? static_cast<void*>(g->pgr + (size_t)(iters & 1) * fstride) : slot(iters);
     fa.status = persistent_ran ? g->pstatus : nullptr;
     fa.host_status = persistent_ran ? g->host_status : nullptr;  // (no read-back copy launch)
     if (persistent_ran && !timed) {
@@ -1900,7 +1993,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         fa.seq = ++g->seq;
         g->seq_stream = s;
     }
-    if (f64) hipLaunchKernelGGL(gl_ola_kernel<pframe_t>, ogrid, oblock, 0, s, fa);
+    if (persistent_ran) hipLaunchKernelGGL(gl_ola_kernel<gran_t>, ogrid, oblock, 0, s, fa);
     else hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, fa);
     fa.status = nullptr;
     fa.host_status = nullptr;
@@ -1937,7 +2030,6 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         if (cst) return cst;
     }
     g->last_fused = fused;
-    g->last_f64 = f64;
     g->have_last = true;
     g->last_iter = ia;
     g->last_fin = fa;
@@ -1965,7 +2057,7 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
     for (int r = 0; r < reps; ++r) {
         // one GL iteration as tts_gl_run launches it: overlap-add -> per-frame STFT/iSTFT
         FinArgs f = g->last_fin;
-        const size_t es = g->last_f64 ? sizeof(pframe_t) : sizeof(frame_t);
+        const size_t es = sizeof(frame_t);
         f.frames = static_cast<char*>(g->frames) + (r & 1) * g->last_fstride * es;
         IterArgs a = ia;
         a.phase_u = nullptr;
@@ -1976,9 +2068,7 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
             hipLaunchKernelGGL(gl_ola_kernel<frame_t>, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[1], s));
-        if (g->last_fused && g->last_f64)
-            hipLaunchKernelGGL((gl_iter_kernel<false, true, pframe_t>), grid, block, 0, s, a);
-        else if (g->last_fused)
+        if (g->last_fused)
             hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
         else if (g->wave)
             hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
