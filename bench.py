@@ -218,6 +218,54 @@ def _threads():
         return 1
 
 
+def _physical_cores():
+    """(threads, how): physical cores this process may use — distinct (package, core) pairs of its
+    CPU affinity set, capped by the cgroup CPU quota and by OMP_NUM_THREADS (the GPU box sets it to
+    its per-GPU CPU share)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except Exception:
+        cpus = list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    n = len(cores)
+    how = [f"{n} physical cores in the affinity set ({len(cpus)} logical)"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            lim = max(1, int(int(q) / int(per)))
+            how.append(f"cgroup quota {lim} CPUs")
+            n = min(n, lim)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        how.append(f"OMP_NUM_THREADS={omp}")
+        n = min(n, int(omp))
+    return max(1, n), "; ".join(how)
+
+
+def _port_over_reference():
+    """The committed CPU port vs reference timing (tools/cpu_port_vs_reference.py, build container:
+    the reference cannot run on the GPU box)."""
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "cpu_port_vs_reference_r*.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        out = {f"model_{k}": round(v["port_over_reference"], 3) for k, v in d.get("model", {}).items()}
+        if "griffin_lim" in d:
+            out["griffin_lim_60"] = round(d["griffin_lim"]["port_over_reference"], 3)
+        out["source"] = os.path.relpath(p, REPO) + " (" + d.get("cpu_model", "?") + ")"
+        return out
+    return None
+
+
 def cpu_baseline_gst(args):
     """Oracle TacotronGST (fp32) + linear GL (fp64) on the host for ONE config-5 sentence (sentence 0:
     its L, speaker 0, style mel 0), full 500-step cap and 60 GL iterations."""
@@ -245,43 +293,59 @@ def cpu_baseline_gst(args):
 
 
 def cpu_baseline(args, seconds_target=12.0):
-    """Oracle (numpy restatement of the reference path) on the host: decoder + postnet + GL."""
+    """The reference's CPU path restated on the host: torch-CPU decoder + postnet
+    (oracle/tacotron2_torch.py, the reference's op order on the same torch CPU kernels) on the
+    process's physical cores + the numpy Griffin-Lim restatement (fp64, scipy.fftpack,
+    single-threaded like librosa's)."""
     from oracle.griffin_lim_oracle import AudioOracle
-    from oracle.tacotron2_oracle import Tacotron2Oracle
+    from oracle.tacotron2_torch import Tacotron2TorchCPU
     if args.model == "gst":
         return cpu_baseline_gst(args)
-    threads = _threads()
+    threads, how = _physical_cores()
     cfg = gu.default_config("config_tacotron2.json")
-    o = Tacotron2Oracle(weights.tacotron2_weights(0), dtype=np.float32, attn_norm=cfg.attention_norm,
-                        forward_attn=cfg.use_forward_attn, trans_agent=cfg.transition_agent,
-                        forward_attn_mask=True, location_attn=cfg.location_attn, attn_win=cfg.windowing)
+    o = Tacotron2TorchCPU(weights.tacotron2_weights(0), attn_norm=cfg.attention_norm,
+                          forward_attn=cfg.use_forward_attn, trans_agent=cfg.transition_agent,
+                          forward_attn_mask=True, location_attn=cfg.location_attn, attn_win=cfg.windowing)
     ap = AudioOracle(**{**cfg.audio, "griffin_lim_iters": args.iters})
     ids = weights.synthetic_ids(args.L, 1)
-    frames = 0
-    n = 0
-    t0 = time.time()
-    while True:
-        res = o.inference(ids)
-        np.random.seed(n)
-        ap.inv_mel_spectrogram(res["mel_post"].T)
-        frames += res["mel"].shape[0]
-        n += 1
-        if time.time() - t0 >= seconds_target or n >= 8:
-            break
-    dt = time.time() - t0
-    # configs[0]: the reference's own CPU case, synthesize.py with 30-iteration Griffin-Lim, one sentence
-    ap30 = AudioOracle(**{**cfg.audio, "griffin_lim_iters": 30})
-    t1 = time.time()
-    r30 = o.inference(ids)
-    np.random.seed(0)
-    ap30.inv_mel_spectrogram(r30["mel_post"].T)
-    d30 = time.time() - t1
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        o.inference(ids)  # warm (allocator, BLAS thread pool)
+        frames = 0
+        n = 0
+        t_model = 0.0
+        t0 = time.time()
+        while True:
+            tm = time.time()
+            res = o.inference(ids)
+            t_model += time.time() - tm
+            np.random.seed(n)
+            ap.inv_mel_spectrogram(res["mel_post"].T)
+            frames += res["mel"].shape[0]
+            n += 1
+            if time.time() - t0 >= seconds_target or n >= 8:
+                break
+        dt = time.time() - t0
+        # configs[0]: the reference's own CPU case, synthesize.py with 30-iteration Griffin-Lim, one sentence
+        ap30 = AudioOracle(**{**cfg.audio, "griffin_lim_iters": 30})
+        t1 = time.time()
+        r30 = o.inference(ids)
+        np.random.seed(0)
+        ap30.inv_mel_spectrogram(r30["mel_post"].T)
+        d30 = time.time() - t1
+    finally:
+        torch.set_num_threads(prev_threads)
     T30 = r30["mel"].shape[0]
+    T = res["mel"].shape[0]
     return dict(value=frames / dt, unit="mel-frames/s", cores=int(threads), kind="port",
-                sample=f"{n} x one L={args.L} sentence ({res['mel'].shape[0]} frames): numpy oracle decoder+postnet "
-                       f"(fp32, BLAS on {threads} threads) + GL {args.iters} iters (fp64, scipy.fftpack, "
-                       f"single-threaded) on the host, {dt:.1f} s",
-                rtf=dt / (n * 275 * (res["mel"].shape[0] - 1) / 22050.0), cpu_model=_cpu_model(),
+                cores_how=how,
+                sample=f"{n} x one L={args.L} sentence ({T} frames): torch-CPU restatement decoder+postnet "
+                       f"(fp32, {threads} threads, {t_model / n:.3f} s/sentence) + GL {args.iters} iters (fp64, "
+                       f"scipy.fftpack, single-threaded) on the host, {dt:.1f} s",
+                model_half_frames_per_s=frames / t_model,
+                port_over_reference=_port_over_reference(),
+                rtf=dt / (n * 275 * (T - 1) / 22050.0), cpu_model=_cpu_model(),
                 configs0=dict(value=T30 / d30, unit="mel-frames/s", seconds=d30, rtf=d30 / (275 * (T30 - 1) / 22050.0),
                               sample=f"configs[0]: one L={args.L} sentence ({T30} frames), GL 30 iters, same port"))
 

@@ -192,3 +192,23 @@ def _t2_batch(max_batch):
                      trans_agent=fl["trans_agent"], forward_attn_mask=fl["forward_attn_mask"],
                      location_attn=fl["location_attn"], max_batch=max_batch)
     return m.cuda().eval()
+
+
+def test_persistent_griffin_lim_fresh_handles_ignore_freed_granules(audio_cfg):
+    """Short-lived handles in sequence (the allocator hands a new handle the freed granule buffer of
+    the last one, and every handle's tag salts start at 1): each persistent run, at 2 and at 3
+    iterations, is bitwise the fused loop on the same input."""
+    audio = load_pkg("audio")
+    rng = np.random.Generator(np.random.PCG64(5))
+    for k, iters in enumerate([2, 2, 3, 2, 3, 2]):
+        mel = torch.from_numpy(rng.uniform(0, 1, size=(1, 100, 80)).astype(np.float32)).cuda()
+        pu = rng.uniform(0, 1, size=(1, 1025, 100))
+        ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": iters})
+        a = ap.griffin_lim_batch(mel, [100], phase_u=pu)
+        assert ap.last_gl_path() == "persistent"
+        with _env(TTS_RESIDENT="0"):
+            b = ap.griffin_lim_batch(mel, [100], phase_u=pu)
+            assert ap.last_gl_path() == "fused"
+        assert torch.equal(a, b), k
+        del ap
+        torch.cuda.synchronize()

@@ -7,8 +7,9 @@ Build container only (imports /root/reference; nothing here runs on the GPU box)
 configs[1]'s model half: one L=100 sentence (ids seed 1, generator weights seed 0,
 config_tacotron2.json + forward_attn_mask) through the reference ``Tacotron2.inference`` (imported
 with the text front-end stubbed, as tests/golden/make_golden.py does) and through the oracle's
-``Tacotron2Oracle.inference`` (float32), at 8 threads and at 1 thread (torch.set_num_threads for the
-reference, threadpoolctl's BLAS limit for the port).  Griffin-Lim half: the reference
+torch-CPU restatement ``Tacotron2TorchCPU.inference`` (bench.py's cpu_baseline model half), plus the
+numpy ``Tacotron2Oracle.inference`` (float32) for the record, at 8 threads and at 1 thread
+(torch.set_num_threads, and threadpoolctl's BLAS limit for numpy).  Griffin-Lim half: the reference
 ``AudioProcessor.inv_mel_spectrogram`` with librosa replaced by the oracle's restatement (librosa
 is absent here) against ``AudioOracle.inv_mel_spectrogram``, 60 iterations, on the reference's own
 mel_post, same initial phases.  Medians of several runs; the ratio port / reference is what
@@ -32,6 +33,7 @@ import make_golden as mg  # noqa: E402  (stubs + weights loader; generates nothi
 from conftest import golden, golden_flags, tacotron2_config  # noqa: E402
 from oracle.griffin_lim_oracle import AudioOracle  # noqa: E402
 from oracle.tacotron2_oracle import Tacotron2Oracle  # noqa: E402
+from oracle.tacotron2_torch import Tacotron2TorchCPU  # noqa: E402
 
 
 def median_time(fn, reps):
@@ -64,7 +66,8 @@ def main(out_path):
     ids = mg.weights.synthetic_ids(100, 1)
     x = torch.from_numpy(ids).unsqueeze(0)
     fl = golden_flags(golden("t2_fwdmask_L100"))
-    port = Tacotron2Oracle(sd, dtype=np.float32, **fl)
+    port = Tacotron2TorchCPU(sd, **fl)
+    port_np = Tacotron2Oracle(sd, dtype=np.float32, **fl)
 
     res = {"workload": "configs[1] model half: Tacotron2 inference, one L=100 sentence (222 frames)",
            "cpu_model": _cpu_model(), "model": {}, "griffin_lim": {}}
@@ -79,10 +82,12 @@ def main(out_path):
         with threadpool_limits(limits=threads, user_api="blas"):
             tr, _ = median_time(ref_run, 5 if threads > 1 else 3)
             tp, _ = median_time(lambda: port.inference(ids), 5 if threads > 1 else 3)
+            tn, _ = median_time(lambda: port_np.inference(ids), 3)
         if mel_post is None:
             mel_post = ref_run()[1][0].numpy()
-        res["model"][f"threads_{threads}"] = dict(reference_s=tr, port_s=tp, port_over_reference=tp / tr)
-        print(threads, "threads: reference", tr, "port", tp, "ratio", tp / tr, flush=True)
+        res["model"][f"threads_{threads}"] = dict(reference_s=tr, port_s=tp, port_over_reference=tp / tr,
+                                                  numpy_oracle_s=tn, numpy_over_reference=tn / tr)
+        print(threads, "threads: reference", tr, "torch port", tp, "ratio", tp / tr, "numpy", tn, flush=True)
 
     # Griffin-Lim 60: reference AudioProcessor glue (librosa = the restatement) vs AudioOracle
     a = dict(tacotron2_config()["audio"])
@@ -121,4 +126,4 @@ def _cpu_model():
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "cpu_port_vs_reference_r03.json"))
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "cpu_port_vs_reference_r04.json"))

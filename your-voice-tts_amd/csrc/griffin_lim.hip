@@ -1698,7 +1698,9 @@ static bool contrib_symmetric(const Geo& g, int F) {
     return true;
 }
 bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters) {
-    if (!(gl_fused_path(g, B, Fmax) && iters > 0 && frames_total <= 256 && g->tmo > 0 && !getenv_off("TTS_RESIDENT")))
+    // (tags hold the iteration in 14 bits below the salt)
+    if (!(gl_fused_path(g, B, Fmax) && iters > 0 && iters < (1 << 14) && frames_total <= 256 && g->tmo > 0 &&
+          !getenv_off("TTS_RESIDENT")))
         return false;
     // every frame count the run may have (a speculative run knows only the upper bound Fmax)
     for (int F = 2; F <= Fmax; ++F) {
@@ -1830,6 +1832,9 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         g->pgr = nullptr;
         TTS_HIP(hipMalloc(&g->pgr, 2 * fstride * sizeof(gran_t)));
         g->pgr_n = 2 * fstride;
+        // fresh memory may hold a freed handle's granules, and every handle's salts start at 1: a
+        // stale granule there can carry a tag this handle is about to wait for
+        TTS_HIP(hipMemsetAsync(g->pgr, 0, g->pgr_n * sizeof(gran_t), s));
     }
     // frame slot i of the two ping-pong slots of the fused / batched loops
     auto slot = [&](int i) -> void* { return static_cast<frame_t*>(g->frames) + (i & 1) * fstride; };
