@@ -71,7 +71,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                       bool F_bound = false);
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 // whether gl_run_dev takes the persistent loop for this shape (host values only)
-bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters);
+bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters);  // (caches per-F checks in g)
 
 // Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent
 // Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This checks

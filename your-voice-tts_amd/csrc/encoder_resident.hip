@@ -57,6 +57,21 @@ __device__ __forceinline__ bool sweep4(u64* g, unsigned tag, float (&v)[4], long
         if (ENC_SLEEP) __builtin_amdgcn_s_sleep(ENC_SLEEP);
     }
 }
+// one lane polls the 16-byte granule pair `pair` (granules 2 pair, 2 pair + 1 of rsrc r) until
+// both tags match (sc1 | volatile buffer loads: L1 bypass, re-issued every poll)
+typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bool sweep_pair(__amdgpu_buffer_rsrc_t r, int pair, unsigned tag, float (&v)[2], long long tmo) {
+    long long t_end = 0;
+    for (int spin = 0;; ++spin) {
+        const u32x4_ x = __builtin_bit_cast(u32x4_, __builtin_amdgcn_raw_buffer_load_b128(r, pair * 16, 0, (int)0x80000010u));
+        v[0] = __uint_as_float(x.x);
+        v[1] = __uint_as_float(x.z);
+        if (__all(x.y == tag && x.w == tag)) return true;
+        if (spin == 0) t_end = (long long)wall_clock64() + tmo;
+        else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) return false;
+        if (ENC_SLEEP) __builtin_amdgcn_s_sleep(ENC_SLEEP);
+    }
+}
 __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
     acc = fmaf(w.x, x.x, acc);
     acc = fmaf(w.y, x.y, acc);
@@ -120,6 +135,8 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         return a.xi[(int64_t)pos * (2 * G4) + dir * G4 + gate * H + unit];
     };
     float xcur = L > 0 ? xi_at(0) : 0.f;
+    // the h granules [2 parity][2 dir][256] as 16-byte pairs (buffer loads, sc1)
+    const auto gr = __builtin_amdgcn_make_buffer_rsrc(a.gran + GR_H, (short)0, 2 * 2 * H * 8, 0x00020000);
     __syncthreads();
     for (int s = 0; s < L; ++s) {
         const float xnext = s + 1 < L ? xi_at(s + 1) : 0.f;  // in flight during this step
@@ -146,15 +163,18 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
             a.out[(int64_t)pos * (2 * H) + dir * H + unit] = h;
         }
         xcur = xnext;
-        if (wave == 0) {
-            float v[4];
-            const bool ok = sweep4(gh, (a.salt << 14) | (unsigned)(s + 1), v, a.tmo);
+        if (wave < 2) {
+            // the direction's 256 h values: one 16-byte granule pair per lane on waves 0 and 1
+            // (one load instruction per poll instead of four on one wave)
+            float v[2];
+            const int pr = wave * 64 + lane;
+            const bool ok = sweep_pair(gr, ((par * 2 + dir) * H) / 2 + pr, (a.salt << 14) | (unsigned)(s + 1), v, a.tmo);
             if (!ok) {
                 if (lane == 0)
                     __hip_atomic_store((gint*)a.status, (int)((a.salt << 8) | 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 info[3] = 1;
             }
-            *reinterpret_cast<float4*>(hsb[(s + 1) & 1] + lane * 4) = float4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<float2*>(hsb[(s + 1) & 1] + pr * 2) = float2{v[0], v[1]};
         }
         __syncthreads();
         if (info[3] == 1) return;

@@ -994,9 +994,18 @@ struct PersArgs {
     int* status;
     long long* prof;    // diagnostic (TTS_GL_PHASES): per-phase wall_clock64 ticks of frame prof_f, or null
     int prof_f;
+    int nowait;         // measurement only (TTS_GL_NOWAIT=1): one gather sweep, tags unchecked (wrong results)
     int drop_f;         // fault injection (tests, TTS_GL_INJECT_DROP): sentence 0's frame drop_f stops
                         // after its first iteration without storing it (-1: none)
 };
+constexpr int GL_SC1_VOLATILE = (int)0x80000010u;  // buffer aux: sc1 (bit 4) | volatile (bit 31)
+constexpr int GL_OOB_OFF = 0x7FFFFFF0;               // past every granule buffer: reads 0, no access
+constexpr int GL_DMAX = 4;                            // overlap-add contributors lie within 4 frames
+constexpr int GL_SLOTS = 2 * GL_DMAX + 1;              // gather buffer slots (frames f-4 .. f+4)
+constexpr int GL_PAIRS = 9;                            // granule pairs per thread (<= 2304 per frame:
+                                                       // 2216 at most for n_fft 2048 / win 1102 / hop 275)
+// fill word of a fresh (or salt-wrapped) granule buffer, every dword: tag 1 = salt 0, never a live tag
+constexpr unsigned GL_GRAN_FILL = 1u;
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned gu32_t;
 typedef __attribute__((address_space(1))) int gi32_t;
@@ -1072,7 +1081,6 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     constexpr int PN = NFFT / GL_THREADS;
     // ---- iteration-invariant operands
     const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
-    const FftTw ftw = load_fft_tw(a.c.tw);
     double2 tk[PK];
     double sk[PK];
 #pragma unroll
@@ -1087,9 +1095,20 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         const int m = edge_sample(tid, i), n = m - g.woff;
         wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
     }
-    // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors
-    // (granule offsets into one slot's sentence block, -1 = none) and window sum-square, as ola_sample
+    // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors and
+    // window sum-square, as ola_sample.  A contributor is an index into the gather buffer og: slot
+    // s = fi - f + GL_DMAX holds frame fi's granule values (every contributor lies within GL_DMAX
+    // frames, reflection included: checked here), index og_zero a 0.0 for absent ones.
     const int N = g.hop * (Fb - 1);
+    extern __shared__ __align__(16) float og[];  // [GL_SLOTS][winp] + 2
+    const int og_zero = GL_SLOTS * g.winp;
+    __shared__ int rlo[GL_SLOTS], rhi[GL_SLOTS], rpre[GL_SLOTS + 1];
+    if (tid < GL_SLOTS) {
+        rlo[tid] = 0x7FFFFFFF;
+        rhi[tid] = -1;
+    }
+    if (tid < 2) og[og_zero + tid] = 0.f;
+    __syncthreads();
     double wi[PN];
     int off[PN][OLA_MAX];
     float wssv[PN];
@@ -1110,10 +1129,57 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const int fi = ilo + k;
             const int o = q - fi * g.hop;
             const bool ok = any && fi <= ihi;
-            off[i][k] = ok ? fi * g.winp + (o - g.fb) : -1;
+            const int sl = fi - f + GL_DMAX, gg = o - g.fb;
+            if (ok && (sl < 0 || sl >= GL_SLOTS)) fail(4);  // (never: contributors are within GL_DMAX)
+            const bool in = ok && sl >= 0 && sl < GL_SLOTS;
+            off[i][k] = in ? sl * g.winp + gg : og_zero;
+            if (in) {
+                atomicMin(&rlo[sl], gg);
+                atomicMax(&rhi[sl], gg);
+            }
             wss = (float)((double)wss + (ok ? a.c.win2[o] : 0.0));
         }
-        wssv[i] = wss;
+        // (a sample whose sum-square is below FLT_MIN keeps its sum undivided: y / 1.0f == y)
+        wssv[i] = wss > 1.17549435e-38f ? wss : 1.0f;
+    }
+    // The gather's loads: slot s needs granules [rlo, rhi] of frame f + s - GL_DMAX, read as
+    // 16-byte-aligned pairs (winp is a multiple of 4: granule pairs start at even indices); pair u of
+    // the workgroup goes to thread u % 256 (at most GL_PAIRS per thread).  gdst: LDS index | need
+    // bits (bit 30: the pair's first granule is needed, bit 31: its second); pairs past the list
+    // read out of range (zeros, to the zero word).
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int sl = 0; sl < GL_SLOTS; ++sl) {
+            rpre[sl] = acc;
+            acc += rhi[sl] >= 0 ? (rhi[sl] - (rlo[sl] & ~1)) / 2 + 1 : 0;
+        }
+        rpre[GL_SLOTS] = acc;
+        if (acc > GL_PAIRS * GL_THREADS) fail(5);
+    }
+    __syncthreads();
+    int goff[GL_PAIRS];
+    unsigned gdst[GL_PAIRS];
+#pragma unroll
+    for (int m = 0; m < GL_PAIRS; ++m) {
+        const int u = tid + m * GL_THREADS;
+        goff[m] = GL_OOB_OFF;
+        gdst[m] = (unsigned)og_zero;
+        if (u < rpre[GL_SLOTS]) {
+            int sl = 0;
+            while (u >= rpre[sl + 1]) ++sl;
+            const int g0 = (rlo[sl] & ~1) + 2 * (u - rpre[sl]);
+            goff[m] = ((f + sl - GL_DMAX) * g.winp + g0) * 8;
+            gdst[m] = (unsigned)(sl * g.winp + g0) | (g0 >= rlo[sl] ? 1u << 30 : 0u) | (g0 + 1 <= rhi[sl] ? 1u << 31 : 0u);
+        }
+    }
+    // byte offset of output sample i's granule in the frame slot; samples outside the window
+    // support take an out-of-range offset (the buffer store drops them)
+    int soff[PN];
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+        const int n = edge_sample(tid, i) - g.woff;
+        soff[i] = n >= 0 && n < g.win ? (n + g.woff - g.fb) * 8 : GL_OOB_OFF;
     }
     const bool timed = p.prof && f == p.prof_f && b == 0 && tid == 0;
     long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -1129,29 +1195,21 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         const gran_t* src = p.frames + (it & 1) * p.fstride + (int64_t)b * a.Fmax * g.winp;
         gran_t* dst = p.frames + ((it + 1) & 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
         const unsigned want = tag0 | (unsigned)it;
-        // ---- gather: every contributor granule of the thread's 8 samples, read (all in flight at
-        // once; absent contributors read this frame's first granule and are masked) until every tag
-        // is this iteration's
-        float fv[PN][OLA_MAX];
+        // ---- gather: the workgroup's granule pairs (each thread <= GL_PAIRS 16-byte sc1 loads, all in
+        // flight at once), re-read until every needed tag is this iteration's, then into LDS
         {
+            const auto rG = buf_rsrc(src, (unsigned)(a.Fmax * g.winp * 8));
             long long t_end = 0;
+            u32x4 x[GL_PAIRS];
             for (int spin = 0;; ++spin) {
-                unsigned long long x[PN][OLA_MAX];
 #pragma unroll
-                for (int i = 0; i < PN; ++i)
-#pragma unroll
-                    for (int k = 0; k < OLA_MAX; ++k)
-                        x[i][k] = __hip_atomic_load((gu64_t*)&src[off[i][k] >= 0 ? off[i][k] : 0].v, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
+                for (int m = 0; m < GL_PAIRS; ++m)
+                    x[m] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rG, goff[m], 0, GL_SC1_VOLATILE));
                 bool ok = true;
 #pragma unroll
-                for (int i = 0; i < PN; ++i)
-#pragma unroll
-                    for (int k = 0; k < OLA_MAX; ++k) {
-                        ok = ok && (off[i][k] < 0 || (unsigned)(x[i][k] >> 32) == want);
-                        fv[i][k] = __uint_as_float((unsigned)x[i][k]);
-                    }
-                if (__all(ok)) break;
+                for (int m = 0; m < GL_PAIRS; ++m)
+                    ok = ok && (!(gdst[m] & (1u << 30)) || x[m].y == want) && (!(gdst[m] & (1u << 31)) || x[m].w == want);
+                if (__all(ok) || p.nowait) break;
                 if (spin == 0) {
                     t_end = (long long)wall_clock64() + p.tmo;
                 } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
@@ -1160,8 +1218,14 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
                 }
                 if (GLP_SLEEP) __builtin_amdgcn_s_sleep(GLP_SLEEP);
             }
+            // (unneeded granules of a pair land on LDS words no sum reads; out-of-range pairs write
+            // zeros to the zero word)
+#pragma unroll
+            for (int m = 0; m < GL_PAIRS; ++m)
+                *reinterpret_cast<float2*>(og + (gdst[m] & 0x3FFFFFFFu)) =
+                    float2{__uint_as_float(x[m].x), __uint_as_float(x[m].z)};
         }
-        __syncthreads();  // every wave's gather (or a timeout) before the FFT's LDS passes
+        __syncthreads();  // the gather buffer (or a timeout) before the sums and the FFT's LDS passes
         if (sh[2]) return;
         GL_PHASE(0)
         // ---- overlap-add sums (librosa istft: float64 contributions into a float32 signal, frame
@@ -1169,15 +1233,17 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         double2 v[4];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
+            // (absent contributors read the zero word: adding +0.0 leaves the sum bitwise unchanged,
+            // which is never -0.0)
             float y = 0.f;
 #pragma unroll
-            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (off[i][k] >= 0 ? (double)fv[i][k] : 0.0));
-            const float yv = wssv[i] > 1.17549435e-38f ? y / wssv[i] : y;
+            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (double)og[off[i][k]]);
+            const float yv = y / wssv[i];
             if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
             else v[i >> 1].x = wi[i] * (double)yv;
         }
         GL_PHASE(1)
-        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
+        const double2* Z = fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw);
         GL_PHASE(2)
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
@@ -1211,23 +1277,20 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double2 O = cmul(D, cconj(tk[i]));
             v[i] = double2{E.x - O.y, E.y + O.x};
         }
-        fft1024_regs<true, true>(v, buf0, buf1, ftw);
+        fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
         GL_PHASE(4)
         if (b == 0 && f == p.drop_f) return;  // fault injection only: never stores iteration 1
         // ---- the frame's samples, tagged with the next iteration: XCD-local (workgroup-scope store,
         // the line stays in the XCD's L2) when every consumer shares this XCD, else written through
         const unsigned nt = tag0 | (unsigned)(it + 1);
+        const auto rD = buf_rsrc(dst, (unsigned)g.winp * 8);
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
-            const int n = edge_sample(tid, i) - g.woff;
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-            const unsigned long long gv = ((unsigned long long)nt << 32) |
-                                          (unsigned long long)__float_as_uint((float)(wo[i] * (zv * (1.0 / NH))));
-            gu64_t* q = (gu64_t*)&dst[n + g.woff - g.fb].v;
-            if (n >= 0 && n < g.win) {
-                if (local) __hip_atomic_store(q, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else __hip_atomic_store(q, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            const u32x2 gv = u32x2{__float_as_uint((float)(wo[i] * (zv * (1.0 / NH)))), nt};
+            // plain (workgroup-scope) store: the line stays in this XCD's L2; sc1: written through
+            if (local) __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0x10);
         }
         GL_PHASE(5)
     }
@@ -1506,6 +1569,7 @@ struct tts_gl {
     size_t flags_n = 0;
     gran_t* pgr = nullptr;      // persistent loop: two granule slots
     size_t pgr_n = 0;
+    std::vector<signed char> gather_fit;  // by frame count: the persistent gather's layout holds (-1: unknown)
     int* pstatus = nullptr;     // [dev] status of the persistent loop
     int* host_status = nullptr; // pinned coherent: [0] status of the last persistent loop, [1] its sequence
     int seq = 0;                // pipeline mode: the sequence the last persistent run's overlap-add sets
@@ -1697,7 +1761,47 @@ static bool contrib_symmetric(const Geo& g, int F) {
             if (c[(size_t)f * F + fi] != c[(size_t)fi * F + f]) return false;
     return true;
 }
-bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int iters) {
+// The persistent loop's gather layout for a sentence of F frames (gl_persistent_kernel): every
+// overlap-add contributor within GL_DMAX frames and at most GL_PAIRS granule pairs per thread.  Only
+// frames whose STFT window reaches a sentence edge (reflection) differ from the interior ones: those
+// and one interior frame are checked, restating the kernel's index arithmetic.
+static bool gather_fits(const Geo& g, int F) {
+    const int N = g.hop * (F - 1);
+    auto frame_ok = [&](int f) {
+        int lo[GL_SLOTS], hi[GL_SLOTS];
+        for (int k = 0; k < GL_SLOTS; ++k) {
+            lo[k] = 1 << 30;
+            hi[k] = -1;
+        }
+        for (int n = g.woff; n < g.woff + g.win; ++n) {
+            const int q = reflect_host(f * g.hop + n - NFFT / 2, N) + NFFT / 2;
+            if (q < g.woff) continue;
+            int ilo = q - g.woff - g.win + 1;
+            ilo = ilo <= 0 ? 0 : (ilo + g.hop - 1) / g.hop;
+            const int ihi = std::min((q - g.woff) / g.hop, F - 1);
+            for (int fi = ilo; fi <= ihi; ++fi) {
+                const int sl = fi - f + GL_DMAX;
+                if (sl < 0 || sl >= GL_SLOTS || fi - ilo >= OLA_MAX) return false;
+                lo[sl] = std::min(lo[sl], q - fi * g.hop - g.fb);
+                hi[sl] = std::max(hi[sl], q - fi * g.hop - g.fb);
+            }
+        }
+        int pairs = 0;
+        for (int k = 0; k < GL_SLOTS; ++k)
+            if (hi[k] >= 0) pairs += (hi[k] - (lo[k] & ~1)) / 2 + 1;
+        return pairs <= GL_PAIRS * GL_THREADS;
+    };
+    bool interior_done = false;
+    for (int f = 0; f < F; ++f) {
+        const bool edge = f * g.hop + g.woff - NFFT / 2 < 0 || f * g.hop + g.woff + g.win - 1 - NFFT / 2 >= N;
+        if (!edge && interior_done) continue;
+        if (!frame_ok(f)) return false;
+        if (!edge) interior_done = true;
+    }
+    return (g.winp % 2) == 0;
+}
+
+bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters) {
     // (tags hold the iteration in 14 bits below the salt)
     if (!(gl_fused_path(g, B, Fmax) && iters > 0 && iters < (1 << 14) && frames_total <= 256 && g->tmo > 0 &&
           !getenv_off("TTS_RESIDENT")))
@@ -1706,6 +1810,11 @@ bool gl_persistent_path(const tts_gl* g, int B, int Fmax, int frames_total, int 
     for (int F = 2; F <= Fmax; ++F) {
         if (2 * g->g.hop * (F - 1) > g->g.win + 2) break;  // symmetric from here on (above)
         if (!contrib_symmetric(g->g, F)) return false;
+    }
+    if ((int)g->gather_fit.size() <= Fmax) g->gather_fit.resize(Fmax + 1, -1);
+    for (int F = 2; F <= Fmax; ++F) {
+        if (g->gather_fit[F] < 0) g->gather_fit[F] = gather_fits(g->g, F) ? 1 : 0;
+        if (!g->gather_fit[F]) return false;
     }
     return true;
 }
@@ -1833,8 +1942,9 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipMalloc(&g->pgr, 2 * fstride * sizeof(gran_t)));
         g->pgr_n = 2 * fstride;
         // fresh memory may hold a freed handle's granules, and every handle's salts start at 1: a
-        // stale granule there can carry a tag this handle is about to wait for
-        TTS_HIP(hipMemsetAsync(g->pgr, 0, g->pgr_n * sizeof(gran_t), s));
+        // stale granule there can carry a tag this handle is about to wait for.  Filled with a word
+        // that is no live tag and not 0 (0 marks an absent contributor: gl_persistent_kernel)
+        TTS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->pgr), GL_GRAN_FILL, g->pgr_n * 2, s));
     }
     // frame slot i of the two ping-pong slots of the fused / batched loops
     auto slot = [&](int i) -> void* { return static_cast<frame_t*>(g->frames) + (i & 1) * fstride; };
@@ -1843,7 +1953,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         if (g->salt == 0) {
             // wrapped: a granule of the launch 2^18 back could carry a current tag
             g->salt = 1;
-            TTS_HIP(hipMemsetAsync(g->pgr, 0, g->pgr_n * sizeof(gran_t), s));
+            TTS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->pgr), GL_GRAN_FILL, g->pgr_n * 2, s));
         }
     }
     IterArgs ia{};
@@ -1907,6 +2017,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         pa.status = g->pstatus;
         pa.drop_f = -1;
         if (const char* inj = getenv("TTS_GL_INJECT_DROP"); inj && inj[0]) pa.drop_f = atoi(inj);
+        pa.nowait = getenv("TTS_GL_NOWAIT") != nullptr;
         long long* prof = nullptr;
         const char* phases = getenv("TTS_GL_PHASES");
         if (phases && phases[0]) {  // diagnostic: phase ticks of frame TTS_GL_PHASES (stderr)
@@ -1918,7 +2029,13 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         // every workgroup waits on its neighbours inside the launch: co-residency guaranteed, or
         // nothing runs and the fused loop below takes the iterations (bitwise the same waveform)
         void* kargs[] = {&pa};
-        TTS_HIP(launch_persistent(reinterpret_cast<const void*>(&gl_persistent_kernel), grid, block, kargs, 0, s,
+        // dynamic LDS: the gather buffer, GL_SLOTS frame slots + the zero word
+        const size_t og_bytes = ((size_t)GL_SLOTS * geo.winp + 2) * sizeof(float);
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gl_persistent_kernel),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        TTS_HIP(attr);
+        TTS_CHECK(og_bytes <= 96 * 1024, TTS_ERR_INVALID, "persistent Griffin-Lim: window too long for the gather buffer");
+        TTS_HIP(launch_persistent(reinterpret_cast<const void*>(&gl_persistent_kernel), grid, block, kargs, og_bytes, s,
                                   &persistent_ran));
         if (!persistent_ran) {
             // the initial iSTFT wrote slot 0 of the granule buffer: hand it to the fused loop
