@@ -87,6 +87,8 @@ __device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx
 // within a half (MI355X_MICROARCH.md "Valid forms", R2's granule); both tags are checked.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int SC1_VOLATILE = (int)0x80000010u;  // buffer aux: sc1 (bit 4) | volatile (bit 31)
+constexpr int VOLATILE_AUX = (int)0x80000000u;  // buffer aux: volatile only (default cache policy)
+constexpr int OOB_OFF = 0x7FFFFFF0;             // past every buffer: reads 0, no access
 // One wave polls one pair per lane at granule slot `slot` (even; < 0: none) until its tags equal
 // `tag` (the second half only when `both`); v0/v1 = the two values.  false after `tmo` ticks.
 __device__ __forceinline__ bool sweep_pair(__amdgpu_buffer_rsrc_t r, int slot, bool both, unsigned tag, float& v0,
@@ -174,6 +176,10 @@ constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 
 static_assert(SM_RM >= 6 * 64 * 4 + RES_WAVES * RES_LMAX, "attention CU partials");
 static_assert(SM_RQ >= 3 * RES_LMAX + 2 * RES_WAVES + 16 + ADIM, "attention CU scratch");
 
+// PROF: the profiling re-run's instantiation (phase marks, event trace); the production kernel
+// compiles every measurement site out (their pointers, ticks and step compares otherwise stay live
+// across the step loop in scalar registers, which this kernel already spills)
+template <bool PROF>
 __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const ResArgs a) {
     const int c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -205,11 +211,11 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     long long plast = 0;
     // event trace of the profiling re-run (RES_TRACE_STEPS steps x RES_TRACE_EV events per CU,
     // wall_clock64 ticks): measurement only
-    long long* trace = a.prof ? a.prof + 2 * RES_PHASES + (size_t)c * RES_TRACE_STEPS * RES_TRACE_EV : nullptr;
+    long long* trace = PROF && a.prof ? a.prof + 2 * RES_PHASES + (size_t)c * RES_TRACE_STEPS * RES_TRACE_EV : nullptr;
 #define RES_EV(t, k)                                                                                \
-    if (trace && (t) < RES_TRACE_STEPS) trace[(t) * RES_TRACE_EV + (k)] = (long long)wall_clock64();
+    if (PROF && trace && (t) < RES_TRACE_STEPS) trace[(t) * RES_TRACE_EV + (k)] = (long long)wall_clock64();
 #define RES_MARK(k)                                     \
-    if (prof && tid == 0) {                             \
+    if (PROF && prof && tid == 0) {                     \
         const long long now = (long long)wall_clock64(); \
         pacc[k] += now - plast;                         \
         plast = now;                                    \
@@ -309,16 +315,22 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     const bool att_cu = rank == nx - 1;               // the last CU of each XCD runs its attention copy
     const bool xlog = xcc == flags[4];                // the XCD whose copies write the outputs
     const bool att_log = att_cu && xlog;              // ... alignment rows
-    prof = a.prof != nullptr && a.prof_marks && (c == 0 || att_log);
+    prof = PROF && a.prof != nullptr && a.prof_marks && (c == 0 || att_log);
     if (prof && tid == 0) plast = (long long)wall_clock64();
     int n = 0, n_prev = 0;
     float ufa = 0.f, vb = 0.f, ex = 0.f, erow[4] = {0.f, 0.f, 0.f, 0.f}, ptc[4] = {0.f, 0.f, 0.f, 0.f};
+    // (volatile buffer loads: the compiler may not sink them past the volatile polls of the h_att
+    // gather to their use in the context, where their latency would sit on the critical path)
+    const auto renc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.enc), (short)0, L * ENC * 4, 0x00020000);
+    const auto rpt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.Pt), (short)0, ADIM * a.Lcap * 4, 0x00020000);
     auto prefetch_rows = [&](int nn) {
         // the rows the context can use after the mask: (nn-2) mod L and [nn-1, nn+2]
         const int cx = (nn - 2 + L) % L, clo = nn >= 1 ? nn - 1 : L - 1, chi = min(nn + 2, L - 1);
-        ex = a.enc[(int64_t)cx * ENC + tid];
+        ex = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(renc, (cx * ENC + tid) * 4, 0, VOLATILE_AUX));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) erow[k] = clo + k <= chi ? a.enc[(int64_t)(clo + k) * ENC + tid] : 0.f;
+        for (int k = 0; k < 4; ++k)
+            erow[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                renc, clo + k <= chi ? ((clo + k) * ENC + tid) * 4 : OOB_OFF, 0, VOLATILE_AUX));
     };
     if (att_cu) {
         n = a.nidx[0];
@@ -447,7 +459,9 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             prefetch_rows(n);
             const int pos = res_candidate(tid >> 5, n, n_prev, L);
 #pragma unroll
-            for (int m = 0; m < 4; ++m) ptc[m] = pos >= 0 ? a.Pt[(int64_t)((tid & 31) + 32 * m) * a.Lcap + pos] : 0.f;
+            for (int m = 0; m < 4; ++m)
+                ptc[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                    rpt, pos >= 0 ? (((tid & 31) + 32 * m) * a.Lcap + pos) * 4 : OOB_OFF, 0, VOLATILE_AUX));
         }
         {
             if (wave == 4 && t > 0) mel_row(t - 1);
@@ -819,7 +833,10 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
 size_t resident_smem_bytes() { return (size_t)SM_FLOATS * sizeof(float); }
 
 hipError_t resident_prepare() {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel<false>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel<true>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
 }
 
@@ -828,8 +845,9 @@ hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched) {
     if (a.L < 2 || a.L > RES_LMAX || a.nmel > RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
     ResArgs arg = a;
     void* args[] = {&arg};
-    return launch_persistent(reinterpret_cast<const void*>(&resident_decoder_kernel), dim3(RES_CUS), dim3(RES_THREADS),
-                             args, resident_smem_bytes(), s, launched);
+    const void* fn = a.prof ? reinterpret_cast<const void*>(&resident_decoder_kernel<true>)
+                            : reinterpret_cast<const void*>(&resident_decoder_kernel<false>);
+    return launch_persistent(fn, dim3(RES_CUS), dim3(RES_THREADS), args, resident_smem_bytes(), s, launched);
 }
 
 }  // namespace tts
