@@ -513,3 +513,18 @@ def test_tacotron2_forward_batch20_teacher_forcing_mirrors():
     assert rel_rms(mel_post[1].cpu().numpy(), ref["mel_post"]) < MEL_RTOL
     np.testing.assert_array_equal(align[1, :, :7].cpu().numpy().argmax(1), ref["align"].argmax(1))
     assert np.abs(stop[1].cpu().numpy() - ref["stop"]).max() < 1e-3
+
+
+def test_batched_varlen_convs_bitwise(monkeypatch):
+    """configs[2]-shaped batch (B=64, L ~ U{60..160}): the encoder and postnet convs on varlen 64-frame
+    tiles (conv1d.hip: conv_vl_kernel) give bitwise the padded-tile kernel's results."""
+    w = weights_mod()
+    lens = w.synthetic_lengths(64, 2)
+    ids = [w.synthetic_ids(int(L), 100 + b) for b, L in enumerate(lens)]
+    fl = golden_flags(golden("t2_fwdmask_L100"))
+    m = _model(fl, max_batch=64)
+    a = m.inference_batch(ids)
+    monkeypatch.setenv("TTS_CONV_VL", "0")
+    b = m.inference_batch(ids)
+    assert a["frames"] == b["frames"]
+    assert torch.equal(a["mel_post"], b["mel_post"]) and torch.equal(a["mel"], b["mel"])

@@ -273,6 +273,186 @@ __global__ __launch_bounds__(256) void conv_kernel(const ConvArgs a, int nsplit 
             }
 }
 
+// ---------------------------------------------------------------- varlen tiles (batched KW <= 5)
+// The batched Tacotron2 encoder / postnet convs (64 sentences of 60-1000 frames) as conv_kernel
+// over a virtual packed frame axis: sentence b occupies T_b + 2 PAD consecutive virtual rows (its
+// frames between PAD zero rows on each side), so 64-frame tiles cross sentence boundaries instead
+// of padding each sentence to a tile multiple (+25 % rows at 64-frame tiles, +13 % at 32), and the
+// zero rows give every output frame its own sentence's halo.  Each 64 x 64 tile reuses a weight slab
+// for twice the frames of the 32-frame tiles, halving the L2 -> LDS weight stream that bounds them.
+// Per output element the MFMA sequence (K steps, taps, per-tap chains summed in tap order) is
+// conv_kernel's: bitwise its results.  The virtual offsets come from the device lengths (a wave
+// prefix in every workgroup: the synthesis postnet runs before the host knows the step counts).
+constexpr int CONV_VL_BMAX = 256;  // sentences per launch
+template <int KW>
+__global__ __launch_bounds__(256) void conv_vl_kernel(const ConvArgs a, int nb) {
+    constexpr int PAD = (KW - 1) / 2;
+    constexpr int BM = 64, WM = 2, WN = 2, BK = 16, NACC = KW;
+    constexpr int BN = CONV_BN;
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int XROWS = BM + KW - 1;
+    constexpr int XN = XROWS * (BK / 4);
+    constexpr int WN4 = BK * KW * (BN / 4);
+    constexpr int XR = (XN + 255) / 256, WR = (WN4 + 255) / 256;
+    __shared__ float xs[2][XROWS][BK + 1];
+    __shared__ __align__(16) float ws[2][BK][KW][BN];
+    __shared__ int vpre[CONV_VL_BMAX + 1];
+    __shared__ int rowbt[XROWS];  // input row r of the tile: b << 16 | t, or -1 (a zero row)
+    const int ntl = a.co_pad / BN;
+    const int ntile = (int)blockIdx.x % ntl, vt = (int)blockIdx.x / ntl;
+    const int c0 = ntile * BN;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // ---- virtual row offsets: vpre[b] = sum_{b' < b} (T_b' + 2 PAD)
+    if (wave == 0) {
+        int carry = 0;
+        for (int b0 = 0; b0 < nb; b0 += 64) {
+            const int b = b0 + lane;
+            const int len = b < nb ? (a.tmul > 1 ? a.T[b] * a.tmul : a.T[b]) + 2 * PAD : 0;
+            int x = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(x, d, 64);
+                if (lane >= d) x += y;
+            }
+            if (b < nb) vpre[b + 1] = carry + x;
+            carry += __shfl(x, 63, 64);
+        }
+        if (lane == 0) vpre[0] = 0;
+    }
+    __syncthreads();
+    const int V0 = vt * BM;
+    if (V0 >= vpre[nb]) return;  // (uniform) past the last sentence
+    if (tid < XROWS) {
+        const int v = V0 - PAD + tid;
+        int code = -1;
+        if (v >= 0 && v < vpre[nb]) {
+            int lo = 0, hi = nb - 1;  // the last b with vpre[b] <= v
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (vpre[mid] <= v) lo = mid;
+                else hi = mid - 1;
+            }
+            const int t = v - vpre[lo] - PAD;
+            const int Tb = a.tmul > 1 ? a.T[lo] * a.tmul : a.T[lo];
+            if (t >= 0 && t < Tb) code = (lo << 16) | t;
+        }
+        rowbt[tid] = code;
+    }
+    __syncthreads();
+    const int64_t Tin = a.in_tmax ? a.in_tmax : a.Tmax;
+    const int wt = (wave / WN) * (BM / WM);
+    const int wc = (wave % WN) * (BN / WN);
+    floatx4 acc[NACC][TM][TN];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[k][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // this thread's staged input rows: their source row (a valid dummy for zero rows)
+    const float* xsrc[XR];
+    bool xok[XR];
+#pragma unroll
+    for (int q = 0; q < XR; ++q) {
+        const int i = min(tid + q * 256, XN - 1);
+        const int code = rowbt[i / (BK / 4)];
+        xok[q] = code >= 0;
+        const int b = xok[q] ? code >> 16 : 0, t = xok[q] ? code & 0xFFFF : 0;
+        xsrc[q] = (a.ids ? a.table + (int64_t)a.ids[(int64_t)b * a.Tmax + t] * a.Cin : a.in + ((int64_t)b * Tin + t) * a.Cin) +
+                  (i % (BK / 4)) * 4;
+    }
+    float4 xr[XR], wr[WR];
+#define VL_GLOAD(CI0)                                                                                      \
+    {                                                                                                      \
+        const int ci0_ = (CI0);                                                                            \
+        _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                    \
+            const float4 v = *reinterpret_cast<const float4*>(xsrc[q] + ci0_);                             \
+            xr[q] = xok[q] ? v : float4{0.f, 0.f, 0.f, 0.f};                                               \
+        }                                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                    \
+            const int i = min(tid + q * 256, WN4 - 1);                                                     \
+            const int c4 = i % (BN / 4), rk = i / (BN / 4);                                                \
+            wr[q] = *reinterpret_cast<const float4*>(a.W + ((int64_t)(ci0_ * KW + rk)) * a.co_pad + c0 + c4 * 4); \
+        }                                                                                                  \
+    }
+#define VL_LSTORE(BUF)                                                                                     \
+    {                                                                                                      \
+        const int buf_ = (BUF);                                                                            \
+        _Pragma("unroll") for (int q = 0; q < XR; ++q) {                                                    \
+            const int i = tid + q * 256;                                                                   \
+            if (i < XN) {                                                                                  \
+                const int r = i / (BK / 4), c4 = i % (BK / 4);                                             \
+                xs[buf_][r][c4 * 4 + 0] = xr[q].x;                                                         \
+                xs[buf_][r][c4 * 4 + 1] = xr[q].y;                                                         \
+                xs[buf_][r][c4 * 4 + 2] = xr[q].z;                                                         \
+                xs[buf_][r][c4 * 4 + 3] = xr[q].w;                                                         \
+            }                                                                                              \
+        }                                                                                                  \
+        _Pragma("unroll") for (int q = 0; q < WR; ++q) {                                                    \
+            const int i = tid + q * 256;                                                                   \
+            if (i < WN4) {                                                                                 \
+                const int c4 = i % (BN / 4), rk = i / (BN / 4);                                            \
+                *reinterpret_cast<float4*>(&ws[buf_][rk / KW][rk % KW][c4 * 4]) = wr[q];                   \
+            }                                                                                              \
+        }                                                                                                  \
+    }
+    const int nsteps = a.Cin / BK;
+    VL_GLOAD(0);
+    VL_LSTORE(0);
+    __syncthreads();
+    const int row = lane & 15, kq = lane >> 4;
+    for (int st = 0; st < nsteps; ++st) {
+        const int cur = st & 1;
+        VL_GLOAD(min(st + 1, nsteps - 1) * BK);  // the last step reloads itself (unused)
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+#pragma unroll
+            for (int kk = 0; kk < BK; kk += 4) {
+                float av[TM], bv[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) av[i] = xs[cur][wt + i * 16 + row + k][kk + kq];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bv[j] = ws[cur][kk + kq][k][wc + j * 16 + row];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[k][i][j] = mfma16x16x4(av[i], bv[j], acc[k][i][j]);
+            }
+        }
+        VL_LSTORE(cur ^ 1);
+        __syncthreads();
+    }
+#undef VL_GLOAD
+#undef VL_LSTORE
+    // epilogue (conv_kernel's): D lane l holds C[(l>>4)*4 + r][l&15]; output row lr of the tile is
+    // input row lr + PAD of the map
+    const int ld = a.out_ld ? a.out_ld : a.Cout;
+    const int rtm = a.res_tmax ? a.res_tmax : a.Tmax;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int code = rowbt[wt + i * 16 + (lane >> 4) * 4 + r + PAD];
+            if (code < 0) continue;
+            const int b = code >> 16, t = code & 0xFFFF;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int co = c0 + wc + j * 16 + (lane & 15);
+                if (co >= a.Cout) continue;
+                float sum = acc[0][i][j][r];
+#pragma unroll
+                for (int k = 1; k < NACC; ++k) sum += acc[k][i][j][r];
+                float y = a.scale ? sum * a.scale[co] : sum;
+                if (a.shift) y += a.shift[co];
+                if (a.act == CONV_RELU) y = fmaxf(y, 0.f);
+                else if (a.act == CONV_TANH) y = tanhf(y);
+                else if (a.act == CONV_SIGMOID) y = sigmoidf_(y);
+                if (a.resid) y = a.resid[((int64_t)b * rtm + t) * ld + co] + y;
+                a.out[((int64_t)b * a.Tmax + t) * ld + co] = y;
+            }
+        }
+}
+
 // ---------------------------------------------------------------- small-batch convolution
 // The batch-1 postnet / encoder convs (T ~ 100-300 frames, ~100 output tiles) were bound by the
 // tiled kernel's per-K-step global -> LDS -> barrier round trip (2 us per 16-channel step at one
@@ -531,6 +711,14 @@ hipError_t launch_kw(const ConvArgs& a, int B, int frames_hint, hipStream_t s) {
             }
             return hipGetLastError();
         }
+    }
+    const char* vle = getenv("TTS_CONV_VL");  // A/B + test knob (read per launch: one per layer)
+    const bool vl_off = vle && vle[0] == '0';
+    if (KW == 5 && frames_hint > 4096 && !vl_off && !a.pool2 && a.act != CONV_HIGHWAY && B <= CONV_VL_BMAX &&
+        Tt < 65536 - 4 && B * (Tt + 4) < (1 << 30) / 64) {
+        const int vtiles = (B * (Tt + 2 * ((KW - 1) / 2)) + 63) / 64;  // upper bound: tiles past the end exit
+        hipLaunchKernelGGL(conv_vl_kernel<5>, dim3((unsigned)(vtiles * (a.co_pad / CONV_BN))), block, 0, s, a, B);
+        return hipGetLastError();
     }
     if (frames_hint <= 4096) {
         const dim3 grid(((Tt + 15) / 16) * (a.co_pad / CONV_BN) * B);
