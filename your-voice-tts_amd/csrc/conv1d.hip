@@ -295,7 +295,11 @@ __global__ __launch_bounds__(256) void conv_vl_kernel(const ConvArgs a, int nb) 
     constexpr int WN4 = BK * KW * (BN / 4);
     constexpr int XR = (XN + 255) / 256, WR = (WN4 + 255) / 256;
     __shared__ float xs[2][XROWS][BK + 1];
-    __shared__ __align__(16) float ws[2][BK][KW][BN];
+    // weight slab rows padded to BNP: the B-operand read's four k-quarter lane groups (stride
+    // KW * BNP floats) then fall on four disjoint 16-bank sets (KW * BNP = 16 mod 64), not one
+    constexpr int BNP = BN + 16;
+    static_assert((KW * BNP) % 64 == 16 || KW != 5, "bank spread for KW = 5");
+    __shared__ __align__(16) float ws[2][BK][KW][BNP];
     __shared__ int vpre[CONV_VL_BMAX + 1];
     __shared__ int rowbt[XROWS];  // input row r of the tile: b << 16 | t, or -1 (a zero row)
     const int ntl = a.co_pad / BN;
