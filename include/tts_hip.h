@@ -64,6 +64,13 @@ tts_status tts_encoder_run(tts_encoder* e, const int32_t* ids, const int32_t* le
 tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32_t* lens, int B, int Lmax,
                                  const float* state_in, float* state_out, float* out, void* stream);
 
+/* Tacotron2._add_speaker_embedding (models/tacotron2.py:65, 91-100) on an encoder output:
+ * enc[b][t] += speaker_embedding.weight[speaker_ids[b]] for t < lens[b] (rows past stay zero).
+ * The handle must have been created with speaker_embedding.weight among its tensors.
+ *   enc [dev] fp32 [B][Lmax][512]; lens, speaker_ids [host] int32 [B] (B <= 64) */
+tts_status tts_encoder_add_speakers(tts_encoder* e, float* enc, const int32_t* lens, const int32_t* speaker_ids, int B,
+                                    int Lmax, void* stream);
+
 /* 1 if the last run's BiLSTM took the resident (one co-resident launch) path, 0 for the per-step
  * launches (batches, or a device where the resident grid cannot be co-resident). */
 tts_status tts_encoder_last_path(tts_encoder* e, int* resident);
@@ -231,7 +238,7 @@ tts_status tts_gl_last_path(tts_gl* g, int* path);
 tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels);
 
 /* ---------------------------------------------------------------- whole-sentence synthesis
- * Replaces utils/synthesis.py:synthesis for Tacotron2 without speakers (model.inference, :50-57,
+ * Replaces utils/synthesis.py:synthesis for Tacotron2 (model.inference, :50-57,
  * then ap.inv_mel_spectrogram of the postnet output, :69-77) in ONE call over the handles above:
  * tts_encoder_run -> tts_decoder_run -> tts_postnet_run -> tts_gl_run (mel mode, device phases
  * from `seed`), bitwise the same as calling them one by one, without the host round trips in
@@ -246,6 +253,12 @@ void tts_synth_destroy(tts_synth* s);
  *          waveform is the first hop*(frames[b]-1) samples of its row, the rest zero. */
 tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, int B, int Lmax, int max_steps,
                          int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames, void* stream);
+/* tts_synth_run for a multi-speaker Tacotron2 (utils/synthesis.py:synthesis with speaker_id):
+ * the speaker embedding is added to the encoder output (tts_encoder_add_speakers) before the decoder.
+ *   speaker_ids [host] int32 [B] */
+tts_status tts_synth_run_speakers(tts_synth* s, const int32_t* ids, const int32_t* lens, const int32_t* speaker_ids,
+                                  int B, int Lmax, int max_steps, int gl_iters, uint64_t seed, double* wav,
+                                  int64_t wav_cap, int32_t* frames, void* stream);
 /* tts_synth_run returns once Griffin-Lim is enqueued; its completion status (a persistent loop's
  * hand-off timeout) is otherwise collected by the next run.  This waits for the last run and
  * returns that status.  A failed run's waveform is NaN, never a plausible-looking signal. */

@@ -119,6 +119,47 @@ def make_model_fixtures():
         print(f"{name}: L={L} T={mel.shape[1]} flags={flags}")
 
 
+SPEAKER_CASES = [
+    # name, L, id seed, speaker id (of 4): Tacotron2 with speaker embeddings (models/tacotron2.py:32-34,
+    # 91-100) under the synthesis attention configuration (forward attention + mask)
+    ("t2spk_fwdmask_L24_s2", 24, 21, 2),
+    ("t2spk_fwdmask_L40_s0", 40, 22, 0),
+]
+
+
+def make_speaker_fixtures():
+    import torch
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    from utils.generic_utils import load_config, setup_model
+    torch.set_num_threads(os.cpu_count())
+    for name, L, seed, spk in SPEAKER_CASES:
+        C = load_config(os.path.join(REF, "config_tacotron2.json"))
+        C.num_speakers = 4
+        C.forward_attn_mask = True
+        model = setup_model(130, 4, C)
+        sd = weights.tacotron2_weights(0, num_chars=130, num_speakers=4)
+        ref_sd = model.state_dict()
+        assert list(ref_sd.keys()) == list(sd.keys()), (set(ref_sd) ^ set(sd))
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        model.eval()
+        ids = weights.synthetic_ids(L, seed)
+        with torch.no_grad():
+            x = torch.from_numpy(ids).unsqueeze(0)
+            sid = torch.tensor([spk])
+            enc = model._add_speaker_embedding(model.encoder.inference(model.embedding(x).transpose(1, 2)), sid)
+            mel, mel_post, align, stop = model.inference(x, speaker_ids=sid)
+        flags = dict(attn_norm=C.attention_norm, forward_attn=C.use_forward_attn,
+                     trans_agent=C.transition_agent, forward_attn_mask=C.forward_attn_mask,
+                     location_attn=C.location_attn, attn_win=C.windowing,
+                     max_decoder_steps=model.decoder.max_decoder_steps)
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), ids=ids, speaker_id=np.array(spk), enc=enc[0].numpy(),
+            mel=mel[0].numpy(), mel_post=mel_post[0].numpy(), align=align[0].numpy(), stop=stop[0, :, 0].numpy(),
+            flags=np.array(repr(flags)))
+        print(f"{name}: L={L} speaker={spk} T={mel.shape[1]}")
+
+
 # name, config file, L, id seed, num_speakers, speaker id, (style frames, style seed) or None,
 # max_decoder_steps, overrides.  Small L exercise the stop rule (layers/tacotron.py:464-469): L=2
 # stops on the stop token at t=1, L=4/10 on the alignment tail, L=24 runs into the cap.
@@ -367,7 +408,9 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "taco", "truncated", "teacher", "text", "split", "gl"]
+    which = sys.argv[1:] or ["model", "speakers", "taco", "truncated", "teacher", "text", "split", "gl"]
+    if "speakers" in which:
+        make_speaker_fixtures()
     if "teacher" in which:
         make_teacher_fixtures()
     if "split" in which:

@@ -528,3 +528,44 @@ def test_batched_varlen_convs_bitwise(monkeypatch):
     b = m.inference_batch(ids)
     assert a["frames"] == b["frames"]
     assert torch.equal(a["mel_post"], b["mel_post"]) and torch.equal(a["mel"], b["mel"])
+
+
+def _speaker_model():
+    t2 = load_pkg("tacotron2")
+    fl = golden_flags(golden("t2spk_fwdmask_L24_s2"))
+    m = t2.Tacotron2(130, 4, r=1, attn_win=fl["attn_win"], attn_norm=fl["attn_norm"], forward_attn=fl["forward_attn"],
+                     trans_agent=fl["trans_agent"], forward_attn_mask=fl["forward_attn_mask"],
+                     location_attn=fl["location_attn"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in weights_mod().tacotron2_weights(0, num_speakers=4).items()})
+    return m.cuda().eval()
+
+
+def test_speaker_embedding_batch_vs_reference():
+    """Tacotron2 with 4 speakers: a ragged batch of two sentences with different speakers through
+    inference_batch (native tts_encoder_add_speakers) against the reference's own outputs."""
+    zs = [golden("t2spk_fwdmask_L24_s2"), golden("t2spk_fwdmask_L40_s0")]
+    m = _speaker_model()
+    out = m.inference_batch([z["ids"] for z in zs], speaker_ids=[int(z["speaker_id"]) for z in zs])
+    for b, z in enumerate(zs):
+        T = out["frames"][b]
+        assert T == z["mel"].shape[0]
+        np.testing.assert_array_equal(out["align"][b, :T, :len(z["ids"])].cpu().numpy().argmax(1), z["align"].argmax(1))
+        assert rel_rms(out["mel"][b, :T].cpu().numpy(), z["mel"]) < MEL_RTOL
+        assert rel_rms(out["mel_post"][b, :T].cpu().numpy(), z["mel_post"]) < MEL_RTOL
+
+
+def test_speaker_embedding_synthesize_native_vs_oracle(audio_cfg):
+    """The one-call synthesis with a speaker (tts_synth_run_speakers, batch 1: resident path) against
+    the oracle chain on the reference's mel_post with the device's phases."""
+    z = golden("t2spk_fwdmask_L24_s2")
+    m = _speaker_model()
+    ap = load_pkg("audio").AudioProcessor(**audio_cfg)
+    wav, frames = m.synthesize_native([z["ids"]], ap, seed=5, speaker_ids=[int(z["speaker_id"])])
+    wav = wav.clone()  # (the returned waveform is a view of the model's buffer)
+    F = z["mel"].shape[0]
+    assert frames == [F]
+    ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(z["mel_post"].T, device_phases(5, F))
+    assert rel_rms(wav.cpu().numpy()[0], ref) < WAV_RTOL
+    # and without a speaker id the reference adds no embedding: not the speaker fixture's output
+    wav0, _ = m.synthesize_native([z["ids"]], ap, seed=5)
+    assert not torch.equal(wav0, wav)

@@ -178,3 +178,24 @@ def test_teacher_forced_oracle_matches_reference(case):
     assert np.abs(align - z["align"]).max() < 1e-6
     np.testing.assert_array_equal(align.argmax(1), z["align"].argmax(1))
     assert np.abs(o.postnet(mel) - z["mel_post"].T).max() < 1e-5
+
+
+SPK_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2spk_*.npz")))
+
+
+@pytest.mark.parametrize("case", SPK_CASES)
+def test_tacotron2_oracle_speakers_match_reference(case):
+    """Tacotron2 with speaker embeddings (models/tacotron2.py:32-34, 91-100): the oracles against the
+    reference run with 4 speakers (tests/golden/make_golden.py speakers)."""
+    from oracle.tacotron2_torch import Tacotron2TorchCPU
+    z = golden(case)
+    fl = golden_flags(z)
+    sd = weights_mod().tacotron2_weights(0, num_speakers=4)
+    spk = int(z["speaker_id"])
+    o = Tacotron2Oracle(sd, dtype=np.float32, **fl)
+    assert rel_rms(o.encoder(z["ids"], spk), z["enc"]) < 1e-6
+    for res in (o.inference(z["ids"], spk), Tacotron2TorchCPU(sd, **fl).inference(z["ids"], spk)):
+        assert res["mel"].shape == z["mel"].shape
+        np.testing.assert_array_equal(res["align"].argmax(1), z["align"].argmax(1))
+        assert rel_rms(res["mel"], z["mel"]) < 1e-4
+        assert rel_rms(res["mel_post"], z["mel_post"]) < 1e-4

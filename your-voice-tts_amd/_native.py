@@ -23,6 +23,7 @@ TACOTRON_STEP_KERNELS = ("prenet2", "att_gru", "query", "attention", "proj", "de
 # every symbol include/tts_hip.h declares
 EXPORTS = (
     "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state", "tts_encoder_last_path",
+    "tts_encoder_add_speakers", "tts_synth_run_speakers",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue", "tts_decoder_run_teacher",
     "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases", "tts_decoder_resident_trace",
     "tts_decoder_profile",
@@ -74,6 +75,7 @@ def _declare(lib):
     lib.tts_encoder_destroy.argtypes = [vp]
     lib.tts_encoder_destroy.restype = None
     lib.tts_encoder_run.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.tts_encoder_add_speakers.argtypes = [vp, vp, I32P, I32P, ctypes.c_int, ctypes.c_int, vp]
     lib.tts_decoder_create.argtypes = [ctypes.POINTER(DecoderConfig), ctypes.POINTER(TensorView), ctypes.c_int, vp,
                                        ctypes.POINTER(vp)]
     lib.tts_decoder_destroy.argtypes = [vp]
@@ -108,6 +110,8 @@ def _declare(lib):
     lib.tts_synth_destroy.restype = None
     lib.tts_synth_run.argtypes = [vp, I32P, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.c_uint64, vp, ctypes.c_int64, I32P, vp]
+    lib.tts_synth_run_speakers.argtypes = [vp, I32P, I32P, I32P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_uint64, vp, ctypes.c_int64, I32P, vp]
     FP = ctypes.POINTER(ctypes.c_float)
     lib.tts_decoder_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]
     lib.tts_gl_profile.argtypes = [vp, ctypes.c_int, FP, ctypes.c_int]

@@ -57,6 +57,9 @@ void decoder_set_pipeline_io(tts_decoder* d, const int* lens_dev, const int* rb_
 const int* encoder_lens_buffer(tts_encoder* e);
 void encoder_status_words(tts_encoder* e, const int** dev, int** host);
 void encoder_set_defer_status(tts_encoder* e, bool defer);
+// _add_speaker_embedding on an encoder output, on stream s (tts_encoder_add_speakers's body)
+tts_status encoder_add_speakers(tts_encoder* e, float* enc, const int32_t* lens, const int32_t* speaker_ids, int B,
+                                int Lmax, hipStream_t s);
 // the next pipeline-mode run's lengths are already in encoder_lens_buffer (stage_ids): no upload
 void encoder_set_lens_staged(tts_encoder* e, bool staged);
 // postnet.hip: tts_postnet_run with device frame counts (T_dev[b] * tmul) and input rows mel_tmax

@@ -33,6 +33,8 @@ struct tts_encoder {
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     std::vector<void*> allocs;
     float* emb = nullptr;
+    float* spk = nullptr;  // speaker_embedding.weight [nspk][512] (models/tacotron2.py:32-34), or null
+    int nspk = 0;
     float *Wc[3] = {}, *sc[3] = {}, *sh[3] = {};
     float *Wp = nullptr, *bp = nullptr;  // projection [512][1][2048], bias [2048]
     float *Wcf[3] = {}, *Wpf = nullptr;  // fragment-order copies (conv_pack_frag): small-batch conv kernel
@@ -231,6 +233,15 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
     e->num_chars = (int)(it->second.second / EDIM);
     CK(emalloc(e, &e->emb, (size_t)e->num_chars * EDIM));
     HK(hipMemcpyAsync(e->emb, it->second.first, sizeof(float) * e->num_chars * EDIM, hipMemcpyDeviceToDevice, s));
+    if (auto sp = wm.find("speaker_embedding.weight"); sp != wm.end()) {
+        if (sp->second.second % EDIM || sp->second.second == 0) {
+            set_error("bad speaker_embedding.weight");
+            return fail(TTS_ERR_INVALID);
+        }
+        e->nspk = (int)(sp->second.second / EDIM);
+        CK(emalloc(e, &e->spk, (size_t)e->nspk * EDIM));
+        HK(hipMemcpyAsync(e->spk, sp->second.first, sizeof(float) * e->nspk * EDIM, hipMemcpyDeviceToDevice, s));
+    }
     for (int l = 0; l < 3; ++l) {
         const std::string pre = "encoder.convolutions." + std::to_string(l) + ".net.";
         const float* w = get(pre + "0.weight", (int64_t)EDIM * EDIM * 5);
@@ -539,7 +550,60 @@ tts_status encoder_pending_status(tts_encoder* e, int* placement_failed) {
 }
 }  // namespace tts
 
+namespace {
+// _add_speaker_embedding (models/tacotron2.py:91-100): enc[b][t] += table[speaker[b]] for t < len[b]
+struct SpeakerAdd {
+    int spk[64];
+    int len[64];
+};
+__global__ void speaker_add_kernel(float* enc, int Lmax, const float* table, const SpeakerAdd a) {
+    const int t = blockIdx.x, b = blockIdx.y;
+    if (t >= a.len[b]) return;  // rows past the sentence stay zero
+    float4* row = reinterpret_cast<float4*>(enc + ((size_t)b * Lmax + t) * EDIM) + threadIdx.x;
+    const float4 v = reinterpret_cast<const float4*>(table + (size_t)a.spk[b] * EDIM)[threadIdx.x];
+    const float4 x = *row;
+    *row = float4{x.x + v.x, x.y + v.y, x.z + v.z, x.w + v.w};
+}
+}  // namespace
+
+namespace tts {
+tts_status encoder_add_speakers(tts_encoder* e, float* enc, const int32_t* lens, const int32_t* speaker_ids, int B,
+                                int Lmax, hipStream_t s) {
+    TTS_CHECK(e && enc && lens && speaker_ids, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(e->spk, TTS_ERR_INVALID, "speaker embeddings need speaker_embedding.weight at tts_encoder_create");
+    TTS_CHECK(B >= 1 && B <= 64 && B <= e->Bcap && Lmax >= 1, TTS_ERR_INVALID, "bad batch for speaker embeddings");
+    SpeakerAdd a{};
+    for (int b = 0; b < B; ++b) {
+        TTS_CHECK(speaker_ids[b] >= 0 && speaker_ids[b] < e->nspk, TTS_ERR_INVALID, "speaker id out of range");
+        TTS_CHECK(lens[b] >= 0 && lens[b] <= Lmax, TTS_ERR_INVALID, "length out of range [0, Lmax]");
+        a.spk[b] = speaker_ids[b];
+        a.len[b] = lens[b];
+    }
+    hipLaunchKernelGGL(speaker_add_kernel, dim3(Lmax, B), dim3(EDIM / 4), 0, s, enc, Lmax, e->spk, a);
+    TTS_HIP(hipGetLastError());
+    return TTS_OK;
+}
+}  // namespace tts
+
 extern "C" {
+
+tts_status tts_encoder_add_speakers(tts_encoder* e, float* enc, const int32_t* lens, const int32_t* speaker_ids, int B,
+                                    int Lmax, void* stream) {
+    TTS_CHECK(e, TTS_ERR_INVALID, "null argument");
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    hipStream_t s = e->pipeline ? cs : e->stream;
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(e->ev_in, cs));
+        TTS_HIP(hipStreamWaitEvent(s, e->ev_in, 0));
+    }
+    tts_status st = tts::encoder_add_speakers(e, enc, lens, speaker_ids, B, Lmax, s);
+    if (st) return st;
+    if (s != cs) {
+        TTS_HIP(hipEventRecord(e->ev_out, s));
+        TTS_HIP(hipStreamWaitEvent(cs, e->ev_out, 0));
+    }
+    return TTS_OK;
+}
 
 tts_status tts_encoder_last_path(tts_encoder* e, int* resident) {
     TTS_CHECK(e && resident, TTS_ERR_INVALID, "null argument");

@@ -71,9 +71,12 @@ struct PipelineScope {
 };
 
 // the stages of one tts_synth_run after the host staging (defined below)
-tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* h_frames, int B, int Lmax,
-                        int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
-                        void* stream);
+tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int32_t* spk, int32_t* h_frames, int B,
+                        int Lmax, int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap,
+                        int32_t* frames, void* stream);
+tts_status synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, const int32_t* spk, int B, int Lmax,
+                     int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
+                     void* stream);
 }  // namespace
 
 extern "C" {
@@ -132,6 +135,21 @@ void tts_synth_destroy(tts_synth* s) {
 
 tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, int B, int Lmax, int max_steps,
                          int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames, void* stream) {
+    return synth_run(s, ids, lens, nullptr, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
+}
+
+tts_status tts_synth_run_speakers(tts_synth* s, const int32_t* ids, const int32_t* lens, const int32_t* speaker_ids,
+                                  int B, int Lmax, int max_steps, int gl_iters, uint64_t seed, double* wav,
+                                  int64_t wav_cap, int32_t* frames, void* stream) {
+    TTS_CHECK(speaker_ids, TTS_ERR_INVALID, "null speaker_ids");
+    return synth_run(s, ids, lens, speaker_ids, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
+}
+}  // extern "C"
+
+namespace {
+tts_status synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, const int32_t* spk, int B, int Lmax,
+                     int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
+                     void* stream) {
     TTS_CHECK(s && ids && lens && wav && frames && B >= 1 && Lmax >= 2 && max_steps >= 1 && gl_iters >= 0,
               TTS_ERR_INVALID, "bad synth arguments");
     hipStream_t ss = s->stream;
@@ -178,7 +196,7 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
     std::copy(lens, lens + B, h_lens);
     // a call that fails after staging may still have copies from pin[par] in flight: drain them
     // before returning, so the next call can restage the same buffer
-    st = synth_stages(s, h_ids, h_lens, h_frames, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
+    st = synth_stages(s, h_ids, h_lens, spk, h_frames, B, Lmax, max_steps, gl_iters, seed, wav, wav_cap, frames, stream);
     if (st) {
         (void)hipStreamSynchronize(s->stream);
         (void)hipStreamSynchronize(s->gl_stream);
@@ -187,7 +205,9 @@ tts_status tts_synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, 
     ++s->calls;  // only now: a failed call leaves the parity (and its drained buffers) to the next
     return TTS_OK;
 }
+}  // namespace
 
+extern "C" {
 tts_status tts_synth_sync(tts_synth* s) {
     TTS_CHECK(s, TTS_ERR_INVALID, "null handle");
     TTS_HIP(hipStreamSynchronize(s->stream));
@@ -198,9 +218,9 @@ tts_status tts_synth_sync(tts_synth* s) {
 }  // extern "C"
 
 namespace {
-tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* h_frames, int B, int Lmax,
-                        int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap, int32_t* frames,
-                        void* stream) {
+tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int32_t* spk, int32_t* h_frames, int B,
+                        int Lmax, int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap,
+                        int32_t* frames, void* stream) {
     hipStream_t cs = static_cast<hipStream_t>(stream);
     hipStream_t ss = s->stream;
     const int cap = max_steps + 21;
@@ -309,6 +329,8 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, int32_t* 
     tts::decoder_set_post_hook(s->d, B == 1 && !no_hook ? +hook_fn : nullptr, &hook);
     for (int attempt = 0;; ++attempt) {
         if ((st = tts_encoder_run(s->e, ids_dev, h_lens, B, Lmax, enc, ss))) return st;
+        // Tacotron2._add_speaker_embedding (models/tacotron2.py:65, 91-100)
+        if (spk && (st = tts::encoder_add_speakers(s->e, enc, h_lens, spk, B, Lmax, ss))) return st;
         // synchronises ss: the encoder's placement status is then readable
         st = tts_decoder_run(s->d, enc, h_lens, B, Lmax, max_steps, cap, s->mel, s->stop, nullptr, s->steps.data(), ss);
         if (!st) st = hook.st;

@@ -24,7 +24,6 @@ from collections import OrderedDict
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import _native, weights
 
@@ -167,7 +166,8 @@ class Tacotron2:
             p = ctypes.c_void_p()
             _native.check(lib.tts_postnet_create(arr2, len(post_w), 80, stream, ctypes.byref(p)), "tts_postnet_create")
             enc_w = {k: v.float().contiguous() for k, v in self._params.items()
-                     if (k.startswith("encoder.") or k == "embedding.weight") and v.is_floating_point()}
+                     if (k.startswith("encoder.") or k in ("embedding.weight", "speaker_embedding.weight"))
+                     and v.is_floating_point()}
             arr3, keep3 = _native.tensor_views(enc_w)
             e = ctypes.c_void_p()
             _native.check(lib.tts_encoder_create(arr3, len(enc_w), key[2], key[1], stream, ctypes.byref(e)),
@@ -190,9 +190,18 @@ class Tacotron2:
                                           B, Lmax, ctypes.c_void_p(out.data_ptr()), _native.stream_handle()),
                       "tts_encoder_run")
         if speaker_ids is not None and "speaker_embedding.weight" in p:
-            out = out + F.embedding(torch.as_tensor(speaker_ids, device=ids.device).view(-1),
-                                    p["speaker_embedding.weight"])[:, None, :]
+            self._add_speakers(lib, out, lens, speaker_ids)
         return out
+
+    def _add_speakers(self, lib, enc, lens, speaker_ids):
+        """models/tacotron2.py:91-100 on the device (tts_encoder_add_speakers), in place."""
+        B, Lmax = enc.shape[0], enc.shape[1]
+        spk = np.asarray(torch.as_tensor(speaker_ids).view(-1).cpu().numpy(), dtype=np.int32)
+        if spk.size == 1 and B > 1:
+            spk = np.repeat(spk, B)
+        _native.check(lib.tts_encoder_add_speakers(self._native[3], ctypes.c_void_p(enc.data_ptr()),
+                                                   _native.i32_array(lens), _native.i32_array(spk), B, Lmax,
+                                                   _native.stream_handle()), "tts_encoder_add_speakers")
 
     # ------------------------------------------------------------------ inference
     @torch.no_grad()
@@ -315,7 +324,7 @@ class Tacotron2:
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
     @torch.no_grad()
-    def synthesize_native(self, ids_list, ap, seed=0, iters=None, sync=True):
+    def synthesize_native(self, ids_list, ap, seed=0, iters=None, sync=True, speaker_ids=None):
         """utils/synthesis.py:synthesis (model.inference, :50-57 -> ap.inv_mel_spectrogram, :69-77)
         for a ragged batch in ONE native call (tts_synth_run): encoder -> decoder -> postnet ->
         Griffin-Lim with device phases from ``seed``, bitwise what inference_batch followed by
@@ -325,8 +334,8 @@ class Tacotron2:
         sync=True waits for the run and raises on its completion status; sync=False returns once
         Griffin-Lim is enqueued (the next call overlaps it and raises a failure of this one; a
         failed run's waveform is NaN, never a plausible signal)."""
-        if "speaker_embedding.weight" in self._params:
-            raise ValueError("synthesize_native: speaker embeddings go through inference_batch")
+        if speaker_ids is not None and "speaker_embedding.weight" not in self._params:
+            speaker_ids = None  # (the reference adds no embedding without the table either)
         lens = [len(x) for x in ids_list]
         if min(lens) < 2:
             raise ValueError("encoder length must be >= 2 (common_layers.py:213)")
@@ -355,9 +364,18 @@ class Tacotron2:
             self._wav_buf = torch.empty(cap, dtype=torch.float64, device=self.device)
         frames = (ctypes.c_int32 * B)()
         iters = ap.griffin_lim_iters if iters is None else iters
-        _native.check(lib.tts_synth_run(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens), B, Lmax,
-                                        max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
-                                        cap, frames, _native.stream_handle()), "tts_synth_run")
+        if speaker_ids is None:
+            _native.check(lib.tts_synth_run(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens), B, Lmax,
+                                            max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
+                                            cap, frames, _native.stream_handle()), "tts_synth_run")
+        else:
+            spk = np.asarray(torch.as_tensor(speaker_ids).view(-1).cpu().numpy(), dtype=np.int32)
+            if spk.size == 1 and B > 1:
+                spk = np.repeat(spk, B)
+            _native.check(lib.tts_synth_run_speakers(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens),
+                                                     _native.i32_array(spk), B, Lmax, max_steps, int(iters), int(seed),
+                                                     ctypes.c_void_p(self._wav_buf.data_ptr()), cap, frames,
+                                                     _native.stream_handle()), "tts_synth_run_speakers")
         frames = [int(f) for f in frames]
         if sync:
             _native.check(lib.tts_synth_sync(hs), "tts_synth_sync")
@@ -442,8 +460,7 @@ class Tacotron2:
             ctypes.c_void_p(enc.data_ptr()), _native.stream_handle()), "tts_encoder_run_state")
         self._enc_state = state_out
         if speaker_ids is not None and "speaker_embedding.weight" in self._params:
-            enc = enc + F.embedding(torch.as_tensor(speaker_ids, device=self.device).view(-1),
-                                    self._params["speaker_embedding.weight"])[:, None, :]
+            self._add_speakers(lib, enc, [L], speaker_ids)
         out = self.inference_batch(None, enc=enc, lens=[L], _continue=self._trunc_started)
         self._trunc_started = True
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
