@@ -92,7 +92,10 @@ typedef struct tts_decoder_config {
 
 /* Replaces the construction + load_state_dict of layers/tacotron2.py:97-150 (Decoder).
  * `tensors` must hold every decoder.* key of the reference state_dict for this config; they
- * are repacked into the library's MFMA-fragment layout (the caller may free them after). */
+ * are repacked into the library's MFMA-fragment layout (the caller may free them after).
+ * prenet_type "bn" (common_layers.py:28-70) is selected by the presence of the
+ * decoder.prenet.layers.{0,1}.bn.* keys (eval-mode BatchNorm1d, folded into the prenet at create;
+ * tts_tacotron_create does the same for its decoder prenet). */
 tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* tensors, int n_tensors,
                               void* stream, tts_decoder** out);
 void tts_decoder_destroy(tts_decoder* d);

@@ -95,6 +95,17 @@ class Tacotron2Oracle:
         return (out, (hN, cN)) if return_state else out
 
     # ------------------------------------------------------------------ decoder
+    def _prenet_layer(self, i, x):
+        """Prenet layer i without its ReLU: Linear(bias=False) (layers/tacotron2.py:114), then for
+        prenet_type "bn" BatchNorm1d in eval mode (common_layers.py:45-52; running statistics,
+        eps 1e-5), present when the state dict holds its keys."""
+        p = f"decoder.prenet.layers.{i}."
+        y = self.w[p + "linear_layer.weight"] @ x
+        if p + "bn.weight" in self.w:
+            y = ((y - self.w[p + "bn.running_mean"]) / np.sqrt(self.w[p + "bn.running_var"] + 1e-5) *
+                 self.w[p + "bn.weight"] + self.w[p + "bn.bias"])
+        return y
+
     def decoder(self, memory_in, carry=None, return_carry=False, teacher=None):
         """Decoder.inference (layers/tacotron2.py:249-285) for one sentence; with ``teacher`` ([T, 80]
         frames) Decoder.forward (:227-247) instead: step t decodes from the go frame (t = 0) or teacher
@@ -131,9 +142,9 @@ class Tacotron2Oracle:
         stop_count = 0
         t = 0
         while True:
-            # Prenet (common_layers.py:77-83), eval: no dropout
-            x = np.maximum(w["decoder.prenet.layers.0.linear_layer.weight"] @ memory, 0)
-            x = np.maximum(w["decoder.prenet.layers.1.linear_layer.weight"] @ x, 0)
+            # Prenet (common_layers.py:77-83), eval: no dropout; prenet_type "bn": LinearBN (:28-52)
+            x = np.maximum(self._prenet_layer(0, memory), 0)
+            x = np.maximum(self._prenet_layer(1, x), 0)
             # decode() (:194-225)
             h_att, c_att = self._lstm_cell(np.concatenate([x, ctx]), h_att, c_att,
                                            w["decoder.attention_rnn.weight_ih"], w["decoder.attention_rnn.weight_hh"],

@@ -104,8 +104,13 @@ class Tacotron2TorchCPU:
         u = 0.5 * torch.ones(1, 1)
         win_idx = -1
         memory = F.embedding(zero, w["decoder.go_frame_init.weight"])
-        w_p0 = w["decoder.prenet.layers.0.linear_layer.weight"]
-        w_p1 = w["decoder.prenet.layers.1.linear_layer.weight"]
+        def prenet_layer(i, x):  # Linear(bias=False), + eval BatchNorm1d for prenet_type "bn" (:28-52)
+            p = f"decoder.prenet.layers.{i}."
+            y = F.linear(x, w[p + "linear_layer.weight"])
+            if p + "bn.weight" in w:
+                y = F.batch_norm(y, w[p + "bn.running_mean"], w[p + "bn.running_var"], w[p + "bn.weight"],
+                                 w[p + "bn.bias"], False, 0.0, 1e-5)
+            return y
         w_mel, b_mel = w["decoder.linear_projection.linear_layer.weight"], w["decoder.linear_projection.linear_layer.bias"]
         w_st, b_st = w["decoder.stopnet.1.linear_layer.weight"], w["decoder.stopnet.1.linear_layer.bias"]
         outs, stops, aligns = [], [], []
@@ -113,7 +118,7 @@ class Tacotron2TorchCPU:
         stop_count = 0
         t = 0
         while True:
-            x = torch.relu(F.linear(torch.relu(F.linear(memory, w_p0)), w_p1))
+            x = torch.relu(prenet_layer(1, torch.relu(prenet_layer(0, memory))))
             h_att, c_att = torch.lstm_cell(torch.cat((x, ctx), -1), (h_att, c_att), *self._cell["attention_rnn"])
             e = self._energies(h_att, P, att_w, att_cum)
             if self.attn_win:

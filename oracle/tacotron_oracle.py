@@ -87,10 +87,16 @@ class TacotronOracle:
         return out
 
     def _prenet(self, prefix, x):
-        """Prenet eval (layers/common_layers.py:77-83): relu(linear) per layer, no dropout."""
+        """Prenet eval (layers/common_layers.py:77-83): relu(linear) per layer, no dropout; with
+        prenet_type "bn" (the decoder's, layers/tacotron.py:283-287) each linear is followed by an
+        eval-mode BatchNorm1d (LinearBN, common_layers.py:28-52; eps 1e-5)."""
         for i in range(2):
-            x = np.maximum(x @ self.w[f"{prefix}.layers.{i}.linear_layer.weight"].T +
-                           self.w[f"{prefix}.layers.{i}.linear_layer.bias"], 0)
+            p = f"{prefix}.layers.{i}."
+            y = x @ self.w[p + "linear_layer.weight"].T + self.w[p + "linear_layer.bias"]
+            if p + "bn.weight" in self.w:
+                y = ((y - self.w[p + "bn.running_mean"]) / np.sqrt(self.w[p + "bn.running_var"] + 1e-5) *
+                     self.w[p + "bn.weight"] + self.w[p + "bn.bias"])
+            x = np.maximum(y, 0)
         return x
 
     def cbhg(self, prefix, x, K, projections):

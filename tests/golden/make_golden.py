@@ -160,6 +160,40 @@ def make_speaker_fixtures():
         print(f"{name}: L={L} speaker={spk} T={mel.shape[1]}")
 
 
+def make_prenet_bn_fixtures():
+    """Tacotron2 with prenet_type "bn" (common_layers.py:27-52, 55-83; eval-mode BatchNorm1d)."""
+    import torch
+    _stub_text_deps()
+    sys.path.insert(0, REF)
+    from utils.generic_utils import load_config, setup_model
+    torch.set_num_threads(os.cpu_count())
+    for name, L, seed in (("t2bn_fwdmask_L24", 24, 31), ("t2bn_fwdmask_L40", 40, 32)):
+        C = load_config(os.path.join(REF, "config_tacotron2.json"))
+        C.num_speakers = 0
+        C.forward_attn_mask = True
+        C.prenet_type = "bn"
+        model = setup_model(130, 0, C)
+        sd = weights.tacotron2_weights(0, num_chars=130, prenet_bn=True)
+        ref_sd = model.state_dict()
+        assert list(ref_sd.keys()) == list(sd.keys()), (set(ref_sd) ^ set(sd))
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        model.eval()
+        ids = weights.synthetic_ids(L, seed)
+        with torch.no_grad():
+            x = torch.from_numpy(ids).unsqueeze(0)
+            enc = model.encoder.inference(model.embedding(x).transpose(1, 2))
+            mel, mel_post, align, stop = model.inference(x)
+        flags = dict(attn_norm=C.attention_norm, forward_attn=C.use_forward_attn,
+                     trans_agent=C.transition_agent, forward_attn_mask=C.forward_attn_mask,
+                     location_attn=C.location_attn, attn_win=C.windowing,
+                     max_decoder_steps=model.decoder.max_decoder_steps)
+        np.savez_compressed(
+            os.path.join(HERE, name + ".npz"), ids=ids, enc=enc[0].numpy(), mel=mel[0].numpy(),
+            mel_post=mel_post[0].numpy(), align=align[0].numpy(), stop=stop[0, :, 0].numpy(),
+            flags=np.array(repr(flags)))
+        print(f"{name}: L={L} T={mel.shape[1]}")
+
+
 # name, config file, L, id seed, num_speakers, speaker id, (style frames, style seed) or None,
 # max_decoder_steps, overrides.  Small L exercise the stop rule (layers/tacotron.py:464-469): L=2
 # stops on the stop token at t=1, L=4/10 on the alignment tail, L=24 runs into the cap.
@@ -172,21 +206,27 @@ TACO_CASES = [
     ("taco_L12_softmax", "config_tacotron.json", 12, 23, 0, None, None, 16,
      dict(attention_norm="softmax", use_forward_attn=False, transition_agent=False)),
 ]
+# prenet_type "bn" (common_layers.py:28-52, 66-70) on the Tacotron decoder prenet ("taco_bn" target)
+TACO_BN_CASES = [
+    ("gst_L10_prenetbn", "config_tacotron_gst.json", 10, 51, 0, None, (40, 33), 30, dict(prenet_type="bn")),
+    ("taco_L12_prenetbn", "config_tacotron.json", 12, 52, 0, None, None, 30, dict(prenet_type="bn")),
+]
 
 
-def make_taco_fixtures():
+def make_taco_fixtures(cases=TACO_CASES):
     import torch
     _stub_text_deps()
     sys.path.insert(0, REF)
     from utils.generic_utils import load_config, setup_model
     torch.set_num_threads(os.cpu_count())
-    for name, cfgname, L, seed, nspk, spk, style, cap, over in TACO_CASES:
+    for name, cfgname, L, seed, nspk, spk, style, cap, over in cases:
         C = load_config(os.path.join(REF, cfgname))
         C.update(over)
         gst = C.model == "TacotronGST"
         model = setup_model(130, nspk, C)
         sd = weights.tacotron_gst_weights(0, num_chars=130, num_speakers=nspk, r=C.r, memory_size=C.memory_size,
-                                          location_attn=C.location_attn, trans_agent=C.transition_agent, gst=gst)
+                                          location_attn=C.location_attn, trans_agent=C.transition_agent, gst=gst,
+                                          prenet_bn=C.prenet_type == "bn")
         assert list(model.state_dict().keys()) == list(sd.keys()), (set(model.state_dict()) ^ set(sd))
         model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
         model.eval()
@@ -211,6 +251,8 @@ def make_taco_fixtures():
                      forward_attn=C.use_forward_attn, trans_agent=C.transition_agent,
                      forward_attn_mask=C.forward_attn_mask, location_attn=C.location_attn, attn_win=C.windowing,
                      max_decoder_steps=cap, num_speakers=nspk)
+        if C.prenet_type != "original":
+            flags["prenet_type"] = C.prenet_type
         np.savez_compressed(
             os.path.join(HERE, name + ".npz"), ids=ids, enc=enc[0].numpy(), mel=mel[0].numpy(),
             linear=lin[0].numpy(), align=align[0].numpy(), stop=stop[0].numpy(),
@@ -408,7 +450,11 @@ def make_gl_fixtures():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["model", "speakers", "taco", "truncated", "teacher", "text", "split", "gl"]
+    which = sys.argv[1:] or ["model", "speakers", "prenet_bn", "taco", "taco_bn", "truncated", "teacher", "text", "split", "gl"]
+    if "taco_bn" in which:
+        make_taco_fixtures(TACO_BN_CASES)
+    if "prenet_bn" in which:
+        make_prenet_bn_fixtures()
     if "speakers" in which:
         make_speaker_fixtures()
     if "teacher" in which:

@@ -569,3 +569,46 @@ def test_speaker_embedding_synthesize_native_vs_oracle(audio_cfg):
     # and without a speaker id the reference adds no embedding: not the speaker fixture's output
     wav0, _ = m.synthesize_native([z["ids"]], ap, seed=5)
     assert not torch.equal(wav0, wav)
+
+
+BN_CASES = ["t2bn_fwdmask_L24", "t2bn_fwdmask_L40"]
+
+
+def _bn_model(**kw):
+    t2 = load_pkg("tacotron2")
+    fl = golden_flags(golden(BN_CASES[0]))
+    m = t2.Tacotron2(130, 0, r=1, attn_win=fl["attn_win"], attn_norm=fl["attn_norm"], forward_attn=fl["forward_attn"],
+                     trans_agent=fl["trans_agent"], forward_attn_mask=fl["forward_attn_mask"],
+                     location_attn=fl["location_attn"], prenet_type="bn", **kw)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in weights_mod().tacotron2_weights(0, prenet_bn=True).items()})
+    m.decoder.max_decoder_steps = fl["max_decoder_steps"]
+    return m.cuda().eval()
+
+
+@pytest.mark.parametrize("case", BN_CASES)
+def test_prenet_bn_inference_vs_reference(case):
+    """prenet_type "bn" at batch 1 (the resident decoder: BatchNorm folded into the prenet rows,
+    prenet-2 bias per XCD row, prenet-1 bias in the folded mel rows) against the reference run."""
+    z = golden(case)
+    m = _bn_model()
+    mel, mel_post, align, stop = m.inference(torch.from_numpy(z["ids"])[None])
+    assert mel.shape == (1,) + z["mel"].shape
+    np.testing.assert_array_equal(align[0].cpu().numpy().argmax(1), z["align"].argmax(1))
+    np.testing.assert_array_equal(stop[0, :, 0].cpu().numpy() > 0.5, z["stop"] > 0.5)
+    assert rel_rms(mel[0].cpu().numpy(), z["mel"]) < MEL_RTOL
+    assert rel_rms(mel_post[0].cpu().numpy(), z["mel_post"]) < MEL_RTOL
+
+
+@pytest.mark.parametrize("B", [2, 20])
+def test_prenet_bn_batch_vs_reference(B):
+    """prenet_type "bn" through the multi-launch batched step (prenet GEMM biases; B = 20 also the
+    fragment-mirror GEMMs) from the reference's encoder outputs, alternating the two fixtures."""
+    zs = [golden(BN_CASES[b % 2]) for b in range(B)]
+    m = _bn_model(max_batch=max(B, 2))
+    Lmax = max(len(z["ids"]) for z in zs)
+    enc = torch.zeros(B, Lmax, 512)
+    for b, z in enumerate(zs):
+        enc[b, :len(z["ids"])] = torch.from_numpy(z["enc"])
+    out = m.inference_batch(None, enc=enc.cuda(), lens=[len(z["ids"]) for z in zs])
+    for b, z in enumerate(zs):
+        _check_decoder(out, b, z)

@@ -27,7 +27,8 @@ def _model(fl, **kw):
     cls = t.TacotronGST if fl["model"] == "TacotronGST" else t.Tacotron
     m = cls(130, fl["num_speakers"], r=fl["r"], memory_size=fl["memory_size"], attn_win=fl["attn_win"],
             attn_norm=fl["attn_norm"], forward_attn=fl["forward_attn"], trans_agent=fl["trans_agent"],
-            forward_attn_mask=fl["forward_attn_mask"], location_attn=fl["location_attn"], **kw)
+            forward_attn_mask=fl["forward_attn_mask"], location_attn=fl["location_attn"],
+            prenet_type=fl.get("prenet_type", "original"), **kw)
     m.decoder.max_decoder_steps = fl["max_decoder_steps"]
     return m.cuda().eval()
 

@@ -99,10 +99,12 @@ TACO_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOL
 
 def taco_oracle(z, dtype=np.float64):
     from oracle.tacotron_oracle import TacotronOracle
-    fl = golden_flags(z)
+    fl = dict(golden_flags(z))
+    bn = fl.pop("prenet_type", "original") == "bn"
     sd = weights_mod().tacotron_gst_weights(0, num_speakers=fl["num_speakers"], r=fl["r"],
                                             memory_size=fl["memory_size"], location_attn=fl["location_attn"],
-                                            trans_agent=fl["trans_agent"], gst=fl["model"] == "TacotronGST")
+                                            trans_agent=fl["trans_agent"], gst=fl["model"] == "TacotronGST",
+                                            prenet_bn=bn)
     return TacotronOracle(sd, dtype=dtype, **fl)
 
 
@@ -178,6 +180,30 @@ def test_teacher_forced_oracle_matches_reference(case):
     assert np.abs(align - z["align"]).max() < 1e-6
     np.testing.assert_array_equal(align.argmax(1), z["align"].argmax(1))
     assert np.abs(o.postnet(mel) - z["mel_post"].T).max() < 1e-5
+
+
+BN_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2bn_*.npz")))
+
+
+@pytest.mark.parametrize("case", BN_CASES)
+def test_tacotron2_oracle_prenet_bn_matches_reference(case):
+    """prenet_type "bn" (LinearBN layers, common_layers.py:28-52, 66-70; eval BatchNorm1d): both
+    oracles against the reference run (tests/golden/make_golden.py prenet_bn)."""
+    from oracle.tacotron2_torch import Tacotron2TorchCPU
+    z = golden(case)
+    fl = golden_flags(z)
+    sd = weights_mod().tacotron2_weights(0, prenet_bn=True)
+    assert "decoder.prenet.layers.1.bn.running_var" in sd
+    for res in (Tacotron2Oracle(sd, dtype=np.float32, **fl).inference(z["ids"]),
+                Tacotron2TorchCPU(sd, **fl).inference(z["ids"])):
+        assert res["mel"].shape == z["mel"].shape
+        np.testing.assert_array_equal(res["align"].argmax(1), z["align"].argmax(1))
+        assert rel_rms(res["mel"], z["mel"]) < 1e-4
+        assert rel_rms(res["mel_post"], z["mel_post"]) < 1e-4
+    # the BatchNorm matters: the same weights without it give another utterance
+    plain = {k: v for k, v in sd.items() if ".bn." not in k}
+    res = Tacotron2Oracle(plain, dtype=np.float32, **fl).inference(z["ids"])
+    assert res["mel"].shape != z["mel"].shape or rel_rms(res["mel"], z["mel"]) > 1e-2
 
 
 SPK_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2spk_*.npz")))

@@ -42,6 +42,7 @@ struct tts_decoder {
     hipEvent_t ev_sync = nullptr;  // spin_sync (runtime.hip)
     std::vector<void*> allocs;
     // packed GEMM weights + logical biases
+    float *b_pre1 = nullptr, *b_pre2 = nullptr;  // prenet_type "bn": the folded shifts (else null)
     float *W_pre1 = nullptr, *W_pre2 = nullptr, *W_att = nullptr, *b_att = nullptr, *W_q = nullptr;
     float *W_dec = nullptr, *b_dec = nullptr, *W_melf = nullptr, *b_melf = nullptr;
     // reference-layout small weights
@@ -198,7 +199,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         SGemmArgs a = g;
         a.seg[0] = Seg{d->pre1, PRE, PRE, fr ? d->pre1f : nullptr};
         a.nseg = 1;
-        a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU;
+        a.W = d->W_pre2; a.K = PRE; a.N = PRE; a.act = ACT_RELU; a.bias = d->b_pre2;
         a.out = xa_cur; a.ldo = XA;
         a.outf = xaf_cur; a.outf_k0 = 0;
         MARK();
@@ -314,7 +315,7 @@ tts_status enqueue_prenet_go(tts_decoder* d, int B, hipStream_t s, int* slot = n
     a.out_par = -1;
     a.seg[0] = Seg{d->mem, d->nmel, d->nmel};
     a.nseg = 1;
-    a.W = d->W_pre1; a.K = d->nmel; a.N = PRE; a.act = ACT_RELU;
+    a.W = d->W_pre1; a.K = d->nmel; a.N = PRE; a.act = ACT_RELU; a.bias = d->b_pre1;
     a.out = d->pre1; a.ldo = PRE;
     if (frag_on(d, B)) { a.outf = d->pre1f; a.outf_k0 = 0; a.ntf = d->ntf; }
     TTS_HIP(sgemm_launch(a, ROLE_PRENET, s));
@@ -413,6 +414,29 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         probe.enc_dim = ENC;
         d->fast_attention = attention_uses_epart(probe);
     }
+    // prenet_type "bn" (common_layers.py:55-70, Decoder's Prenet(bias=False) layers/tacotron2.py:114):
+    // each layer is Linear -> BatchNorm1d (eval: running statistics, eps 1e-5) -> ReLU, folded here
+    // into the layer's weight plus a bias that every prenet consumer below adds
+    const float *w_p0 = pre0, *w_p1 = pre1;
+    if (wm.m.count("decoder.prenet.layers.0.bn.weight") || wm.m.count("decoder.prenet.layers.1.bn.weight")) {
+        const int fan_in[2] = {nmel, PRE};
+        const float* w_in[2] = {pre0, pre1};
+        float* w_out[2] = {nullptr, nullptr};
+        float* b_out[2] = {nullptr, nullptr};
+        for (int l = 0; l < 2; ++l) {
+            const std::string k = "decoder.prenet.layers." + std::to_string(l) + ".bn.";
+            const float* g = wm.get(k + "weight", PRE);
+            const float* be = wm.get(k + "bias", PRE);
+            const float* mu = wm.get(k + "running_mean", PRE);
+            const float* var = wm.get(k + "running_var", PRE);
+            if (!g || !be || !mu || !var) return fail(TTS_ERR_INVALID);
+            CK(dmalloc(d, &w_out[l], (size_t)PRE * fan_in[l]));
+            CK(dmalloc(d, &b_out[l], PRE));
+            HK(fold_linear_bn(w_in[l], nullptr, g, be, mu, var, PRE, fan_in[l], 1e-5f, w_out[l], b_out[l], s));
+        }
+        w_p0 = w_out[0]; w_p1 = w_out[1];
+        d->b_pre1 = b_out[0]; d->b_pre2 = b_out[1];
+    }
     // packed GEMM weights
     const int nfused = nmel + PRE + 1;
     {
@@ -431,9 +455,9 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         }
     }
     CK(dmalloc(d, &d->W_pre1, sgemm_packed_floats(PRE, nmel)));
-    HK(sgemm_pack(pre0, nmel, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre1, s));
+    HK(sgemm_pack(w_p0, nmel, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre1, s));
     CK(dmalloc(d, &d->W_pre2, sgemm_packed_floats(PRE, PRE)));
-    HK(sgemm_pack(pre1, PRE, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre2, s));
+    HK(sgemm_pack(w_p1, PRE, nullptr, 0, PRE, ROWMAP_IDENTITY, 0, d->W_pre2, s));
     CK(dmalloc(d, &d->W_att, sgemm_packed_floats(4 * HATT, XA + HATT)));
     HK(sgemm_pack(a_wih, XA, a_whh, HATT, 4 * HATT, ROWMAP_LSTM, HATT, d->W_att, s));
     CK(dmalloc(d, &d->b_att, 4 * HATT));
@@ -448,7 +472,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         float *wf = nullptr, *bf = nullptr;  // folded logical matrix (temporary)
         HK(hipMalloc(&wf, sizeof(float) * nfused * (HDEC + ENC)));
         HK(hipMalloc(&bf, sizeof(float) * nfused));
-        hipError_t e = fold_mel_weights(pw, pb, pre0, sw, sb, nmel, HDEC + ENC, HDEC, wf, bf, s);
+        hipError_t e = fold_mel_weights(pw, pb, w_p0, d->b_pre1, sw, sb, nmel, HDEC + ENC, HDEC, wf, bf, s);
         if (e == hipSuccess) e = dmalloc(d, &d->W_melf, sgemm_packed_floats(nfused, HDEC + ENC)) ? hipErrorOutOfMemory
                                                                                                 : hipSuccess;
         if (e == hipSuccess) e = sgemm_pack(wf, HDEC + ENC, nullptr, 0, nfused, ROWMAP_IDENTITY, 0, d->W_melf, s);
@@ -461,14 +485,15 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
             if (dmalloc(d, &pa, nwa) || dmalloc(d, &pdl, nwdl) || dmalloc(d, &pdc, nwdc) ||
                 dmalloc(d, &d->rw.wf, (size_t)nfused * (HDEC + ENC)) || dmalloc(d, &d->rw.bf, nfused) ||
                 dmalloc(d, &d->rw.ba, RES_CUS * 16) || dmalloc(d, &d->rw.bd, RES_CUS * 16) ||
-                dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) || dmalloc(d, &d->rw.wq, (size_t)ADIM * HATT) ||
+                dmalloc(d, &d->rw.w2, (size_t)PRE * PRE) || dmalloc(d, &d->rw.b2, PRE) ||
+                dmalloc(d, &d->rw.wq, (size_t)ADIM * HATT) ||
                 dmalloc(d, &d->gran, (size_t)2 * GR_TOTAL + 2))
                 e = hipErrorOutOfMemory;
             if (e == hipSuccess) {
                 d->rw.wa = reinterpret_cast<float4*>(pa);
                 d->rw.wdl = reinterpret_cast<float4*>(pdl);
                 d->rw.wdc = reinterpret_cast<float4*>(pdc);
-                ResSrc src{a_wih, a_whh, a_bih, a_bhh, d_wih, d_whh, d_bih, d_bhh, pre1, wq, wf, bf, nfused};
+                ResSrc src{a_wih, a_whh, a_bih, a_bhh, d_wih, d_whh, d_bih, d_bhh, w_p1, d->b_pre2, wq, wf, bf, nfused};
                 e = resident_pack(src, d->rw, s);
             }
         }

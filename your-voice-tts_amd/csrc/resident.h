@@ -62,6 +62,7 @@ struct ResWeights {
     float* bd;    // [256][16] decoder LSTM bias
     float* w2;    // prenet layer-2 weight, reference layout [256][256] (rows picked per XCD rank)
     float* wq;    // query_layer weight, reference layout [128][1024] (rows picked per XCD rank)
+    float* b2;    // [256] prenet layer-2 bias (the BatchNorm prenet's folded shift; zeros otherwise)
 };
 
 struct ResArgs {
@@ -110,7 +111,8 @@ constexpr size_t RES_PROF_LL = 2 * RES_PHASES + (size_t)RES_CUS * RES_TRACE_STEP
 struct ResSrc {
     const float *a_wih, *a_whh, *a_bih, *a_bhh;  // attention_rnn [4096][768], [4096][1024]
     const float *d_wih, *d_whh, *d_bih, *d_bhh;  // decoder_rnn [4096][1536], [4096][1024]
-    const float* w_pre2;                         // prenet layer 1 weight [256][256]
+    const float* w_pre2;                         // prenet layer 2 weight [256][256]
+    const float* b_pre2;                         // its bias [256] or null (no bias)
     const float* w_q;                            // query_layer [128][1024]
     const float *wf, *bf;                        // folded [nrows][1536] + [nrows]
     int nrows;

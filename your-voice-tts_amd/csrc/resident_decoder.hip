@@ -300,6 +300,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     const bool has_row = r0 < p2hi;
     const float4 wp0 = has_row ? ld4(a.w.w2 + r0 * PRE + lane * 4) : float4{0.f, 0.f, 0.f, 0.f};
     const float bp1 = has_row ? a.w.bf[a.nmel + r0] : 0.f;
+    const float bp2 = has_row ? a.w.b2[r0] : 0.f;
     // folded prenet-1 row (re-read from the XCD's L2 every step: no register or LDS room); a wave
     // without a row loads row 0 and discards it (no branch around the loads)
     const float* w1p = a.w.wf + (size_t)(a.nmel + (has_row ? r0 : 0)) * KF + lane * 4;
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             u64* gx = Gx + (t & 1) * GR_TOTAL;
             if (has_row) {
                 const float s0 = wave_sum_dpp(dot4(wp0, x, 0.f));
-                if (lane == 0) publish_xcd(gx + r0, E + 1, fmaxf(s0, 0.f));
+                if (lane == 0) publish_xcd(gx + r0, E + 1, fmaxf(s0 + bp2, 0.f));
             }
             RES_MARK(1);
             if (wave < 2) {
@@ -822,6 +823,10 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
     hipLaunchKernelGGL(res_pack_wd, blocks((int64_t)RES_CUS * (8192 + 4 * RES_THREADS)), dim3(256), 0, st, s.d_wih,
                        s.d_whh, w.wdl, w.wdc);
     (void)hipMemcpyAsync(w.w2, s.w_pre2, sizeof(float) * PRE * PRE, hipMemcpyDeviceToDevice, st);
+    if (s.b_pre2)
+        (void)hipMemcpyAsync(w.b2, s.b_pre2, sizeof(float) * PRE, hipMemcpyDeviceToDevice, st);
+    else
+        (void)hipMemsetAsync(w.b2, 0, sizeof(float) * PRE, st);
     (void)hipMemcpyAsync(w.wq, s.w_q, sizeof(float) * ADIM * HATT, hipMemcpyDeviceToDevice, st);
     (void)hipMemcpyAsync(w.wf, s.wf, sizeof(float) * s.nrows * (HDEC + ENC), hipMemcpyDeviceToDevice, st);
     (void)hipMemcpyAsync(w.bf, s.bf, sizeof(float) * s.nrows, hipMemcpyDeviceToDevice, st);

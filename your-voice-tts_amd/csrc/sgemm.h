@@ -144,7 +144,12 @@ inline size_t sgemm_packed_floats(int N, int K) { return (size_t)((N + 15) / 16)
 
 hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s);
 // Wf [nmel+257][K] logical rows + bf [nmel+257] for ROLE_MEL_FUSED (see MelFused).
-hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
-                            int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s);
+hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* b1, const float* ws,
+                            const float* bs, int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s);
+// Eval-mode BatchNorm1d after a linear layer (LinearBN, common_layers.py:28-52) folded into it:
+// Wout = diag(s) W, bout = s (b - mean) + beta, s = gamma / sqrt(var + eps) (fp64, rounded once);
+// b may be null (bias=False).  W, Wout: [rows][cols] reference layout.
+hipError_t fold_linear_bn(const float* W, const float* b, const float* gamma, const float* beta, const float* mean,
+                          const float* var, int rows, int cols, float eps, float* Wout, float* bout, hipStream_t s);
 
 }  // namespace tts

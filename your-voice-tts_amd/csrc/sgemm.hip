@@ -617,9 +617,10 @@ hipError_t sgemm_launch(const SGemmArgs& a, int role, hipStream_t s) {
 
 // Folded weights of the fused mel/prenet-1/stop GEMM (logical row-major [nmel+257][K], fp64
 // accumulation, rounded once):  rows [0,nmel) = W_mel;  [nmel, nmel+256) = W1 W_mel;
-// nmel+256 = [w_s_h | 0] + w_s_mel W_mel.  Biases b_mel, W1 b_mel, b_s + w_s_mel b_mel.
-__global__ void fold_mel_kernel(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
-                                int nmel, int K, int hdec, float* Wf, float* bf) {
+// nmel+256 = [w_s_h | 0] + w_s_mel W_mel.  Biases b_mel, W1 b_mel (+ b1: the BatchNorm prenet's
+// folded shift), b_s + w_s_mel b_mel.
+__global__ void fold_mel_kernel(const float* Wm, const float* bm, const float* W1, const float* b1, const float* ws,
+                                const float* bs, int nmel, int K, int hdec, float* Wf, float* bf) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int nrow = nmel + PRE_DIM + 1;
     if (i >= (int64_t)nrow * (K + 1)) return;
@@ -630,6 +631,7 @@ __global__ void fold_mel_kernel(const float* Wm, const float* bm, const float* W
     } else if (n < nmel + PRE_DIM) {
         const float* w1 = W1 + (int64_t)(n - nmel) * nmel;
         for (int m = 0; m < nmel; ++m) v += (double)w1[m] * (k < K ? Wm[(int64_t)m * K + k] : bm[m]);
+        if (k == K && b1) v += b1[n - nmel];
     } else {
         v = k < K ? (k < hdec ? ws[k] : 0.0) : bs[0];
         for (int m = 0; m < nmel; ++m) v += (double)ws[hdec + m] * (k < K ? Wm[(int64_t)m * K + k] : bm[m]);
@@ -640,11 +642,32 @@ __global__ void fold_mel_kernel(const float* Wm, const float* bm, const float* W
         bf[n] = (float)v;
 }
 
-hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* ws, const float* bs,
-                            int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s) {
+hipError_t fold_mel_weights(const float* Wm, const float* bm, const float* W1, const float* b1, const float* ws,
+                            const float* bs, int nmel, int K, int hdec, float* Wf, float* bf, hipStream_t s) {
     const int64_t total = (int64_t)(nmel + PRE_DIM + 1) * (K + 1);
-    hipLaunchKernelGGL(fold_mel_kernel, dim3((total + 255) / 256), dim3(256), 0, s, Wm, bm, W1, ws, bs, nmel, K, hdec,
-                       Wf, bf);
+    hipLaunchKernelGGL(fold_mel_kernel, dim3((total + 255) / 256), dim3(256), 0, s, Wm, bm, W1, b1, ws, bs, nmel, K,
+                       hdec, Wf, bf);
+    return hipGetLastError();
+}
+
+__global__ void fold_linear_bn_kernel(const float* W, const float* b, const float* gamma, const float* beta,
+                                      const float* mean, const float* var, int rows, int cols, float eps, float* Wout,
+                                      float* bout) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)rows * (cols + 1)) return;
+    const int n = i / (cols + 1), k = i % (cols + 1);  // k == cols: bias
+    const double sc = (double)gamma[n] / sqrt((double)var[n] + (double)eps);
+    if (k < cols)
+        Wout[(int64_t)n * cols + k] = (float)(sc * W[(int64_t)n * cols + k]);
+    else
+        bout[n] = (float)(sc * ((b ? (double)b[n] : 0.0) - mean[n]) + beta[n]);
+}
+
+hipError_t fold_linear_bn(const float* W, const float* b, const float* gamma, const float* beta, const float* mean,
+                          const float* var, int rows, int cols, float eps, float* Wout, float* bout, hipStream_t s) {
+    const int64_t total = (int64_t)rows * (cols + 1);
+    hipLaunchKernelGGL(fold_linear_bn_kernel, dim3((total + 255) / 256), dim3(256), 0, s, W, b, gamma, beta, mean, var,
+                       rows, cols, eps, Wout, bout);
     return hipGetLastError();
 }
 

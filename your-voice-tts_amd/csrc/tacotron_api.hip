@@ -179,6 +179,43 @@ tts_status fold_bn_key(tts_tacotron* t, const WeightMap& wm, const std::string& 
     return TTS_OK;
 }
 
+// prenet_type "bn" (common_layers.py:55-70; layers/tacotron.py:283-287): each decoder prenet layer is
+// Linear -> BatchNorm1d (eval, eps 1e-5) -> ReLU.  The BatchNorm is folded into the layer's weight
+// and bias here, and the folded tensors replace the linear_layer entries, so every consumer (the
+// prenet launches, the prenet-1/stop fold, the resident kernel's copies) reads them unchanged.
+tts_status fold_prenet_bn(tts_tacotron* t, WeightMap& wm, hipStream_t s) {
+    const int outs[2] = {T_PRE1, T_PRE2};
+    for (int l = 0; l < 2; ++l) {
+        const std::string p = "decoder.prenet.layers." + std::to_string(l) + ".";
+        if (!wm.m.count(p + "bn.weight")) {
+            if (l == 1 && wm.m.count("decoder.prenet.layers.0.bn.weight")) {
+                set_error("missing weight " + p + "bn.weight");
+                return TTS_ERR_INVALID;
+            }
+            continue;
+        }
+        auto it = wm.m.find(p + "linear_layer.weight");
+        if (it == wm.m.end() || it->second.second % outs[l]) {
+            set_error("missing or misshapen weight " + p + "linear_layer.weight");
+            return TTS_ERR_INVALID;
+        }
+        const int rows = outs[l], cols = (int)(it->second.second / rows);
+        GET(b, p + "linear_layer.bias", rows);
+        GET(g, p + "bn.weight", rows);
+        GET(be, p + "bn.bias", rows);
+        GET(mu, p + "bn.running_mean", rows);
+        GET(var, p + "bn.running_var", rows);
+        float *wf = nullptr, *bf = nullptr;
+        tts_status st = talloc(t, &wf, (size_t)rows * cols);
+        if (!st) st = talloc(t, &bf, rows);
+        if (st) return st;
+        TTS_HIP(fold_linear_bn(it->second.first, b, g, be, mu, var, rows, cols, 1e-5f, wf, bf, s));
+        wm.m[p + "linear_layer.weight"] = {wf, (int64_t)rows * cols};
+        wm.m[p + "linear_layer.bias"] = {bf, rows};
+    }
+    return TTS_OK;
+}
+
 tts_status make_cbhg(tts_tacotron* t, Cbhg& c, const WeightMap& wm, const std::string& p, int cin, int K, int p0,
                      int p1, hipStream_t s) {
     c.K = K;
@@ -954,7 +991,8 @@ tts_status tts_tacotron_create(const tts_tacotron_config* cfg, const tts_tensor*
     }
     WeightMap wm;
     for (int i = 0; i < n_tensors; ++i) wm.m[tensors[i].key] = {tensors[i].data, tensors[i].numel};
-    tts_status st = create_weights(t, wm, s);
+    tts_status st = fold_prenet_bn(t, wm, s);
+    if (!st) st = create_weights(t, wm, s);
     if (!st) st = create_workspace(t, s);
     if (!st) st = create_resident(t, wm, s);
     if (!st && hipStreamSynchronize(s) != hipSuccess) {

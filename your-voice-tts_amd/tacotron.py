@@ -40,8 +40,10 @@ class TacotronGST:
                  attn_norm="sigmoid", prenet_type="original", prenet_dropout=True, forward_attn=False,
                  trans_agent=False, forward_attn_mask=False, location_attn=True, separate_stopnet=True,
                  max_batch=64, max_len=256, seed=0):
-        if prenet_type != "original":
-            raise NotImplementedError("prenet_type 'bn' is not on the MI355X path (no BASELINE config uses it)")
+        if prenet_type not in ("original", "bn"):
+            # common_layers.py:66-75 builds no layers for any other value (its forward then fails)
+            raise ValueError(f"Unknown prenet_type {prenet_type!r}: expected 'original' or 'bn'")
+        self.prenet_type = prenet_type
         if attn_norm not in ("softmax", "sigmoid"):
             raise RuntimeError("Unknown value for attention norm type")
         if linear_dim != 1025 or mel_dim != 80:
@@ -64,7 +66,7 @@ class TacotronGST:
         self.training = False
         self.device = torch.device("cpu")
         self._spec = weights.tacotron_gst_spec(num_chars, num_speakers, r, self.memory_size, location_attn,
-                                               trans_agent, gst=self._gst)
+                                               trans_agent, gst=self._gst, prenet_bn=prenet_type == "bn")
         self._params = OrderedDict((k, torch.from_numpy(v)) for k, v in weights.generate(self._spec, seed).items())
         self._native = None  # (handle, key)
         self.last_lengths = None

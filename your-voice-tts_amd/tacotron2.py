@@ -41,8 +41,10 @@ class Tacotron2:
                  prenet_type="original", prenet_dropout=True, forward_attn=False, trans_agent=False,
                  forward_attn_mask=False, location_attn=True, separate_stopnet=True,
                  max_batch=64, max_len=256, seed=0):
-        if prenet_type != "original":
-            raise NotImplementedError("prenet_type 'bn' is not on the MI355X path (no BASELINE config uses it)")
+        if prenet_type not in ("original", "bn"):
+            # common_layers.py:66-75 builds no layers for any other value (its forward then fails)
+            raise ValueError(f"Unknown prenet_type {prenet_type!r}: expected 'original' or 'bn'")
+        self.prenet_type = prenet_type
         if attn_norm not in ("softmax", "sigmoid"):
             raise RuntimeError("Unknown value for attention norm type")
         self.num_chars = num_chars
@@ -58,7 +60,10 @@ class Tacotron2:
         self.max_len = max_len
         self.training = False
         self.device = torch.device("cpu")
-        self._spec = weights.tacotron2_spec(num_chars, num_speakers, r, location_attn, trans_agent)
+        # prenet_type "bn": LinearBN layers (common_layers.py:28-52), folded into the prenet weights
+        # and biases when the decoder handle is created (decoder_api.hip, fold_linear_bn)
+        self._spec = weights.tacotron2_spec(num_chars, num_speakers, r, location_attn, trans_agent,
+                                            prenet_bn=prenet_type == "bn")
         self._params = OrderedDict(
             (k, torch.from_numpy(v)) for k, v in weights.generate(self._spec, seed).items())
         self._native = None  # (decoder handle, postnet handle, key)

@@ -50,7 +50,7 @@ def _lin(fan_in, fan_out, gain=1.0):
 
 
 def tacotron2_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 1,
-                   location_attn: bool = False, trans_agent: bool = False):
+                   location_attn: bool = False, trans_agent: bool = False, prenet_bn: bool = False):
     """Ordered list of (key, shape, (kind, arg)) in the reference ``state_dict`` order."""
     s = []
     add = lambda k, shape, init: s.append((k, tuple(shape), init))
@@ -80,8 +80,15 @@ def tacotron2_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 1,
         add(f"encoder.lstm.bias_hh_l0{sfx}", (1024,), ("uniform", hb))
 
     nm = N_MEL * r
-    add("decoder.prenet.layers.0.linear_layer.weight", (PRENET, nm), _lin(nm, PRENET))
-    add("decoder.prenet.layers.1.linear_layer.weight", (PRENET, PRENET), _lin(PRENET, PRENET))
+    for i, nin in enumerate((nm, PRENET)):
+        add(f"decoder.prenet.layers.{i}.linear_layer.weight", (PRENET, nin), _lin(nin, PRENET))
+        if prenet_bn:  # LinearBN (common_layers.py:27-52): BatchNorm1d over the layer's outputs
+            pb = f"decoder.prenet.layers.{i}.bn."
+            add(pb + "weight", (PRENET,), ("range", (0.8, 1.2)))
+            add(pb + "bias", (PRENET,), ("uniform", 0.1))
+            add(pb + "running_mean", (PRENET,), ("uniform", 0.1))
+            add(pb + "running_var", (PRENET,), ("range", (0.5, 1.5)))
+            add(pb + "num_batches_tracked", (), ("zero_i64", None))
     ab = 1.0 / math.sqrt(ATT_RNN)
     add("decoder.attention_rnn.weight_ih", (4 * ATT_RNN, PRENET + ENC_DIM), ("uniform", ab))
     add("decoder.attention_rnn.weight_hh", (4 * ATT_RNN, ATT_RNN), ("uniform", ab))
@@ -129,7 +136,8 @@ def _default_linear(fan_in):
 
 
 def tacotron_gst_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 5, memory_size: int = 5,
-                      location_attn: bool = False, trans_agent: bool = False, gst: bool = True):
+                      location_attn: bool = False, trans_agent: bool = False, gst: bool = True,
+                      prenet_bn: bool = False):
     """Ordered (key, shape, init) table of the reference ``TacotronGST`` (models/tacotrongst.py:10-45;
     ``gst=False`` gives the plain ``Tacotron`` of models/tacotron.py:9-43): Tacotron ``Encoder`` /
     ``CBHG`` / ``Decoder`` / ``PostCBHG`` (layers/tacotron.py:7-489) and ``GST``
@@ -173,10 +181,12 @@ def tacotron_gst_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 5, m
                 add(f"{prefix}.highways.{i}.{n}.bias", (128,), _default_linear(128))
         gru(f"{prefix}.gru", 128, 128, True)
 
-    def prenet(prefix, nin, outs):
+    def prenet(prefix, nin, outs, with_bn=False):
         for i, (a, b) in enumerate(zip([nin] + outs[:-1], outs)):
             add(f"{prefix}.layers.{i}.linear_layer.weight", (b, a), _lin(a, b))
             add(f"{prefix}.layers.{i}.linear_layer.bias", (b,), _default_linear(a))
+            if with_bn:  # LinearBN (common_layers.py:28-52)
+                bn(f"{prefix}.layers.{i}.bn", b)
 
     prenet("encoder.prenet", 256, [256, 128])
     cbhg("encoder.cbhg.cbhg", 128, 16, [128, 128])
@@ -193,7 +203,7 @@ def tacotron_gst_spec(num_chars: int = 130, num_speakers: int = 0, r: int = 5, m
         add("gst.style_token_layer.attention.W_key.weight", (256, 64), _default_linear(64))
         add("gst.style_token_layer.attention.W_value.weight", (256, 64), _default_linear(64))
     mem = 80 * memory_size
-    prenet("decoder.prenet", mem, [256, 128])
+    prenet("decoder.prenet", mem, [256, 128], prenet_bn)  # prenet_type (layers/tacotron.py:283-287)
     hb = 1.0 / math.sqrt(256)
     add("decoder.attention_rnn.weight_ih", (768, 384), ("uniform", hb))
     add("decoder.attention_rnn.weight_hh", (768, 256), ("uniform", hb))
