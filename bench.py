@@ -654,10 +654,11 @@ def main():
             tf = flops / (kdom["mean_ms"] * 1e-3) / 1e12
             roofline["diagnostics"] = dict(
                 limiter="batched: one wave per frame (gl_iter_wave_kernel), fp64 VALU (~65% busy) and the "
-                        "vector-memory return path (TD ~74% busy); small batches: the persistent loop's "
-                        "per-iteration neighbour hand-offs. HBM traffic beyond the algorithmic bytes is the "
-                        "float32 windowed frames written by the iteration launch and read back by the "
-                        "overlap-add launch (float64 frames in the persistent loop)",
+                        "vector-memory return path (TD ~74% busy); HBM traffic beyond the algorithmic bytes "
+                        "is the float32 windowed frames written by the iteration launch and read back by the "
+                        "overlap-add launch. Batch 1 (persistent loop): per iteration ~1.8 us of neighbour "
+                        "hand-off (tagged float32 granules, two ping-pong slots) and ~4 us of fp64 FFT + "
+                        "spectrum on one wave per SIMD (latency-bound LDS passes)",
                 fp64_flops_per_launch=flops, fp64_tflops=tf, fp64_vector_frac=tf / FP64_VECTOR_PEAK_TF,
                 traffic_gbs=(traffic / (kdom["mean_ms"] * 1e-3) / 1e9) if traffic else None)
         if dom == "resident_decoder":

@@ -763,10 +763,14 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.mel_hist = d->mel_hist; ra.stop_hist = d->stop_hist; ra.align_hist = d->align_hist;
         ra.gran = d->gran;
         ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
-        d->res_salt = (d->res_salt + 1) & 0x3FFFF;
+        // direct (pipelined) runs skip the per-launch clear and rely on the 18-bit tag salt: on a
+        // salt wrap a granule left 2^18 launches back could match a current wait, so clear then
+        bool wrapped = false;
+        d->res_salt = res_next_salt(d->res_salt, &wrapped);
         ra.salt = d->res_salt;
         d->last_ra = ra;
-        if (!direct) TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
+        if (!direct || wrapped)
+            TTS_HIP(hipMemsetAsync(d->gran, 0, sizeof(unsigned long long) * (2 * GR_TOTAL + 2), s));
         if (timed) TTS_HIP(hipEventRecord(d->ev_t0, s));
         bool launched = false;
         TTS_HIP(launch_resident(ra, s, &launched));

@@ -1081,6 +1081,9 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     constexpr int PN = NFFT / GL_THREADS;
     // ---- iteration-invariant operands
     const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
+    // the FFT twiddles in registers for the whole loop (one wave per SIMD: no occupancy to lose;
+    // the per-pass table reads of fft1024_regs_gtw cost 0.25 us of each forward FFT here)
+    const FftTw ftw = load_fft_tw(a.c.tw);
     double2 tk[PK];
     double sk[PK];
 #pragma unroll
@@ -1243,7 +1246,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             else v[i >> 1].x = wi[i] * (double)yv;
         }
         GL_PHASE(1)
-        const double2* Z = fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw);
+        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
         GL_PHASE(2)
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
@@ -1277,7 +1280,7 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double2 O = cmul(D, cconj(tk[i]));
             v[i] = double2{E.x - O.y, E.y + O.x};
         }
-        fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
+        fft1024_regs<true, true>(v, buf0, buf1, ftw);
         GL_PHASE(4)
         if (b == 0 && f == p.drop_f) return;  // fault injection only: never stores iteration 1
         // ---- the frame's samples, tagged with the next iteration: XCD-local (workgroup-scope store,
