@@ -492,6 +492,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
         }
         RES_MARK(5);
+        float wdef = 0.f;  // attention CU: this thread's weight of the step (stored after h_dec is published)
         // 7) attention step.  After the forward mask the previous alpha is nonzero only on the
         //    previous window S' = W(n') = {(n'-2) mod L} + [n'-1, n'+2], so every position outside
         //    C = W(n) + S' + (S'+1) has mix = 1e-8 exactly and anj = 1e-8 * sigmoid <= 1e-8: the
@@ -626,10 +627,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (tid == 0) { RES_EV(t, 11) }
             RES_MARK(8);
             // off the critical path: this step's alpha (next step's prev_alpha) and alignment row
-            const int j = tid;
-            const float w = j < L ? weight(j) : 0.f;
-            if (j < L) anew[j] = w;
-            if (att_log && t < a.hist_cap && j < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + j] = w;
+            wdef = tid < L ? weight(tid) : 0.f;
             n_prev = n;
             n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: h_att wait)
 #pragma unroll 2
@@ -675,6 +673,13 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 publish(G + GR_HDEC + 4 * c + tid, E + 5, h);
                 if (tid == 0) { RES_EV(t, 5) }
             }
+        }
+        // the attention CU's alpha (next step's prev_alpha) and alignment row, after its h_dec
+        // publish: the eight attention CUs are the h_dec edge's last publishers
+        if (att_cu) {
+            float* anew = abuf + ((t & 1) ^ 1) * RES_LMAX;
+            if (tid < L) anew[tid] = wdef;
+            if (att_log && t < a.hist_cap && tid < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + tid] = wdef;
         }
         // 10) gather h_dec_t
         {
