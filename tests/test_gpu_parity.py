@@ -612,3 +612,16 @@ def test_prenet_bn_batch_vs_reference(B):
     out = m.inference_batch(None, enc=enc.cuda(), lens=[len(z["ids"]) for z in zs])
     for b, z in enumerate(zs):
         _check_decoder(out, b, z)
+
+
+def test_location_attention_batch_vs_reference():
+    """Location-sensitive attention with forward attention and the transition agent (the multi-launch
+    path: energies with the location term as query-launch partials, the next step's location
+    features from the attention launch) in a batch of three, against the reference run."""
+    z = golden("t2_loc_fwd_ta_L24")
+    m = _model(golden_flags(z))
+    L = len(z["ids"])
+    enc = torch.from_numpy(z["enc"])[None].repeat(3, 1, 1).cuda()
+    out = m.inference_batch(None, enc=enc, lens=[L] * 3)
+    for b in range(3):
+        _check_decoder(out, b, z)

@@ -38,6 +38,8 @@ __global__ void decoder_init_kernel(const InitArgs a) {
         a.att_w[o] = 0.f;
         a.att_cum[o] = 0.f;
     }
+    if (a.locf)  // location_conv of zero attention state
+        for (int k = threadIdx.x; k < NLOC * a.Lcap; k += blockDim.x) a.locf[(int64_t)b * NLOC * a.Lcap + k] = 0.f;
     if (threadIdx.x == 0) {
         a.u[b] = 0.5f;
         a.win_idx[b] = -1;
@@ -160,7 +162,8 @@ hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lm
 // ------------------------------------------------------------------ attention step
 // One workgroup of 1024 threads per sentence; thread j owns encoder position j (L <= 1024).
 // The reduction area `red` holds at least one float per thread (context partials).
-__host__ __device__ static inline int red_stride(int Lcap) { return Lcap > ATT_THREADS / ATT_WAVES ? Lcap : ATT_THREADS / ATT_WAVES; }
+// (at least 256: the QE form's context reduction holds 8 parts x 512 channels)
+__host__ __device__ static inline int red_stride(int Lcap) { return Lcap > 256 ? Lcap : 256; }
 size_t attention_smem_bytes(int Lcap, int location) {
     size_t f = 2 * ADIM + 3 * (size_t)Lcap + ATT_WAVES * (size_t)red_stride(Lcap) + 4 * ATT_WAVES;
     if (location) f += 2 * ((size_t)Lcap + 32) + (size_t)NLOC * Lcap + ADIM * NLOC;
@@ -204,7 +207,9 @@ __device__ __forceinline__ Red block_reduce(float s, float m, float y, int i, fl
 
 // ENC_ = encoder width, HATT_ = attention-RNN width (Tacotron2: 512 / 1024; Tacotron, TacotronGST:
 // 256 / 256, layers/tacotron.py:290-300).
-template <int ENC_, int HATT_>
+// QE: Tacotron2's form, the energies as QE_TILES partial sums per position from query_energy_kernel
+// (location term included) and the next step's location features computed at the end.
+template <int ENC_, int HATT_, bool QE>
 __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     // the transposed weight, h_att a broadcast read); the 8 partials meet in LDS in slice order
     constexpr int QSL = ATT_THREADS / ADIM, KS = HATT_ / QSL;
     float qpart = 0.f;
-    if (a.wqT) {
+    if (!QE && a.wqT) {
         const int d = tid & (ADIM - 1), ks = tid / ADIM;
         const float* w = a.wqT + (int64_t)ks * KS * ADIM + d;
         const float* h = a.h_att + (int64_t)b * HATT_ + ks * KS;
@@ -244,13 +249,20 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         qpart = s0 + s1;
     }
     const float aold_j = (a.forward_attn && in) ? a.alpha[row + j] : 0.f;
+    // Tacotron2: the energies arrive as QE_TILES partial sums per position from query_energy_kernel
+    // (location term included), and this launch leaves the next step's location features
+    constexpr bool qe = QE;
+    float ep[QE_TILES];
+#pragma unroll
+    for (int k = 0; k < QE_TILES; ++k) ep[k] = (qe && in) ? a.epart[((int64_t)b * QE_TILES + k) * Lc + j] : 0.f;
+    const float cum_old = (qe && a.locf && in) ? a.att_cum[row + j] : 0.f;
     const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
     const int d0 = wave * DPW;
     float pv0[DPW], pv1[DPW];
 #pragma unroll
     for (int dd = 0; dd < DPW; ++dd) {
-        pv0[dd] = lane < L ? Pt[(int64_t)(d0 + dd) * Lc + lane] : 0.f;
-        pv1[dd] = lane + 64 < L ? Pt[(int64_t)(d0 + dd) * Lc + lane + 64] : 0.f;
+        pv0[dd] = !qe && lane < L ? Pt[(int64_t)(d0 + dd) * Lc + lane] : 0.f;
+        pv1[dd] = !qe && lane + 64 < L ? Pt[(int64_t)(d0 + dd) * Lc + lane + 64] : 0.f;
     }
     const float* encb = a.enc + row * ENC_;
     const int cx = sparse ? (n - 2 + L) % L : 0;
@@ -277,7 +289,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     float* locf = cat + 2 * (Lc + 32);
     float* wd = locf + NLOC * Lc;
 
-    if (a.wqT) {
+    if (!QE && a.wqT) {
         // the partials go through their own scratch at the end of the allocation; slice sums in
         // order 0..7
         float* qsc = a.location_attn ? wd + ADIM * NLOC : cat;
@@ -294,7 +306,9 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     if (tid < ADIM) q[tid] = qv;
     else if (tid < 2 * ADIM) vv[tid - ADIM] = qv;
     if (a.forward_attn && in) aold[j] = aold_j;
-    if (a.location_attn) {
+    if (qe && a.locf)  // location_conv weights for the next step's features (end of this launch)
+        for (int i = tid; i < NLOC * 2 * KLOC; i += blockDim.x) wd[i] = a.loc_conv[i];
+    if (a.location_attn && !qe) {
         // attention_cat = [attention_weights; attention_weights_cum] (common_layers.py:167-169),
         // zero padded by (31-1)/2 = 15 on both sides for location_conv (:90-96).
         for (int c = tid; c < L + 2 * 15; c += blockDim.x) {
@@ -306,7 +320,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         for (int i = tid; i < ADIM * NLOC; i += blockDim.x) wd[i] = a.loc_dense[i];
     }
     __syncthreads();
-    if (a.location_attn) {
+    if (a.location_attn && !qe) {
         for (int idx = tid; idx < NLOC * L; idx += blockDim.x) {
             const int f = idx / L, jj = idx - f * L;
             const float* cw = a.loc_conv + f * 2 * KLOC;
@@ -319,7 +333,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     }
     // ---- energy partials e_j = v . tanh(pq [+ loc_j] + P_j) + b_v (common_layers.py:166-182):
     // wave w owns d in [8w, 8w+8), lanes own positions
-    for (int j0 = 0; j0 < L; j0 += 64) {
+    for (int j0 = 0; j0 < L && !qe; j0 += 64) {
         const int jj = j0 + lane;
         if (jj < L) {
             float s = 0.f;
@@ -340,7 +354,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     }
     __syncthreads();
     float e = -INFINITY;
-    if (in) {
+    if (in && qe) {
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < QE_TILES; ++k) s += ep[k];
+        e = s + vb;
+    } else if (in) {
         float s = 0.f;
         for (int w = 0; w < ATT_WAVES; ++w) s += red[w * Lc + j];
         e = s + vb;
@@ -369,7 +388,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         const Red r = block_reduce(sg, -INFINITY, 0.f, 0, scr);
         al = sg / r.s;
     }
-    if (a.location_attn && in) a.att_cum[row + j] += al;  // update_location_attention (:163-164)
+    // update_location_attention (:163-164)
+    const float cum_new = cum_old + al;
+    if (a.location_attn && in) {
+        if (qe && a.locf) a.att_cum[row + j] = cum_new;
+        else a.att_cum[row + j] += al;
+    }
 
     float w = al;
     if (a.forward_attn) {
@@ -403,6 +427,45 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     __syncthreads();
     // ---- outputs: attention weights (alpha or alignment), history, stop-rule tail (tacotron2.py:268)
     if (a.location_attn && in) a.att_w[row + j] = w;
+    if (qe && a.locf) {
+        // the next step's location features: location_conv over [attention_weights;
+        // attention_weights_cum] = [w; cum_new] zero-padded by 15 (common_layers.py:90-104, 167-171),
+        // channel 0's taps then channel 1's, the order of the launch-local evaluation
+        for (int c = tid; c < L + 2 * 15; c += blockDim.x) {  // cat: [2][Lc + 32]
+            const int p = c - 15;
+            const bool ok = p >= 0 && p < L;
+            cat[c] = ok ? wts[p] : 0.f;
+        }
+        if (in) cat[Lc + 32 + 15 + j] = cum_new;
+        if (tid < 15) {
+            cat[Lc + 32 + tid] = 0.f;
+            cat[Lc + 32 + 15 + L + tid] = 0.f;
+        }
+        __syncthreads();  // (wd holds the conv weights [f][c][k], staged at the start)
+        // as an MFMA GEMM: out[j][f] = sum_kk A[j][kk] B[kk][f], kk = 31 c + k < 62 (padded to 64),
+        // A[j][kk] = cat[c][j + k] (im2col from LDS), B[kk][f] = W[f][kk]; tiles of 16 positions x
+        // 16 filters, one per wave at a time, the taps in order (channel 0's, then channel 1's)
+        float* lo = a.locf + (int64_t)b * NLOC * Lc;
+        const int ntile = (L + 15) / 16 * 2;
+        for (int tl = wave; tl < ntile; tl += ATT_WAVES) {
+            const int pt = tl >> 1, ft = tl & 1;
+            const int jA = pt * 16 + (lane & 15), fB = ft * 16 + (lane & 15);
+            floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s4 = 0; s4 < 16; ++s4) {
+                const int kk = 4 * s4 + (lane >> 4);
+                const int c = kk >= KLOC ? 1 : 0, k = kk - c * KLOC;
+                const float av = kk < 2 * KLOC && jA < L ? cat[c * (Lc + 32) + jA + k] : 0.f;
+                const float bv = kk < 2 * KLOC ? wd[fB * 2 * KLOC + kk] : 0.f;
+                acc = mfma16x16x4(av, bv, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = pt * 16 + 4 * (lane >> 4) + r;
+                if (jj < L) lo[(int64_t)fB * Lc + jj] = acc[r];
+            }
+        }
+    }
     if (!a.done[b] && t < a.hist_cap && a.align_hist)
         for (int jj = tid; jj < a.Lalign; jj += blockDim.x)
             a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + jj] = jj < L ? wts[jj] : 0.f;
@@ -431,6 +494,35 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             for (int k = 0; k < 4; ++k)
                 if (clo + k <= chi) ctx += wts[clo + k] * erow[k];
             if (cx > chi) ctx += wts[cx] * ex;
+        }
+    } else if (QE) {
+        // float4 channel groups x PARTS interleaved position sets; each thread issues a batch of 8
+        // rows' loads together (the rows stream from L2 / MALL: one round trip per batch, not per
+        // row), then the parts meet in LDS and are summed in part order
+        constexpr int D4 = ENC_ / 4, PARTS = ATT_THREADS / D4;
+        static_assert(PARTS * ENC_ <= ATT_WAVES * 256, "context partials fit the reduction area");
+        const int d4 = tid % D4, part = tid / D4;
+        float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+        for (int j0 = part; j0 < L; j0 += 8 * PARTS) {
+            float4 ev[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m)
+                ev[m] = *reinterpret_cast<const float4*>(encb + (int64_t)min(j0 + m * PARTS, L - 1) * ENC_ + 4 * d4);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const float wv = j0 + m * PARTS < L ? wts[j0 + m * PARTS] : 0.f;
+                acc.x += wv * ev[m].x;
+                acc.y += wv * ev[m].y;
+                acc.z += wv * ev[m].z;
+                acc.w += wv * ev[m].w;
+            }
+        }
+        *reinterpret_cast<float4*>(red + part * ENC_ + 4 * d4) = acc;
+        __syncthreads();
+        if (tid < ENC_) {
+            ctx = red[tid];
+#pragma unroll
+            for (int p = 1; p < PARTS; ++p) ctx += red[p * ENC_ + tid];
         }
     } else {
         // PARTS interleaved position sets per channel, summed in part order
@@ -607,6 +699,10 @@ __global__ __launch_bounds__(1024) void query_energy_kernel(const QEArgs a) {
     const float* Pt = a.Pt + ((int64_t)b * ADIM + tile * 16) * Lc;
 #pragma unroll
     for (int dd = 0; dd < 16; ++dd) pt[dd] = (a.energies && j < Lc) ? Pt[(int64_t)dd * Lc + j] : 0.f;
+    // this tile's 16 rows of location_dense (LDS, [d][f] padded against bank conflicts)
+    __shared__ float wld[16][NLOC + 1];
+    const bool loc = a.energies && a.locf;
+    if (loc && tid < 16 * NLOC) wld[tid / NLOC][tid % NLOC] = a.loc_dense[(tile * 16 + tid / NLOC) * NLOC + tid % NLOC];
     const float4* Wp = reinterpret_cast<const float4*>(a.Wq) + ((size_t)tile * NCH + wave * CPW) * 64 + lane;
     const float* hb = a.h + (int64_t)b * HATT + (lane >> 4) * 4;
     float4 wv[CPW], xv[CPW];
@@ -644,7 +740,36 @@ __global__ __launch_bounds__(1024) void query_energy_kernel(const QEArgs a) {
     }
     if (!a.energies) return;
     __syncthreads();
-    if (j < L) {
+    if (loc) {
+        // get_location_attention (common_layers.py:166-176): tanh(processed_query +
+        // location_dense(location_conv(attention_cat)) + processed_inputs), summed in that order.
+        // location_dense as an MFMA GEMM per 16 positions: C[j][d] = sum_f locf[f][j] W[d][f]
+        // (lane: positions j0 + 4 (lane >> 4) + r, dim lane & 15), then the 16 dims' v . tanh
+        // summed across each 16-lane row
+        const int d = lane & 15;
+        const float vd = a.v[tile * 16 + d], qd = qs[d];
+        const float* lp = a.locf + (int64_t)b * NLOC * Lc;
+        const float* Pd = a.Pt + ((int64_t)b * ADIM + tile * 16 + d) * Lc;
+        for (int j0 = wave * 16; j0 < L; j0 += 16 * 16) {
+            floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+            const int jA = min(j0 + (lane & 15), L - 1);
+#pragma unroll
+            for (int s4 = 0; s4 < NLOC / 4; ++s4) {
+                const int f = 4 * s4 + (lane >> 4);
+                acc = mfma16x16x4(lp[(int64_t)f * Lc + jA], wld[d][f], acc);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jj = j0 + 4 * (lane >> 4) + r;
+                float e = vd * tanh_fast((qd + acc[r]) + Pd[min(jj, L - 1)]);
+                e += __shfl_xor(e, 1, 64);
+                e += __shfl_xor(e, 2, 64);
+                e += __shfl_xor(e, 4, 64);
+                e += __shfl_xor(e, 8, 64);
+                if (d == 0 && jj < L) a.epart[((int64_t)b * QE_TILES + tile) * Lc + jj] = e;
+            }
+        }
+    } else if (j < L) {
         float e = 0.f;
 #pragma unroll
         for (int dd = 0; dd < 16; ++dd) e += a.v[tile * 16 + dd] * tanh_fast(qs[dd] + pt[dd]);
@@ -677,11 +802,14 @@ hipError_t transpose_f32(const float* src, int rows, int cols, float* dst, hipSt
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (attention_fast(a)) {
         hipLaunchKernelGGL(attention_fm_kernel, dim3(a.B), dim3(ATT_THREADS), attention_fm_smem_bytes(a.Lcap), s, a);
+    } else if (a.enc_dim == ENC && a.epart) {
+        hipLaunchKernelGGL((attention_kernel<ENC, HATT, true>), dim3(a.B), dim3(ATT_THREADS),
+                           attention_smem_bytes(a.Lcap, a.location_attn), s, a);
     } else if (a.enc_dim == ENC) {
-        hipLaunchKernelGGL((attention_kernel<ENC, HATT>), dim3(a.B), dim3(ATT_THREADS),
+        hipLaunchKernelGGL((attention_kernel<ENC, HATT, false>), dim3(a.B), dim3(ATT_THREADS),
                            attention_smem_bytes(a.Lcap, a.location_attn), s, a);
     } else if (a.enc_dim == 256) {
-        hipLaunchKernelGGL((attention_kernel<256, 256>), dim3(a.B), dim3(ATT_THREADS),
+        hipLaunchKernelGGL((attention_kernel<256, 256, false>), dim3(a.B), dim3(ATT_THREADS),
                            attention_smem_bytes(a.Lcap, a.location_attn), s, a);
     } else {
         return hipErrorInvalidValue;
@@ -691,10 +819,13 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
 
 hipError_t attention_prepare(int Lcap, int location) {
     const int bytes = (int)attention_smem_bytes(Lcap, location);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<ENC, HATT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<ENC, HATT, true>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<256, 256>),
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<ENC, HATT, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<256, 256, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_fm_kernel),

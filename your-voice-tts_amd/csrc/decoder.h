@@ -38,7 +38,10 @@ struct AttnArgs {
     const float* enc;      // [B][Lcap][enc_dim]
     const int* lens;       // [B]
     const float* h_att;    // [B][query width] this step's attention-RNN output
-    const float* epart;    // [B][ADIM/16][Lcap] energy partials from query_energy_kernel (fast path)
+    const float* epart;    // [B][ADIM/16][Lcap] energy partials from query_energy_kernel (Tacotron2: every
+                           // attention configuration; null: attention_kernel evaluates the energies)
+    float* locf;           // with epart and location_attn: [B][NLOC][Lcap] the NEXT step's location
+                           // features (location_conv over [att_w; att_cum]), written at the step's end
     // state
     float* alpha;          // [B][Lcap]
     float* att_w;          // [B][Lcap]
@@ -74,6 +77,7 @@ struct InitArgs {
     float* mem;
     float* alpha; float* att_w; float* att_cum; float* u; int* win_idx; int* nidx; float* tail;
     int* flag1; int* count; int* done; int* n_steps; int* step; int* n_active;
+    float* locf;  // [B][NLOC][Lcap] step-0 location features (zero attention state: zeros), or null
     // batch-1 resident runs: the cached go-frame prenet row copied into pre1 (null: the prenet GEMM
     // runs), and a granule array zeroed by INIT_ZERO_BLOCKS extra workgroups (null: none)
     const float* pre1_go; float* pre1;
@@ -95,6 +99,8 @@ struct QEArgs {
     const int* lens;
     int Lcap;
     int energies;       // 0: q only (the general attention kernel evaluates the energies itself)
+    const float* locf;       // [B][NLOC][Lcap] this step's location features, or null (no location layer)
+    const float* loc_dense;  // [ADIM][NLOC] location_dense weight (with locf)
     float* q;           // [B][ADIM]
     float* epart;       // [B][QE_TILES][Lcap]
     const int* step;    // int2 {step, n_active}

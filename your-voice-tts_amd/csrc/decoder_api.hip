@@ -57,7 +57,9 @@ struct tts_decoder {
     // batched GEMM (sgemm.h: Seg::pf).  Null when max_batch <= 16.
     int ntf = 0;
     float *xaf = nullptr, *hattf = nullptr, *hdecf = nullptr, *pre1f = nullptr;
-    bool fast_attention = false;  // attention_uses_epart(): energies evaluated in the query launch
+    bool fast_attention = false;  // attention_uses_epart(): the synthesis configuration's attention
+                                  // launch (attention_fm_kernel) and the resident decoder
+    float* locf = nullptr;        // location_attn: [Bcap][NLOC][Lcap] location features of the next step
     // resident (persistent, one launch per sentence) batch-1 decoder, resident.h
     bool resident = false;
     ResWeights rw{};
@@ -223,7 +225,10 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
     {
         QEArgs a{};
         a.Wq = d->W_q; a.h = h_att_cur; a.v = d->v; a.Pt = d->Pt; a.lens = d->lens; a.Lcap = d->Lcap;
-        a.energies = d->fast_attention ? 1 : 0;
+        // every configuration: the energies as QE_TILES partials per position (with the location
+        // term from the previous attention launch's features)
+        a.energies = 1;
+        a.locf = d->locf; a.loc_dense = d->loc_dense;
         a.q = d->q; a.epart = d->epart; a.step = st_cur;
         MARK();
         TTS_HIP(launch_query_energy(a, B, s));
@@ -239,7 +244,7 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         a.loc_conv = d->loc_conv; a.loc_dense = d->loc_dense;
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
         a.h_att = h_att_cur;
-        a.epart = d->epart;
+        a.epart = d->epart; a.locf = d->locf;
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
         a.nidx = d->nidx; a.tail = d->tail;
         a.ctx = ctx_cur;  // kernel writes ctx[b*XA + d]
@@ -542,6 +547,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         CK(dmalloc(d, &d->pre1f, rows * PRE));
     }
     CK(dmalloc(d, &d->epart, (size_t)Bc * QE_TILES * Lc));
+    if (cfg->location_attn) CK(dmalloc(d, &d->locf, (size_t)Bc * NLOC * Lc));
     CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
     CK(dmalloc(d, &d->att_cum, (size_t)Bc * Lc));
@@ -617,6 +623,7 @@ tts_status tts_decoder_run_teacher(tts_decoder* d, const float* enc, const int32
     ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
     ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
     ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
+    ia.locf = d->locf;
     ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
     ia.step = d->state; ia.n_active = d->state + 1;
     TTS_HIP(launch_decoder_init(ia, s));
@@ -695,6 +702,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     ia.h_att = d->h_att; ia.h_pstride = (int64_t)d->Bcap * HATT; ia.c_att = d->c_att;
     ia.h_dec = d->h_dec; ia.c_dec = d->c_dec; ia.xa = d->xa; ia.xa_pstride = (int64_t)d->Bcap * XA; ia.mem = d->mem;
     ia.alpha = d->alpha; ia.att_w = d->att_w; ia.att_cum = d->att_cum; ia.u = d->u; ia.win_idx = d->win_idx;
+    ia.locf = d->locf;
     ia.nidx = d->nidx; ia.tail = d->tail; ia.flag1 = d->flag1; ia.count = d->count; ia.done = d->done; ia.n_steps = d->n_steps;
     ia.step = d->state; ia.n_active = d->state + 1;
     if (keep) {

@@ -93,7 +93,7 @@ struct tts_tacotron {
     int Bcap = 0, Lcap = 0, hist_cap = 0;
     float *denc = nullptr, *Pt = nullptr, *h_att = nullptr, *h1 = nullptr, *h2 = nullptr, *xa = nullptr;
     float *mem = nullptr, *pre1 = nullptr, *q = nullptr, *din = nullptr, *d1 = nullptr, *d2 = nullptr;
-    float *epart = nullptr, *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
+    float *alpha = nullptr, *att_w = nullptr, *att_cum = nullptr, *u = nullptr, *tail = nullptr;
     int *lens = nullptr, *win_idx = nullptr, *nidx = nullptr, *flag1 = nullptr, *count = nullptr, *done = nullptr;
     int *n_steps = nullptr, *state = nullptr, *host_flags = nullptr;
     float *mel_hist = nullptr, *stop_hist = nullptr, *align_hist = nullptr;
@@ -532,8 +532,7 @@ tts_status enqueue_step(tts_tacotron* t, int B, int Lmax, int max_steps, int p, 
         a.loc_conv = t->loc_conv; a.loc_dense = t->loc_dense;
         a.q = t->q; a.Pt = t->Pt; a.enc = t->denc; a.lens = t->lens;
         a.wqT = t->fused_query ? t->W_qT : nullptr;
-        a.h_att = h_att_cur;
-        a.epart = t->epart;
+        a.h_att = h_att_cur;  // (no epart: the launch evaluates the energies, attention_kernel<256, 256>)
         a.alpha = t->alpha; a.att_w = t->att_w; a.att_cum = t->att_cum; a.u = t->u; a.win_idx = t->win_idx;
         a.nidx = t->nidx; a.tail = t->tail;
         a.ctx = ctx_cur;
@@ -846,7 +845,6 @@ tts_status create_workspace(tts_tacotron* t, hipStream_t s) {
     CK(talloc(t, &t->din, (size_t)Bc * T_DEC));
     CK(talloc(t, &t->d1, (size_t)Bc * T_DEC));
     CK(talloc(t, &t->d2, (size_t)Bc * T_DEC));
-    CK(talloc(t, &t->epart, (size_t)Bc * QE_TILES * Lc));
     CK(talloc(t, &t->alpha, (size_t)Bc * Lc));
     CK(talloc(t, &t->att_w, (size_t)Bc * Lc));
     CK(talloc(t, &t->att_cum, (size_t)Bc * Lc));
