@@ -205,6 +205,30 @@ __device__ __forceinline__ Red block_reduce(float s, float m, float y, int i, fl
     return r;
 }
 
+// Block sum / max of one value over the ATT_WAVES waves: DPP wave reductions, one LDS round, the
+// waves folded in order (the QE form's reductions: one cross-lane chain instead of block_reduce's
+// four shuffle chains)
+__device__ __forceinline__ float block_sum16(float v, float* scr) {
+    v = wave_sum_dpp(v);
+    if ((threadIdx.x & 63) == 0) scr[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float r = scr[0];
+#pragma unroll
+    for (int k = 1; k < ATT_WAVES; ++k) r += scr[k];
+    __syncthreads();
+    return r;
+}
+__device__ __forceinline__ float block_max16(float v, float* scr) {
+    v = wave_max_dpp(v);
+    if ((threadIdx.x & 63) == 0) scr[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float r = scr[0];
+#pragma unroll
+    for (int k = 1; k < ATT_WAVES; ++k) r = fmaxf(r, scr[k]);
+    __syncthreads();
+    return r;
+}
+
 // ENC_ = encoder width, HATT_ = attention-RNN width (Tacotron2: 512 / 1024; Tacotron, TacotronGST:
 // 256 / 256, layers/tacotron.py:290-300).
 // QE: Tacotron2's form, the energies as QE_TILES partial sums per position from query_energy_kernel
@@ -378,7 +402,14 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     }
     // ---- normalisation (common_layers.py:239-245)
     float al = 0.f;
-    if (a.attn_norm == 0) {
+    if (QE && a.attn_norm == 0) {
+        const float mx = block_max16(e, scr);
+        const float exj = in ? expf(e - mx) : 0.f;
+        al = exj / block_sum16(exj, scr);
+    } else if (QE) {
+        const float sg = in ? sigmoidf_(e) : 0.f;
+        al = sg / block_sum16(sg, scr);
+    } else if (a.attn_norm == 0) {
         const Red r1 = block_reduce(0.f, e, 0.f, 0, scr);
         const float exj = in ? expf(e - r1.m) : 0.f;
         const Red r2 = block_reduce(exj, -INFINITY, 0.f, 0, scr);
@@ -406,7 +437,8 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         }
         float denom;
         if (sparse) {
-            const Red r = block_reduce(0.f, in ? anj : -INFINITY, 0.f, 0, scr);
+            const Red r = QE ? Red{0.f, block_max16(in ? anj : -INFINITY, scr), 0.f, 0}
+                             : block_reduce(0.f, in ? anj : -INFINITY, 0.f, 0, scr);
             // Python slicing of :211-213 incl. the negative-index wrap for n < 2
             if (in && ((j >= n + 3) || (n >= 1 ? j < n - 1 : j < L - 1))) anj = 0.f;
             if (j == cx) anj = 0.01f * r.m;
@@ -418,7 +450,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             for (int p = clo; p <= chi; ++p) denom += an[p];
             if (cx > chi) denom += an[cx];
         } else {
-            denom = block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr).s;
+            denom = QE ? block_sum16(in ? anj : 0.f, scr) : block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr).s;
         }
         w = in ? anj / denom : 0.f;
         if (in) a.alpha[row + j] = w;
@@ -558,8 +590,8 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         const float* h = a.h_att + (int64_t)b * HATT_;
         float p = tid < ENC_ ? a.ta_w[tid] * ctx : 0.f;
         if (tid < HATT_) p += a.ta_w[ENC_ + tid] * h[tid];
-        const Red r = block_reduce(p, -INFINITY, 0.f, 0, scr);
-        if (tid == 0) a.u[b] = sigmoidf_(r.s + a.ta_b[0]);
+        const float ts = QE ? block_sum16(p, scr) : block_reduce(p, -INFINITY, 0.f, 0, scr).s;
+        if (tid == 0) a.u[b] = sigmoidf_(ts + a.ta_b[0]);
     }
 }
 
