@@ -235,7 +235,12 @@ __device__ __forceinline__ float block_max16(float v, float* scr) {
 // (location term included) and the next step's location features computed at the end.
 template <int ENC_, int HATT_, bool QE>
 __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a) {
-    const int b = blockIdx.x;
+    // QE: ATT_SPLIT workgroups per sentence (blockIdx.x = slice ks): each recomputes the weights
+    // (cheap), computes 128 context channels and a quarter of the location-feature tiles; slice 0
+    // writes the per-position state (into the other parity slot: the slices read the old one)
+    constexpr int ASPLIT = QE ? ATT_SPLIT : 1;
+    const int ks = QE ? blockIdx.x : 0;
+    const int b = QE ? blockIdx.y : blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int Lc = a.Lcap;
     const int64_t row = (int64_t)b * Lc;
@@ -243,14 +248,31 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     // ---- phase 0: every load that depends only on kernel arguments is issued up front, so the
     // kernel pays one memory round trip before computing (latency-bound at batch 1)
     const int2 st = *reinterpret_cast<const int2*>(a.step);  // {step, n_active}
+    const int par = QE ? (st.x & 1) : 0;
+    const float* alpha_rd = a.alpha + (QE ? par * a.sstride : 0);
+    float* alpha_wr = a.alpha + (QE ? (par ^ 1) * a.sstride : 0);
+    const float* cum_rd = a.att_cum + (QE ? par * a.sstride : 0);
+    float* cum_wr = a.att_cum + (QE ? (par ^ 1) * a.sstride : 0);
+    const int* nidx_rd = a.nidx + (QE ? par * a.istride : 0);
+    int* nidx_wr = a.nidx + (QE ? (par ^ 1) * a.istride : 0);
+    const int* win_rd = a.win_idx + (QE ? par * a.istride : 0);
+    int* win_wr = a.win_idx + (QE ? (par ^ 1) * a.istride : 0);
     const int L = a.lens[b];
     const int j = tid;  // this thread's encoder position
     const bool in = j < L;
     // forward attention + mask: after the mask at most (n-2)%L and [n-1, n+2] are nonzero, where
     // n = argmax(prev_alpha) was carried from the previous step; the context needs only those rows
     const bool sparse = a.forward_attn && a.forward_attn_mask;
-    const int n = sparse ? a.nidx[b] : 0;
-    const float u = a.forward_attn ? a.u[b] : 0.f;
+    const int n = sparse ? nidx_rd[b] : 0;
+    float u = a.forward_attn ? a.u[b] : 0.f;
+    // QE + transition agent: u = sigmoid(ta([context, query])) of the previous step (:220-222),
+    // evaluated here from that step's context and attention-RNN output (step 0: the initial 0.5)
+    const bool ta_here = QE && a.forward_attn && a.trans_agent && st.x > 0;
+    float ta_p = 0.f;
+    if (ta_here) {
+        if (tid < ENC_) ta_p = a.ta_w[tid] * a.ctx_prev[(int64_t)b * a.ctx_ld + tid];
+        if (tid < HATT_) ta_p += a.ta_w[ENC_ + tid] * a.h_att_prev[(int64_t)b * HATT_ + tid];
+    }
     const float vb = a.v_b[0];
     float qv = 0.f;
     if (tid < ADIM && !a.wqT) qv = a.q[(int64_t)b * ADIM + tid];
@@ -272,14 +294,14 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         }
         qpart = s0 + s1;
     }
-    const float aold_j = (a.forward_attn && in) ? a.alpha[row + j] : 0.f;
+    const float aold_j = (a.forward_attn && in) ? alpha_rd[row + j] : 0.f;
     // Tacotron2: the energies arrive as QE_TILES partial sums per position from query_energy_kernel
     // (location term included), and this launch leaves the next step's location features
     constexpr bool qe = QE;
     float ep[QE_TILES];
 #pragma unroll
     for (int k = 0; k < QE_TILES; ++k) ep[k] = (qe && in) ? a.epart[((int64_t)b * QE_TILES + k) * Lc + j] : 0.f;
-    const float cum_old = (qe && a.locf && in) ? a.att_cum[row + j] : 0.f;
+    const float cum_old = (qe && a.locf && in) ? cum_rd[row + j] : 0.f;
     const float* Pt = a.Pt + (int64_t)b * ADIM * Lc;
     const int d0 = wave * DPW;
     float pv0[DPW], pv1[DPW];
@@ -327,6 +349,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         }
         __syncthreads();
     }
+    if (ta_here) u = sigmoidf_(block_sum16(ta_p, scr) + a.ta_b[0]);
     if (tid < ADIM) q[tid] = qv;
     else if (tid < 2 * ADIM) vv[tid - ADIM] = qv;
     if (a.forward_attn && in) aold[j] = aold_j;
@@ -390,7 +413,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     }
     // ---- eval-mode windowing (common_layers.py:184-197)
     if (a.windowing) {
-        const int wi = a.win_idx[b];
+        const int wi = win_rd[b];
         const int back = wi - 2, front = wi + 6;
         if (in && ((back > 0 && j < back) || (front < L && j >= front))) e = -INFINITY;
         if (wi == -1) {
@@ -398,7 +421,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             if (j == 0) e = r.m;
         }
         const Red r = block_reduce(0.f, -INFINITY, in ? e : -INFINITY, in ? j : 0x7fffffff, scr);
-        if (tid == 0) a.win_idx[b] = r.i;
+        if (tid == 0 && ks == 0) win_wr[b] = r.i;
     }
     // ---- normalisation (common_layers.py:239-245)
     float al = 0.f;
@@ -422,8 +445,11 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
     // update_location_attention (:163-164)
     const float cum_new = cum_old + al;
     if (a.location_attn && in) {
-        if (qe && a.locf) a.att_cum[row + j] = cum_new;
-        else a.att_cum[row + j] += al;
+        if (qe && a.locf) {
+            if (ks == 0) cum_wr[row + j] = cum_new;
+        } else {
+            a.att_cum[row + j] += al;
+        }
     }
 
     float w = al;
@@ -453,12 +479,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             denom = QE ? block_sum16(in ? anj : 0.f, scr) : block_reduce(in ? anj : 0.f, -INFINITY, 0.f, 0, scr).s;
         }
         w = in ? anj / denom : 0.f;
-        if (in) a.alpha[row + j] = w;
+        if (in && ks == 0) alpha_wr[row + j] = w;
     }
     if (in) wts[j] = w;
     __syncthreads();
     // ---- outputs: attention weights (alpha or alignment), history, stop-rule tail (tacotron2.py:268)
-    if (a.location_attn && in) a.att_w[row + j] = w;
+    if (!QE && a.location_attn && in) a.att_w[row + j] = w;  // (QE: the features carry it)
     if (qe && a.locf) {
         // the next step's location features: location_conv over [attention_weights;
         // attention_weights_cum] = [w; cum_new] zero-padded by 15 (common_layers.py:90-104, 167-171),
@@ -479,7 +505,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
         // 16 filters, one per wave at a time, the taps in order (channel 0's, then channel 1's)
         float* lo = a.locf + (int64_t)b * NLOC * Lc;
         const int ntile = (L + 15) / 16 * 2;
-        for (int tl = wave; tl < ntile; tl += ATT_WAVES) {
+        for (int tl = ks + ASPLIT * wave; tl < ntile; tl += ASPLIT * ATT_WAVES) {
             const int pt = tl >> 1, ft = tl & 1;
             const int jA = pt * 16 + (lane & 15), fB = ft * 16 + (lane & 15);
             floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -498,10 +524,10 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             }
         }
     }
-    if (!a.done[b] && t < a.hist_cap && a.align_hist)
+    if (ks == 0 && !a.done[b] && t < a.hist_cap && a.align_hist)
         for (int jj = tid; jj < a.Lalign; jj += blockDim.x)
             a.align_hist[(int64_t)b * a.align_ldb + (int64_t)t * a.Lalign + jj] = jj < L ? wts[jj] : 0.f;
-    if (tid == 0) {
+    if (tid == 0 && ks == 0) {
         a.tail[b] = a.tail_rule ? wts[L - 1] : (L >= 2 ? wts[L - 2] + wts[L - 1] : wts[0]);
         if (sparse) {
             // next step's n = argmax(prev_alpha) = 1 + first argmax of alpha[0..L-2], or 0 when
@@ -514,7 +540,7 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             if (cx < clo) consider(cx);
             for (int p = clo; p <= chi; ++p) consider(p);
             if (cx > chi) consider(cx);
-            a.nidx[b] = bi >= 0 ? bi + 1 : 0;
+            nidx_wr[b] = bi >= 0 ? bi + 1 : 0;
         }
     }
     // ---- context = w . inputs  (bmm, common_layers.py:217 / 253)
@@ -528,12 +554,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             if (cx > chi) ctx += wts[cx] * ex;
         }
     } else if (QE) {
-        // float4 channel groups x PARTS interleaved position sets; each thread issues a batch of 8
-        // rows' loads together (the rows stream from L2 / MALL: one round trip per batch, not per
-        // row), then the parts meet in LDS and are summed in part order
-        constexpr int D4 = ENC_ / 4, PARTS = ATT_THREADS / D4;
-        static_assert(PARTS * ENC_ <= ATT_WAVES * 256, "context partials fit the reduction area");
-        const int d4 = tid % D4, part = tid / D4;
+        // this slice's ENC_ / ASPLIT channels as float4 groups x PARTS interleaved position sets;
+        // each thread issues a batch of 8 rows' loads together (the rows stream from L2 / MALL: one
+        // round trip per batch, not per row), then the parts meet in LDS and are summed in order
+        constexpr int CS = ENC_ / ASPLIT, D4 = CS / 4, PARTS = ATT_THREADS / D4;
+        static_assert(PARTS * CS <= ATT_WAVES * 256, "context partials fit the reduction area");
+        const int d4 = ks * D4 + tid % D4, part = tid / D4;
         float4 acc = float4{0.f, 0.f, 0.f, 0.f};
         for (int j0 = part; j0 < L; j0 += 8 * PARTS) {
             float4 ev[8];
@@ -549,12 +575,12 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
                 acc.w += wv * ev[m].w;
             }
         }
-        *reinterpret_cast<float4*>(red + part * ENC_ + 4 * d4) = acc;
+        *reinterpret_cast<float4*>(red + part * CS + 4 * (tid % D4)) = acc;
         __syncthreads();
-        if (tid < ENC_) {
+        if (tid < CS) {
             ctx = red[tid];
 #pragma unroll
-            for (int p = 1; p < PARTS; ++p) ctx += red[p * ENC_ + tid];
+            for (int p = 1; p < PARTS; ++p) ctx += red[p * CS + tid];
         }
     } else {
         // PARTS interleaved position sets per channel, summed in part order
@@ -581,11 +607,18 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const AttnArgs a
             for (int p = 1; p < PARTS; ++p) ctx += red[p * ENC_ + tid];
         }
     }
-    if (tid < ENC_) {
+    if (QE) {  // this slice's channels (sparse: every slice evaluated all of them, cheaply)
+        constexpr int CS = ENC_ / ASPLIT;
+        const int dch = sparse ? tid : ks * CS + tid;
+        if (sparse ? (tid >= ks * CS && tid < (ks + 1) * CS) : tid < CS) {
+            a.ctx[(int64_t)b * a.ctx_ld + dch] = ctx;
+            if (a.ctxf) a.ctxf[frag_idx(b, a.ctxf_k0 + dch, a.ntf)] = ctx;
+        }
+    } else if (tid < ENC_) {
         a.ctx[(int64_t)b * a.ctx_ld + tid] = ctx;
         if (a.ctxf) a.ctxf[frag_idx(b, a.ctxf_k0 + tid, a.ntf)] = ctx;
     }
-    if (a.forward_attn && a.trans_agent) {
+    if (!QE && a.forward_attn && a.trans_agent) {  // (QE: at the start of the next step's launch)
         // u = sigmoid(ta([context, query]))  (:220-222)
         const float* h = a.h_att + (int64_t)b * HATT_;
         float p = tid < ENC_ ? a.ta_w[tid] * ctx : 0.f;
@@ -835,7 +868,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (attention_fast(a)) {
         hipLaunchKernelGGL(attention_fm_kernel, dim3(a.B), dim3(ATT_THREADS), attention_fm_smem_bytes(a.Lcap), s, a);
     } else if (a.enc_dim == ENC && a.epart) {
-        hipLaunchKernelGGL((attention_kernel<ENC, HATT, true>), dim3(a.B), dim3(ATT_THREADS),
+        hipLaunchKernelGGL((attention_kernel<ENC, HATT, true>), dim3(ATT_SPLIT, a.B), dim3(ATT_THREADS),
                            attention_smem_bytes(a.Lcap, a.location_attn), s, a);
     } else if (a.enc_dim == ENC) {
         hipLaunchKernelGGL((attention_kernel<ENC, HATT, false>), dim3(a.B), dim3(ATT_THREADS),

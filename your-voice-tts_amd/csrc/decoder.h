@@ -14,6 +14,7 @@ constexpr int KLOC = 31;   // location kernel
 constexpr int XA = PRE + ENC;  // [prenet | ctx] row of the attention-LSTM input
 constexpr int ATT_THREADS = 1024;  // one thread per encoder position (L <= 1024)
 constexpr int ATT_WAVES = ATT_THREADS / 64;
+constexpr int ATT_SPLIT = 4;  // workgroups per sentence of the general attention launch with epart
 
 // Flags (tts_decoder_config) + weights + device state pointers, passed by value.
 struct AttnArgs {
@@ -42,6 +43,14 @@ struct AttnArgs {
                            // attention configuration; null: attention_kernel evaluates the energies)
     float* locf;           // with epart and location_attn: [B][NLOC][Lcap] the NEXT step's location
                            // features (location_conv over [att_w; att_cum]), written at the step's end
+    // with epart (ATT_SPLIT workgroups per sentence, each recomputing the weights): alpha, att_cum
+    // ([2][B][Lcap]) and nidx, win_idx ([2][B]) by step parity, slot strides sstride / istride (the
+    // step reads slot t & 1 and writes the other); the transition agent's u from the previous
+    // step's context and attention-RNN output (ctx rows of stride ctx_ld, h rows of HATT)
+    int64_t sstride;
+    int istride;
+    const float* ctx_prev;
+    const float* h_att_prev;
     // state
     float* alpha;          // [B][Lcap]
     float* att_w;          // [B][Lcap]

@@ -245,6 +245,8 @@ tts_status enqueue_step(tts_decoder* d, int B, int Lmax, int max_steps, int p, h
         a.q = d->q; a.Pt = d->Pt; a.enc = d->enc; a.lens = d->lens;
         a.h_att = h_att_cur;
         a.epart = d->epart; a.locf = d->locf;
+        a.sstride = (int64_t)d->Bcap * d->Lcap; a.istride = d->Bcap;
+        a.ctx_prev = xa_cur + PRE; a.h_att_prev = h_att_prev;
         a.alpha = d->alpha; a.att_w = d->att_w; a.att_cum = d->att_cum; a.u = d->u; a.win_idx = d->win_idx;
         a.nidx = d->nidx; a.tail = d->tail;
         a.ctx = ctx_cur;  // kernel writes ctx[b*XA + d]
@@ -548,14 +550,16 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     }
     CK(dmalloc(d, &d->epart, (size_t)Bc * QE_TILES * Lc));
     if (cfg->location_attn) CK(dmalloc(d, &d->locf, (size_t)Bc * NLOC * Lc));
-    CK(dmalloc(d, &d->alpha, (size_t)Bc * Lc));
+    // alpha / att_cum / win_idx / nidx: two parity slots (the split general attention launch reads
+    // slot t & 1 and writes the other; the fast paths use slot 0 only)
+    CK(dmalloc(d, &d->alpha, (size_t)2 * Bc * Lc));
     CK(dmalloc(d, &d->att_w, (size_t)Bc * Lc));
-    CK(dmalloc(d, &d->att_cum, (size_t)Bc * Lc));
+    CK(dmalloc(d, &d->att_cum, (size_t)2 * Bc * Lc));
     CK(dmalloc(d, &d->u, Bc));
     CK(dmalloc(d, &d->tail, Bc));
     CK(dmalloc(d, &d->lens, Bc));
-    CK(dmalloc(d, &d->win_idx, Bc));
-    CK(dmalloc(d, &d->nidx, Bc));
+    CK(dmalloc(d, &d->win_idx, 2 * Bc));
+    CK(dmalloc(d, &d->nidx, 2 * Bc));
     CK(dmalloc(d, &d->flag1, Bc));
     CK(dmalloc(d, &d->count, Bc));
     CK(dmalloc(d, &d->done, Bc));
