@@ -225,3 +225,21 @@ def test_tacotron2_oracle_speakers_match_reference(case):
         np.testing.assert_array_equal(res["align"].argmax(1), z["align"].argmax(1))
         assert rel_rms(res["mel"], z["mel"]) < 1e-4
         assert rel_rms(res["mel_post"], z["mel_post"]) < 1e-4
+
+
+def test_prenet_bn_fold_algebra():
+    """The create-time fold of an eval-mode BatchNorm1d into the preceding linear layer (decoder_api.hip /
+    tacotron_api.hip: fold_linear_bn): W' = diag(s) W, b' = s (b - mean) + beta, s = gamma / sqrt(var + eps),
+    equals Linear -> BatchNorm1d (common_layers.py:28-52) on random inputs, with and without a linear bias."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    W = rng.standard_normal((256, 80)).astype(np.float64)
+    g, be = rng.uniform(0.8, 1.2, 256), rng.uniform(-0.1, 0.1, 256)
+    mu, var = rng.uniform(-0.1, 0.1, 256), rng.uniform(0.5, 1.5, 256)
+    x = rng.standard_normal((7, 80))
+    for b in (None, rng.uniform(-0.1, 0.1, 256)):
+        y = x @ W.T + (0 if b is None else b)
+        ref = (y - mu) / np.sqrt(var + 1e-5) * g + be
+        s = g / np.sqrt(var + 1e-5)
+        Wf = W * s[:, None]
+        bf = s * ((0 if b is None else b) - mu) + be
+        np.testing.assert_allclose(x @ Wf.T + bf, ref, rtol=1e-12, atol=1e-12)
