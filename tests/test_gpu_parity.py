@@ -614,14 +614,16 @@ def test_prenet_bn_batch_vs_reference(B):
         _check_decoder(out, b, z)
 
 
-def test_location_attention_batch_vs_reference():
+@pytest.mark.parametrize("B", [3, 20])
+def test_location_attention_batch_vs_reference(B):
     """Location-sensitive attention with forward attention and the transition agent (the multi-launch
-    path: energies with the location term as query-launch partials, the next step's location
-    features from the attention launch) in a batch of three, against the reference run."""
+    path: energies with the location term as query-launch partials, the split attention launch with
+    the next step's location features) in a batch of 3 (row-major GEMM inputs) and of 20 (fragment
+    mirrors, written slice by slice), against the reference run."""
     z = golden("t2_loc_fwd_ta_L24")
     m = _model(golden_flags(z))
     L = len(z["ids"])
-    enc = torch.from_numpy(z["enc"])[None].repeat(3, 1, 1).cuda()
-    out = m.inference_batch(None, enc=enc, lens=[L] * 3)
-    for b in range(3):
+    enc = torch.from_numpy(z["enc"])[None].repeat(B, 1, 1).cuda()
+    out = m.inference_batch(None, enc=enc, lens=[L] * B)
+    for b in range(B):
         _check_decoder(out, b, z)
