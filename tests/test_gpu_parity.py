@@ -238,6 +238,32 @@ def test_griffin_lim_configs1_persistent_vs_oracle(audio_cfg):
     assert rel_rms(wav, ref) < WAV_RTOL
 
 
+@pytest.mark.parametrize("Fs", [[300], [512], [190, 140]])
+def test_griffin_lim_persistent_two_per_cu_vs_oracle(audio_cfg, monkeypatch, Fs):
+    """257..512 frames in all: the persistent loop's two-workgroups-per-CU form
+    (gl_persistent2_kernel), against the oracle per sentence and bitwise against the fused
+    per-iteration loop (TTS_RESIDENT=0)."""
+    audio = load_pkg("audio")
+    ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 20})
+    rng = np.random.Generator(np.random.PCG64(sum(Fs)))
+    Fmax = max(Fs)
+    mel = np.zeros((len(Fs), Fmax, 80), np.float32)
+    pu = np.zeros((len(Fs), 1025, Fmax))
+    for b, F in enumerate(Fs):
+        mel[b, :F] = rng.uniform(0, 1, size=(F, 80))
+        pu[b, :, :F] = rng.uniform(0, 1, size=(1025, F))
+    wav = ap.griffin_lim_batch(torch.from_numpy(mel).cuda(), Fs, phase_u=pu).cpu()
+    assert ap.last_gl_path() == "persistent"
+    monkeypatch.setenv("TTS_RESIDENT", "0")
+    fused = ap.griffin_lim_batch(torch.from_numpy(mel).cuda(), Fs, phase_u=pu).cpu()
+    assert ap.last_gl_path() != "persistent"
+    assert torch.equal(wav, fused)
+    o = AudioOracle(**{**audio_cfg, "griffin_lim_iters": 20})
+    for b, F in enumerate(Fs):
+        n = ap.hop_length * (F - 1)
+        assert rel_rms(wav[b, :n].numpy(), o.inv_mel_spectrogram(mel[b, :F].T, pu[b, :, :F])) < WAV_RTOL, b
+
+
 def test_synthesize_native_configs1_vs_oracle(audio_cfg):
     """configs[1] end to end on the benched path (tts_synth_run: resident decoder, postnet and the
     persistent Griffin-Lim enqueued behind it, device phases) against the oracle chain: the
@@ -379,15 +405,15 @@ def test_synthesize_native_back_to_back(audio_cfg):
 
 
 def test_synthesize_native_pipelined_cross_stream(audio_cfg):
-    """sync=False back to back across the cross-stream path: jobs above 256 frames run Griffin-Lim on
+    """sync=False back to back across the cross-stream path: jobs above 512 frames run Griffin-Lim on
     the synth handle's second stream while the next call's encoder / decoder / postnet run (batch-1
     ones on the resident decoder), the stage buffers alternate by call parity; small jobs in between
     take the same-stream persistent Griffin-Lim.  Every waveform, cloned on the caller's stream right
     after its call, is bitwise inference_batch + griffin_lim_batch at the same seed."""
     w = weights_mod()
     z = {c: golden(c)["ids"] for c in ("t2_fwdmask_L100", "t2_fwdmask_L12", "t2_fwdmask_L40")}
-    z["L150"] = w.synthetic_ids(150, 7)
-    z["L140"] = w.synthetic_ids(140, 8)
+    z["L150"] = w.synthetic_ids(260, 7)  # 2L + 22 frames under the mask: above 512
+    z["L140"] = w.synthetic_ids(140, 8)  # 302 frames: the same-stream persistent loop, two per CU
     m = _model(golden_flags(golden("t2_fwdmask_L100")))
     audio = load_pkg("audio")
     ap = audio.AudioProcessor(**{**audio_cfg, "griffin_lim_iters": 6})
@@ -398,7 +424,7 @@ def test_synthesize_native_pipelined_cross_stream(audio_cfg):
         wav, frames = m.synthesize_native([z[c] for c in cases], ap, seed=50 + k, sync=False)
         outs.append((wav.clone(), frames))
     m.synth_sync()
-    assert sum(outs[0][1]) > 256 and sum(outs[2][1]) > 256 and sum(outs[3][1]) <= 256
+    assert sum(outs[0][1]) > 512 and sum(outs[2][1]) > 512 and 256 < sum(outs[1][1]) <= 512 and sum(outs[3][1]) <= 256
     for k, cases in enumerate(seq):
         ids = [z[c] for c in cases]
         out = m.inference_batch(ids)

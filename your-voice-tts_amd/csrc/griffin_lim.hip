@@ -966,7 +966,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 }
 
 // ---------------------------------------------------------------- persistent GL loop (small batches)
-// Every GL iteration after the initial one, for all frames (<= 256 in all), in ONE launch: one
+// Every GL iteration after the initial one, for all frames (<= 512 in all), in ONE launch: one
 // workgroup per (sentence, frame) keeps its iteration-invariant operands (|S| row, window,
 // twiddles, and the overlap-add geometry of its 2048 STFT input samples: contributor offsets and
 // the window sum-square) in registers.  Frames are 8-byte granules {tag | float32 sample} (gran_t)
@@ -1010,16 +1010,24 @@ typedef __attribute__((address_space(1))) unsigned long long gu64_t;
 typedef __attribute__((address_space(1))) unsigned gu32_t;
 typedef __attribute__((address_space(1))) int gi32_t;
 
-__global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArgs p) {
+// TWO: the form for 257..512 frames, two workgroups per compute unit (one wave per SIMD each):
+// at most 256 registers per lane (the FFT twiddles read pass by pass, fft1024_regs_gtw, instead of
+// 48 VGPRs for the whole loop) and the spectrum X in the FFT buffer the forward transform does not
+// end in, so the static LDS halves.  Same values, same operations: bitwise the one-per-CU form.
+template <bool TWO>
+__device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     const IterArgs& a = p.it;
     const int b = blockIdx.y;
     const int Fb = a.F[b];
     if ((int)blockIdx.x >= Fb) return;  // (a speculative batch-1 run sizes the grid as an upper bound)
     const Geo g = a.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    __shared__ __align__(16) double2 buf0[NH];
+    // (TWO: X in buf0 -- the forward FFT ends in buf1, and the inverse FFT's first LDS writes go to
+    // buf1, its second pass to buf0 after a barrier that follows every read of X)
+    __shared__ __align__(16) double2 buf0[TWO ? NB + 1 : NH];
     __shared__ __align__(16) double2 buf1[NH];
-    __shared__ __align__(16) double2 X[NB + 1];
+    __shared__ __align__(16) double2 Xs[TWO ? 1 : NB + 1];
+    double2* const X = TWO ? buf0 : Xs;
     __shared__ int sh[4];  // frame, local stores, abort
     auto fail = [&](int code) {
         __hip_atomic_store((gi32_t*)p.status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1034,15 +1042,16 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     if (tid == 0)
         __hip_atomic_store((gu32_t*)(xt + blockIdx.x), (p.salt << 8) | (unsigned)xcc, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+    constexpr int PV = TWO ? 8 : 4;  // table entries per lane (Fb <= 64 PV)
     if (wave == 0) {
-        unsigned v[4];  // blocks 4 lane .. 4 lane + 3 (Fb <= 256)
+        unsigned v[PV];  // blocks PV lane .. PV lane + PV - 1
         long long t_end = 0;
         bool ok = true;
         for (int spin = 0;; ++spin) {
             ok = true;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int k = lane * 4 + i;
+            for (int i = 0; i < PV; ++i) {
+                const int k = lane * PV + i;
                 v[i] = k < Fb ? __hip_atomic_load((gu32_t*)(xt + k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
                 ok = ok && (k >= Fb || (v[i] >> 8) == p.salt);
             }
@@ -1057,8 +1066,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
         for (int x = 0; x < 8; ++x) {
             int c = 0, r = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int k = lane * 4 + i;
+            for (int i = 0; i < PV; ++i) {
+                const int k = lane * PV + i;
                 const bool on = k < Fb && (int)(v[i] & 7) == x;
                 c += __popcll(__ballot(on));
                 r += __popcll(__ballot(on && k < (int)blockIdx.x));
@@ -1083,7 +1092,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
     const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     // the FFT twiddles in registers for the whole loop (one wave per SIMD: no occupancy to lose;
     // the per-pass table reads of fft1024_regs_gtw cost 0.25 us of each forward FFT here)
-    const FftTw ftw = load_fft_tw(a.c.tw);
+    FftTw ftw;
+    if (!TWO) ftw = load_fft_tw(a.c.tw);
     double2 tk[PK];
     double sk[PK];
 #pragma unroll
@@ -1246,7 +1256,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             else v[i >> 1].x = wi[i] * (double)yv;
         }
         GL_PHASE(1)
-        const double2* Z = fft1024_regs<false, false>(v, buf0, buf1, ftw);
+        const double2* Z = TWO ? fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw)
+                               : fft1024_regs<false, false>(v, buf0, buf1, ftw);
         GL_PHASE(2)
 #pragma unroll
         for (int i = 0; i < PK; ++i) {
@@ -1280,7 +1291,8 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
             const double2 O = cmul(D, cconj(tk[i]));
             v[i] = double2{E.x - O.y, E.y + O.x};
         }
-        fft1024_regs<true, true>(v, buf0, buf1, ftw);
+        if (TWO) fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
+        else fft1024_regs<true, true>(v, buf0, buf1, ftw);
         GL_PHASE(4)
         if (b == 0 && f == p.drop_f) return;  // fault injection only: never stores iteration 1
         // ---- the frame's samples, tagged with the next iteration: XCD-local (workgroup-scope store,
@@ -1300,6 +1312,11 @@ __global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArg
 #undef GL_PHASE
     if (timed)
         for (int k = 0; k < 6; ++k) p.prof[k] = ph[k];
+}
+__global__ __launch_bounds__(GL_THREADS) void gl_persistent_kernel(const PersArgs p) { gl_persistent_body<false>(p); }
+__global__ __launch_bounds__(GL_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void gl_persistent2_kernel(
+    const PersArgs p) {
+    gl_persistent_body<true>(p);
 }
 
 // the initial iSTFT's granules (slot 0) as float32 frames for the fused loop, when the persistent
@@ -1806,7 +1823,7 @@ static bool gather_fits(const Geo& g, int F) {
 
 bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters) {
     // (tags hold the iteration in 14 bits below the salt)
-    if (!(gl_fused_path(g, B, Fmax) && iters > 0 && iters < (1 << 14) && frames_total <= 256 && g->tmo > 0 &&
+    if (!(gl_fused_path(g, B, Fmax) && iters > 0 && iters < (1 << 14) && frames_total <= 512 && g->tmo > 0 &&
           !getenv_off("TTS_RESIDENT")))
         return false;
     // every frame count the run may have (a speculative run knows only the upper bound Fmax)
@@ -1903,7 +1920,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         TTS_HIP(hipStreamWaitEvent(s, g->ev_in, 0));
     }
     // path choice (host values only): small batches fuse the overlap-add into the iteration launch;
-    // at most 256 frames in all run the whole loop as one persistent launch
+    // at most 512 frames in all run the whole loop as one persistent launch
     const char* fz = getenv("TTS_GL_FUSED");
     const bool fused = gl_fused_path(g, B, Fmax);
     int frames_total = 0;
@@ -2034,12 +2051,21 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         void* kargs[] = {&pa};
         // dynamic LDS: the gather buffer, GL_SLOTS frame slots + the zero word
         const size_t og_bytes = ((size_t)GL_SLOTS * geo.winp + 2) * sizeof(float);
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gl_persistent_kernel),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        // up to 256 workgroups: one per compute unit; up to 512: two per compute unit (gl_persistent2_kernel)
+        const bool two = (long long)grid.x * grid.y > 256;
+        const void* pfn = two ? reinterpret_cast<const void*>(&gl_persistent2_kernel)
+                              : reinterpret_cast<const void*>(&gl_persistent_kernel);
+        static const hipError_t attr = [] {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gl_persistent_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gl_persistent2_kernel),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+            return e;
+        }();
         TTS_HIP(attr);
         TTS_CHECK(og_bytes <= 96 * 1024, TTS_ERR_INVALID, "persistent Griffin-Lim: window too long for the gather buffer");
-        TTS_HIP(launch_persistent(reinterpret_cast<const void*>(&gl_persistent_kernel), grid, block, kargs, og_bytes, s,
-                                  &persistent_ran));
+        TTS_HIP(launch_persistent(pfn, grid, block, kargs, og_bytes, s, &persistent_ran));
         if (!persistent_ran) {
             // the initial iSTFT wrote slot 0 of the granule buffer: hand it to the fused loop
             hipLaunchKernelGGL(gl_gran_to_frames_kernel, dim3((unsigned)((fstride + 255) / 256)), dim3(256), 0, s,

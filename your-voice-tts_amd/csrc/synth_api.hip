@@ -5,7 +5,7 @@
 // host round trips between them: one H2D of the ids, the decoder's stop-step readback (the
 // sentence length is decided on the device) and the stages' own completion waits.  The stages
 // run in pipeline mode (common.h) and the call returns once Griffin-Lim is enqueued: the
-// waveform is ready when the caller's stream reaches it.  Above 256 frames Griffin-Lim runs on a
+// waveform is ready when the caller's stream reaches it.  Above 512 frames Griffin-Lim runs on a
 // second stream of this handle, so call k+1's encoder + decoder (which read only host inputs and
 // this handle's buffers) need not wait for call k's Griffin-Lim; the stage buffers Griffin-Lim
 // reads (mel_post, its compacted copy) alternate per call.
@@ -230,7 +230,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
     PipelineScope scope(s);
     // the front stages do not wait for the caller's stream (they read host inputs and write this
     // handle's buffers only), nor for the previous call's Griffin-Lim.  The persistent Griffin-Lim
-    // (whose workgroups wait on each other) only runs on this same stream (<= 256 frames, below),
+    // (whose workgroups wait on each other) only runs on this same stream (<= 512 frames, below),
     // so it never shares the device with this call's resident launches.  A cross-stream Griffin-Lim
     // is the non-persistent per-iteration form; if its workgroups keep a resident encoder /
     // decoder workgroup from being placed, that launch's bounded waits drain it and the stage
@@ -270,7 +270,11 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
     // launch clamps into fspec (a longer sentence makes it an empty run, redone below)
     const int Ts = (int)std::min<size_t>(256, T);
     const int Tp = (int)std::min<size_t>(1024, T);
-    const bool spec_gl = B == 1 && s->r == 1 && wav_cap >= (int64_t)s->hop * (Ts - 1) &&
+    static const bool no_spec = [] {  // measurement only: no speculative Griffin-Lim in the hook
+        const char* v = getenv("TTS_NO_SPEC_GL");
+        return v && v[0] == '1';
+    }();
+    const bool spec_gl = B == 1 && s->r == 1 && !no_spec && wav_cap >= (int64_t)s->hop * (Ts - 1) &&
                          tts::gl_persistent_path(s->g, 1, Ts, Ts, gl_iters);
     struct Hook {
         tts_synth* s;
@@ -366,13 +370,13 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
         TTS_HIP(hipMemcpy2DAsync(s->spec[par], Fmax * row, post, T * row, Fmax * row, B, hipMemcpyDeviceToDevice, ss));
         spec = s->spec[par];
     }
-    // Small jobs (<= 256 frames: the persistent Griffin-Lim, whose spinning grid must not share the
+    // Small jobs (<= 512 frames: the persistent Griffin-Lim, whose spinning grid must not share the
     // device with the next call's resident launches anyway) stay on the front stream: no
     // cross-queue hand-offs on the latency-bound batch-1 path.  Larger ones move to gl_stream,
     // so the next call's encoder + decoder need not wait for them.
     int frames_total = 0;
     for (int b = 0; b < B; ++b) frames_total += h_frames[b];
-    const bool same = frames_total <= 256;
+    const bool same = frames_total <= 512;
     hipStream_t gs = same ? ss : s->gl_stream;
     if (gl_done) {  // enqueued behind the decoder already (hook_fn)
         TTS_HIP(hipEventRecord(s->ev_out, ss));
