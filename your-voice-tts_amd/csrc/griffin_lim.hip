@@ -1095,18 +1095,12 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     FftTw ftw;
     if (!TWO) ftw = load_fft_tw(a.c.tw);
     double2 tk[PK];
-    double sk[PK];
+    spec_t sk[PK];  // (|S| in its float storage: widened where it is used)
 #pragma unroll
     for (int i = 0; i < PK; ++i) {
         const int k = tid + i * GL_THREADS;
         tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
-        sk[i] = k < NB ? (double)Sf[k] : 0.0;
-    }
-    double wo[PN];  // synthesis window at this thread's output samples (edge_sample)
-#pragma unroll
-    for (int i = 0; i < PN; ++i) {
-        const int m = edge_sample(tid, i), n = m - g.woff;
-        wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
+        sk[i] = k < NB ? Sf[k] : 0.f;
     }
     // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors and
     // window sum-square, as ola_sample.  A contributor is an index into the gather buffer og: slot
@@ -1122,7 +1116,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     }
     if (tid < 2) og[og_zero + tid] = 0.f;
     __syncthreads();
-    double wi[PN];
+    double wi[PN];  // the window at this thread's samples: analysis (input) and synthesis (output) alike
     int off[PN][OLA_MAX];
     float wssv[PN];
 #pragma unroll
@@ -1274,7 +1268,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             // square exactly in double): no divisions on the iteration's critical path
             const double m2 = xre * xre + xim * xim;
             const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
-            const double s = sk[i];
+            const double s = (double)sk[i];
             double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
             if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
             X[k] = xv;
@@ -1302,7 +1296,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-            const u32x2 gv = u32x2{__float_as_uint((float)(wo[i] * (zv * (1.0 / NH)))), nt};
+            const u32x2 gv = u32x2{__float_as_uint((float)(wi[i] * (zv * (1.0 / NH)))), nt};
             // plain (workgroup-scope) store: the line stays in this XCD's L2; sc1: written through
             if (local) __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0);
             else __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0x10);
