@@ -390,7 +390,10 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     double acc[FW];
 #pragma unroll
     for (int i = 0; i < FW; ++i) acc[i] = 0.0;
-    for (int m = 0; m < a.n_in; ++m) {
+    // a fixed trip count (n_in <= 80: the staged rows past n_in are zeros, whose products add +0.0)
+    // keeps the LDS reads in flight ahead of the FMAs
+#pragma unroll 8
+    for (int m = 0; m < 80; ++m) {
         const double w = pw[m][lane];
 #pragma unroll
         for (int i = 0; i < FW; ++i) acc[i] += w * (double)amp[wave * FW + i][m];
