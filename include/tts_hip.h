@@ -226,8 +226,10 @@ tts_status tts_gl_last_timing(tts_gl* g, float* loop_ms, int* launches);
 
 /* Iteration loop the last tts_gl_run took: TTS_GL_PATH_UNFUSED (overlap-add launch + per-frame
  * STFT/iSTFT launch per iteration), TTS_GL_PATH_FUSED (one launch per iteration), or
- * TTS_GL_PATH_PERSISTENT (every iteration in one co-resident launch; when the grid cannot be
- * co-resident the run falls back to the fused loop, bitwise the same waveform). */
+ * TTS_GL_PATH_PERSISTENT (every iteration in one co-resident launch, up to 512 frames in all: one
+ * workgroup per frame, one per compute unit up to 256 workgroups and two per compute unit above;
+ * when the grid cannot be co-resident the run falls back to the fused loop, bitwise the same
+ * waveform). */
 #define TTS_GL_PATH_UNFUSED 0
 #define TTS_GL_PATH_FUSED 1
 #define TTS_GL_PATH_PERSISTENT 2
