@@ -61,7 +61,7 @@ constexpr int NB = 1025;  // bins
 constexpr int NH = 1024;  // complex FFT size
 constexpr int GL_THREADS = 256;
 constexpr int MAG_KT = 64;  // magnitude kernel tile: bins (one per lane) ...
-constexpr int MAG_FT = 32;  // ... x frames (MAG_FT / 4 per wave)
+constexpr int MAG_FT = 16;  // ... x frames (MAG_FT / 4 per wave)
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_PER = 8;  // samples per thread per scan tile
 constexpr int SCAN_CHUNK = 4096;  // de-emphasis output samples per workgroup
