@@ -50,3 +50,15 @@ def test_no_cpu_fallback():
     ap = audio.AudioProcessor(**load_pkg("generic_utils").default_config()["audio"])
     with pytest.raises(RuntimeError, match="no GPU"):
         ap.inv_mel_spectrogram(torch.rand(80, 10).numpy())
+
+
+def test_speaker_ids_must_match_the_batch():
+    """the library reads B speaker ids; one id broadcasts, any other count is rejected
+    before the call (torch's broadcast add in models/tacotron2.py:91-100 rejects it too)."""
+    t2 = load_pkg("tacotron2")
+    assert t2._speaker_array(torch.tensor([3]), 4).tolist() == [3, 3, 3, 3]
+    assert t2._speaker_array([0, 1, 2], 3).tolist() == [0, 1, 2]
+    with pytest.raises(ValueError):
+        t2._speaker_array([0, 1], 3)
+    with pytest.raises(ValueError):
+        t2._speaker_array([0, 1, 2, 3], 3)

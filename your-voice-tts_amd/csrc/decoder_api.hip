@@ -14,6 +14,7 @@
 // bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <string>
 #include <tuple>
@@ -364,6 +365,9 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         set_error("stream/event creation failed");
         return fail(TTS_ERR_HIP);
     }
+    // the host polls host_flags[3] for ++rb_seq (from 1): a recycled pinned block could still hold
+    // an earlier handle's sequence value, so the words start at zero
+    std::memset(d->host_flags, 0, (4 + 64) * sizeof(int));
     WeightMap wm;
     for (int i = 0; i < n_tensors; ++i) wm.m[tensors[i].key] = {tensors[i].data, tensors[i].numel};
     const int nmel = d->nmel;

@@ -1722,6 +1722,9 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
         if ((e = hipMemset(g->pstatus, 0, 16)) != hipSuccess) return fail(e, "hipMemset");
         if ((e = hipHostMalloc(reinterpret_cast<void**>(&g->host_status), 2 * sizeof(int), hipHostMallocCoherent)) != hipSuccess)
             return fail(e, "hipHostMalloc");
+        // host_status[1] is polled for ++seq (from 1): a recycled pinned block may hold a stale match
+        g->host_status[0] = 0;
+        g->host_status[1] = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= 256 &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0)
@@ -2034,7 +2037,11 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         pa.status = g->pstatus;
         pa.drop_f = -1;
         if (const char* inj = getenv("TTS_GL_INJECT_DROP"); inj && inj[0]) pa.drop_f = atoi(inj);
-        pa.nowait = getenv("TTS_GL_NOWAIT") != nullptr;
+        static const bool gl_nowait = [] {
+            const char* v = getenv("TTS_GL_NOWAIT");
+            return v && v[0] == '1';
+        }();
+        pa.nowait = gl_nowait;
         long long* prof = nullptr;
         const char* phases = getenv("TTS_GL_PHASES");
         if (phases && phases[0]) {  // diagnostic: phase ticks of frame TTS_GL_PHASES (stderr)

@@ -28,6 +28,19 @@ import torch
 from . import _native, weights
 
 
+def _speaker_array(speaker_ids, B):
+    """speaker ids as B int32 values: one id broadcasts to the batch (the reference's
+    ``embedding(speaker_ids).unsqueeze(1)`` add, models/tacotron2.py:91-100), otherwise exactly one
+    per sentence — the library reads B values, so a mismatch is rejected here, as torch's broadcast
+    add would reject it."""
+    spk = np.asarray(torch.as_tensor(speaker_ids).view(-1).cpu().numpy(), dtype=np.int32)
+    if spk.size == 1 and B > 1:
+        spk = np.repeat(spk, B)
+    if spk.size != B:
+        raise ValueError(f"speaker_ids has {spk.size} entries for a batch of {B}")
+    return np.ascontiguousarray(spk)
+
+
 class _DecoderAttrs:
     """Mutable attributes callers set on ``model.decoder`` (e.g. server/synthesizer.py:66)."""
 
@@ -201,9 +214,7 @@ class Tacotron2:
     def _add_speakers(self, lib, enc, lens, speaker_ids):
         """models/tacotron2.py:91-100 on the device (tts_encoder_add_speakers), in place."""
         B, Lmax = enc.shape[0], enc.shape[1]
-        spk = np.asarray(torch.as_tensor(speaker_ids).view(-1).cpu().numpy(), dtype=np.int32)
-        if spk.size == 1 and B > 1:
-            spk = np.repeat(spk, B)
+        spk = _speaker_array(speaker_ids, B)
         _native.check(lib.tts_encoder_add_speakers(self._native[3], ctypes.c_void_p(enc.data_ptr()),
                                                    _native.i32_array(lens), _native.i32_array(spk), B, Lmax,
                                                    _native.stream_handle()), "tts_encoder_add_speakers")
@@ -374,9 +385,7 @@ class Tacotron2:
                                             max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
                                             cap, frames, _native.stream_handle()), "tts_synth_run")
         else:
-            spk = np.asarray(torch.as_tensor(speaker_ids).view(-1).cpu().numpy(), dtype=np.int32)
-            if spk.size == 1 and B > 1:
-                spk = np.repeat(spk, B)
+            spk = _speaker_array(speaker_ids, B)
             _native.check(lib.tts_synth_run_speakers(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens),
                                                      _native.i32_array(spk), B, Lmax, max_steps, int(iters), int(seed),
                                                      ctypes.c_void_p(self._wav_buf.data_ptr()), cap, frames,
