@@ -84,13 +84,26 @@ CASES = [
 ]
 
 
-def make_model_fixtures():
+LONG_CASES = [
+    # round 5: the resident decoder's general attention form at full length.  Synthesizer.tts()'s
+    # configuration is config_tacotron2.json as it is (forward attention, sigmoid, mask OFF,
+    # server/synthesizer.py:55); the constructor default is location-sensitive + softmax
+    # (models/tacotron2.py:17,23); both run to their step cap under random weights.
+    ("t2_nomask_L100", 100, 1, dict(), None),
+    ("t2_loc_softmax_L100", 100, 2,
+     dict(location_attn=True, attention_norm="softmax", use_forward_attn=False, forward_attn_mask=False), 300),
+    ("t2_loc_fwd_ta_L100", 100, 3,
+     dict(location_attn=True, use_forward_attn=True, transition_agent=True, forward_attn_mask=False), 300),
+]
+
+
+def make_model_fixtures(cases=CASES):
     import torch
     _stub_text_deps()
     sys.path.insert(0, REF)
     from utils.generic_utils import load_config, setup_model
     torch.set_num_threads(os.cpu_count())
-    for name, L, seed, over, cap in CASES:
+    for name, L, seed, over, cap in cases:
         C = load_config(os.path.join(REF, "config_tacotron2.json"))
         C.num_speakers = 0
         C.update(over)
@@ -463,6 +476,8 @@ if __name__ == "__main__":
         make_split_fixture()
     if "model" in which:
         make_model_fixtures()
+    if "long" in which:
+        make_model_fixtures(LONG_CASES)
     if "taco" in which:
         make_taco_fixtures()
     if "truncated" in which:

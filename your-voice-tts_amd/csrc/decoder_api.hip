@@ -13,6 +13,7 @@
 // The host synchronises only at chunk boundaries: the first chunk is the reference's lower
 // bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -58,6 +59,8 @@ struct tts_decoder {
     // batched GEMM (sgemm.h: Seg::pf).  Null when max_batch <= 16.
     int ntf = 0;
     float *xaf = nullptr, *hattf = nullptr, *hdecf = nullptr, *pre1f = nullptr;
+    int res_gen = 0;              // resident decoder form: 0 = synthesis configuration, else GEN_* bits
+    float* loc_conv_p = nullptr;  // location_conv packed for the general resident form
     bool fast_attention = false;  // attention_uses_epart(): the synthesis configuration's attention
                                   // launch (attention_fm_kernel) and the resident decoder
     float* locf = nullptr;        // location_attn: [Bcap][NLOC][Lcap] location features of the next step
@@ -424,6 +427,15 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         probe.windowing = cfg->windowing;
         probe.enc_dim = ENC;
         d->fast_attention = attention_uses_epart(probe);
+        // the general resident form for every other configuration (resident.h); TTS_RESIDENT_GEN=0
+        // keeps those on the multi-launch path (A/B, parity reference)
+        const char* ge = getenv("TTS_RESIDENT_GEN");
+        if (!d->fast_attention && !(ge && ge[0] == '0')) {
+            d->res_gen = GEN_ON | (cfg->attn_norm == 0 ? GEN_SOFTMAX : 0) | (cfg->forward_attn ? GEN_FORWARD : 0) |
+                         (cfg->forward_attn && cfg->forward_attn_mask ? GEN_MASK : 0) |
+                         (cfg->forward_attn && cfg->trans_agent ? GEN_TA : 0) | (cfg->location_attn ? GEN_LOCATION : 0) |
+                         (cfg->windowing ? GEN_WINDOW : 0);
+        }
     }
     // prenet_type "bn" (common_layers.py:55-70, Decoder's Prenet(bias=False) layers/tacotron2.py:114):
     // each layer is Linear -> BatchNorm1d (eval: running statistics, eps 1e-5) -> ReLU, folded here
@@ -455,7 +467,7 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
         // TTS_RESIDENT=0 disables it (multi-launch path for every batch)
         const char* env = getenv("TTS_RESIDENT");
         int dev = 0, ncu = 0, rate_khz = 0;
-        if (d->fast_attention && nmel <= RES_CUS && !(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
+        if ((d->fast_attention || d->res_gen) && nmel <= RES_CUS && !(env && env[0] == '0') && hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu >= RES_CUS &&
             hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && rate_khz > 0 &&
             resident_prepare() == hipSuccess) {
@@ -527,6 +539,10 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
     if (lcw) {
         CK(copy_weight(d, &d->loc_conv, lcw, NLOC * 2 * KLOC, s));
         CK(copy_weight(d, &d->loc_dense, ldw, ADIM * NLOC, s));
+        if (d->resident && d->res_gen) {
+            CK(dmalloc(d, &d->loc_conv_p, 2 * NLOC * 32));
+            HK(resident_pack_location(d->loc_conv, d->loc_conv_p, s));
+        }
     }
     // workspace
     const int Bc = cfg->max_batch, Lc = (cfg->max_len + 3) / 4 * 4;
@@ -765,6 +781,13 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     // the GPU ~5.8 us between the kernels around it
     const bool timed = !d->pipeline;
     bool res_done = false;
+    static const bool verbose = [] {
+        const char* v = getenv("TTS_VERBOSE");
+        return v && v[0] == '1';
+    }();
+    if (verbose)
+        fprintf(stderr, "[tts] decoder_run B=%d L=%d resident=%d gen=%d keep=%d direct=%d\n", B, lens[0],
+                (int)d->resident, d->res_gen, (int)keep, (int)direct);
     if (d->resident && B == 1 && lens[0] <= RES_LMAX) {
         // one persistent launch runs every step (resident.h); same state / history buffers
         ResArgs ra{};
@@ -777,6 +800,9 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.pre1 = d->pre1; ra.alpha = d->alpha; ra.nidx = d->nidx; ra.u = d->u; ra.flag1 = d->flag1; ra.count = d->count;
         ra.done = d->done; ra.n_steps = d->n_steps;
         ra.mel_hist = d->mel_hist; ra.stop_hist = d->stop_hist; ra.align_hist = d->align_hist;
+        ra.gen = d->res_gen;
+        ra.ta_w = d->ta_w; ra.ta_b = d->ta_b; ra.att_w0 = d->att_w; ra.att_cum0 = d->att_cum; ra.win0 = d->win_idx;
+        ra.loc_conv = d->loc_conv_p; ra.loc_dense = d->loc_dense;
         ra.gran = d->gran;
         ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
         // direct (pipelined) runs skip the per-launch clear and rely on the 18-bit tag salt: on a
@@ -790,6 +816,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         if (timed) TTS_HIP(hipEventRecord(d->ev_t0, s));
         bool launched = false;
         TTS_HIP(launch_resident(ra, s, &launched));
+        if (verbose) fprintf(stderr, "[tts] resident launch: launched=%d\n", (int)launched);
         if (!launched) {
             // the grid cannot be co-resident on this device (launch_persistent): nothing ran and the
             // initial state is untouched; the multi-launch path takes over for the life of the handle
@@ -824,6 +851,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         }
         TTS_HIP(spin_word(d->host_flags + 3, seq, s));
         n_steps[0] = d->host_flags[4];
+        if (verbose) fprintf(stderr, "[tts] resident status=%d steps=%d\n", d->host_flags[0], n_steps[0]);
         if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
             // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
             // stopped before touching any state; use the multi-launch path from now on
@@ -838,6 +866,12 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             // path (same results within the resident tests' tolerance); the handle stays resident.
             // (inference_truncated's carried state may already be overwritten: that case raises.)
             ++d->res_timeouts;
+            if (verbose) {
+                int dbg[3] = {0, 0, 0};
+                (void)hipMemcpy(dbg, ra.status, sizeof(dbg), hipMemcpyDeviceToHost);
+                fprintf(stderr, "[tts] resident decoder: wait %d timed out at step %d on workgroup %d (L=%d); "
+                                "re-running multi-launch\n", dbg[0], dbg[1], dbg[2], lens[0]);
+            }
             if (tts_status st = stage_fallback()) return st;
             TTS_HIP(launch_decoder_init(ia, s));
             if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }

@@ -14,9 +14,19 @@
 // Every wait is bounded: a wave that does not see its data within the timeout flags an error
 // and the grid drains.
 //
-// Scope: B = 1, the synthesis attention configuration (forward attention + eval mask,
-// sigmoid norm, no location / windowing / transition agent — attention_uses_epart()), L <= 256,
-// nmel <= 256 (one mel row per CU; r <= 3).  Reads its initial state from, and leaves its final
+// Scope: B = 1, L <= 256, nmel <= 256 (one mel row per CU; r <= 3), every Tacotron2 attention
+// configuration (common_layers.py:107-256), in two forms:
+//  - the synthesis configuration of synthesize.py:86 (forward attention + eval mask, sigmoid norm,
+//    no location / windowing / transition agent — attention_uses_epart()): one attention CU per XCD
+//    evaluates only the <= 15 positions the mask can keep (resident_decoder_kernel<., false>);
+//  - every other configuration, among them Synthesizer.tts()'s (server/synthesizer.py:46-66 with
+//    config_tacotron2.json: forward attention, sigmoid, mask off) and the constructor default
+//    (location-sensitive + softmax, models/tacotron2.py:17,23): the attention of each XCD is spread
+//    over its 32 CUs (resident_decoder_kernel<., true>).  CU rank k owns positions k + 32 w (one
+//    per wave w) and context channels [16 k, 16 k + 16): energies (+ location features) of its
+//    positions -> XCD-local publish -> every CU gathers all L energies and evaluates the
+//    normalisation / windowing / forward attention / mask over them identically in every wave ->
+//    the context of its 16 channels -> the existing context hand-off.  Reads its initial state from, and leaves its final
 // state in, the multi-launch path's buffers (same slots), so continuous mode and profiling
 // interoperate.
 #pragma once
@@ -34,8 +44,11 @@ constexpr int RES_LMAX = 256;
 // each CU's XCD id, parity 0 only)
 // GR_QX: per-XCD query half-rows [8][128 rows][2]; GR_CTXX: per-XCD context + tail [8][528];
 // GR_P1X: per-XCD prenet-1 rows + continue flag [8][264] (slot 256 = flag).
+// GR_EX: per-XCD attention energies [8][RES_LMAX] (general attention form: each CU of the XCD
+// publishes the energies of its positions, every CU gathers all L).
 constexpr int GR_HATT = 576, GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376, GR_QX = 5632, GR_CTXX = 7680,
-              GR_CTXX_STRIDE = ENC + 16, GR_P1X = 11904, GR_P1X_STRIDE = PRE + 8, GR_TOTAL = GR_P1X + 8 * GR_P1X_STRIDE;
+              GR_CTXX_STRIDE = ENC + 16, GR_P1X = 11904, GR_P1X_STRIDE = PRE + 8, GR_EX = GR_P1X + 8 * GR_P1X_STRIDE,
+              GR_TOTAL = GR_EX + 8 * 256;
 constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-1/2 rows 8 per CU
 static_assert(RES_MIN_CUS_PER_XCD * 8 >= PRE, "at most one prenet row per wave");
 constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
@@ -65,8 +78,20 @@ struct ResWeights {
     float* b2;    // [256] prenet layer-2 bias (the BatchNorm prenet's folded shift; zeros otherwise)
 };
 
+// general attention form: configuration bits (ResArgs::gen; 0 = the synthesis-configuration form)
+constexpr int GEN_ON = 1, GEN_SOFTMAX = 2, GEN_FORWARD = 4, GEN_MASK = 8, GEN_TA = 16, GEN_LOCATION = 32,
+              GEN_WINDOW = 64;
+
 struct ResArgs {
     ResWeights w;
+    int gen;                  // GEN_* bits (general attention form) or 0
+    const float* ta_w;        // transition agent [ENC + HATT] and bias [1] (GEN_TA)
+    const float* ta_b;
+    const float* att_w0;      // initial attention_weights / attention_weights_cum [Lcap] (GEN_LOCATION)
+    const float* att_cum0;
+    const int* win0;          // initial win_idx (GEN_WINDOW)
+    const float* loc_conv;    // location_conv weight, packed [NLOC][2][32] (taps 31 + a zero)
+    const float* loc_dense;   // location_dense weight [ADIM][NLOC] (reference layout)
     int L, Lcap, nmel, nrows, max_steps, hist_cap, Lalign;
     long long timeout_ticks;  // wall_clock64 ticks per wait
     unsigned salt;            // per-launch tag salt (18 bits): no granule of an earlier launch matches
@@ -119,6 +144,8 @@ struct ResSrc {
 };
 void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc);
 hipError_t resident_pack(const ResSrc& src, const ResWeights& w, hipStream_t s);
+// location_conv.weight [NLOC][2][KLOC] -> ResArgs::loc_conv [2][NLOC][32] (2 * NLOC * 32 floats)
+hipError_t resident_pack_location(const float* w, float* out, hipStream_t s);
 size_t resident_smem_bytes();
 hipError_t resident_prepare();
 // co-residency guaranteed or nothing launched (*launched = false): common.h launch_persistent

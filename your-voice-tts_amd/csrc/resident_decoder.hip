@@ -42,8 +42,15 @@ __device__ __forceinline__ void publish_xcd(u64* g, unsigned tag, float v) {
 __device__ __forceinline__ u64 peek(u64* g) {
     return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void fail(int* status, int code) {
-    __hip_atomic_store((gint*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The first failure of a launch wins (the other workgroups then time out in cascade); its step
+// and workgroup go to status[1], status[2] (diagnostics).
+__device__ __forceinline__ void fail(int* status, int code, int step = -1) {
+    int expected = 0;
+    if (__hip_atomic_compare_exchange_strong((gint*)status, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store((gint*)status + 1, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gint*)status + 2, (int)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals tag(i);
@@ -175,11 +182,15 @@ constexpr int SM_PROF = 2 * 16;            // RES_PHASES tick accumulators (long
 constexpr int SM_FLOATS = SM_WDL + HATT + HDEC + (ENC + 16) + PRE + ADIM + 16 + 16 + SM_ST + SM_RQ + SM_RM + SM_PROF + PRE;
 static_assert(SM_RM >= 6 * 64 * 4 + RES_WAVES * RES_LMAX, "attention CU partials");
 static_assert(SM_RQ >= 3 * RES_LMAX + 2 * RES_WAVES + 16 + ADIM, "attention CU scratch");
+static_assert(SM_RQ >= 2 * (RES_LMAX + 32) + RES_LMAX + RES_WAVES, "general attention form: weights, energies");
+static_assert(SM_RM >= 2 * 6 * 64 * 4 + RES_LMAX + 32, "general attention form: cumulative weights");
+static_assert(RES_LMAX == 4 * 64 && RES_LMAX == 32 * RES_WAVES, "4 positions per lane, one per wave of 32 CUs");
 
 // PROF: the profiling re-run's instantiation (phase marks, event trace); the production kernel
 // compiles every measurement site out (their pointers, ticks and step compares otherwise stay live
 // across the step loop in scalar registers, which this kernel already spills)
-template <bool PROF>
+// GEN: the general attention form (resident.h): the attention of each XCD spread over its CUs
+template <bool PROF, bool GEN>
 __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const ResArgs a) {
     const int c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -206,6 +217,15 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     float* red = rm + 6 * 64 * 4;  // [RES_WAVES][RES_LMAX]
     long long* pacc = reinterpret_cast<long long*>(rm + SM_RM);
     float* xp1 = rm + SM_RM + SM_PROF;  // pre1_t (prenet layer 1 output) gathered by wave 0
+    // general attention form (every CU): attention weights of the last two steps, zero-padded by
+    // 16 on both sides for the location convolution ([2][GW_PAD], position j at j + 16), the
+    // gathered energies, the transition agent's wave partials; the cumulative weights (padded)
+    // in the tail of rm (the mask form's attention-CU partials; no mel or stop row there)
+    constexpr int GW_PAD = RES_LMAX + 32;
+    float* gw = rq;                     // [2][GW_PAD]
+    float* geg = rq + 2 * GW_PAD;       // [RES_LMAX]
+    float* gts = geg + RES_LMAX;        // [RES_WAVES]
+    float* gcum = rm + 2 * 6 * 64 * 4;  // [GW_PAD]
     // optional phase timing (thread 0 of CU 0 and of the logging attention CU)
     bool prof = false;
     long long plast = 0;
@@ -269,7 +289,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     if (wave == 0) {
         float v4[4];
         const bool ok = sweep<4>(a.gran, setup_tag, v4, [&](int i) { return GR_SETUP + lane * 4 + i; }, tmo);
-        int rank = 0, nx = 0, nmin = RES_CUS;
+        int rank = 0, nx = 0, nmin = RES_CUS, nmax = 0;
         const int xref = __builtin_amdgcn_readfirstlane(__float_as_int(v4[0]) & 7);  // XCD of CU 0
         for (int k = 0; k < 8; ++k) {
             int cnt = 0;
@@ -281,7 +301,10 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             }
             if (k == xcc) nx = cnt;
             if (cnt > 0) nmin = min(nmin, cnt);
+            nmax = max(nmax, cnt);
         }
+        // (general form: CU rank k owns context channels [16 k, 16 k + 16) of its XCD's copy)
+        if (GEN && nmax > RES_MIN_CUS_PER_XCD) nmin = 0;
         if (lane == 0) {
             int* fl = reinterpret_cast<int*>(flags);
             fl[2] = rank;
@@ -313,7 +336,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     const float4 wq0 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + lane * 4);
     const float4 wq1 = ld4(a.w.wq + qrow * HATT + qhalf * 512 + 256 + lane * 4);
     const int L = a.L;
-    const bool att_cu = rank == nx - 1;               // the last CU of each XCD runs its attention copy
+    const bool att_cu = !GEN && rank == nx - 1;       // the last CU of each XCD runs its attention copy
     const bool xlog = xcc == flags[4];                // the XCD whose copies write the outputs
     const bool att_log = att_cu && xlog;              // ... alignment rows
     prof = PROF && a.prof != nullptr && a.prof_marks && (c == 0 || att_log);
@@ -340,6 +363,87 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         for (int j = tid; j < L; j += RES_THREADS) abuf[j] = a.alpha[j];  // step 0 reads buffer 0
         if (tid < ADIM) xv[tid] = a.v[tid];
         prefetch_rows(n);
+    }
+    // ---- general attention form: this CU's slices (position rank + 32 wave; context channels
+    // 16 rank + 2 wave + {0, 1} at this lane's positions gpos(i) = (i >> 1) 128 + 2 lane + (i & 1))
+    // and the attention state, replicated in every wave of every CU
+    const int gf = GEN ? a.gen : 0;
+    const int s_e = GR_EX + xcc * RES_LMAX;  // this XCD's energy slots
+    float gu = 0.5f, gtb = 0.f;              // forward attention u, transition agent bias
+    int gwin = -1, gn = 1;                   // windowing index, the mask's argmax n
+    float gv0 = 0.f, gv1 = 0.f, gp0 = 0.f, gp1 = 0.f, gl0 = 0.f, gl1 = 0.f;  // v, P, location term: dims lane, lane + 64
+    float gtw[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gtw[k] = 0.f;
+    // location_conv (2 -> 32 filters, k 31, pad 15) at position rank + 32 wave over [weights;
+    // cumulative weights] (padded LDS rows), then location_dense (32 -> 128) for dims lane and
+    // lane + 64 (common_layers.py:86-104, 166-171): lane (f = lane & 31, channel lane >> 5) sums
+    // its 31 taps, the two channels meet by a lane swap, every lane reads the 32 filter outputs
+    auto gen_location = [&](const float* wrow) {
+        const int pe = rank + 32 * wave;
+        if (pe >= L) return;
+        const float* src = (lane < 32 ? wrow : gcum) + pe + 1;  // cat[c][pe + k - 15] = src[k]
+        const float4* wc = reinterpret_cast<const float4*>(a.loc_conv) + lane * 8;
+        float sacc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; q += 2) {
+            const float4 w0 = wc[q], w1_ = wc[q + 1];
+            sacc = fmaf(w0.x, src[4 * q], sacc);
+            sacc = fmaf(w0.y, src[4 * q + 1], sacc);
+            sacc = fmaf(w0.z, src[4 * q + 2], sacc);
+            sacc = fmaf(w0.w, src[4 * q + 3], sacc);
+            sacc = fmaf(w1_.x, src[4 * q + 4], sacc);
+            sacc = fmaf(w1_.y, src[4 * q + 5], sacc);
+            sacc = fmaf(w1_.z, src[4 * q + 6], sacc);
+            sacc = fmaf(w1_.w, src[4 * q + 7], sacc);
+            asm volatile("" ::: "memory");  // two weight loads in flight at a time (registers)
+        }
+        const float tot = sacc + __shfl_xor(sacc, 32, 64);  // lane f < 32: filter f
+        const float4* wd0 = reinterpret_cast<const float4*>(a.loc_dense + lane * NLOC);
+        const float4* wd1 = reinterpret_cast<const float4*>(a.loc_dense + (lane + 64) * NLOC);
+        float l0 = 0.f, l1 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 u0 = wd0[q], u1 = wd1[q];
+            const float f0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), 4 * q));
+            const float f1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), 4 * q + 1));
+            const float f2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), 4 * q + 2));
+            const float f3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tot), 4 * q + 3));
+            l0 = fmaf(u0.x, f0, l0); l0 = fmaf(u0.y, f1, l0); l0 = fmaf(u0.z, f2, l0); l0 = fmaf(u0.w, f3, l0);
+            l1 = fmaf(u1.x, f0, l1); l1 = fmaf(u1.y, f1, l1); l1 = fmaf(u1.z, f2, l1); l1 = fmaf(u1.w, f3, l1);
+            asm volatile("" ::: "memory");
+        }
+        gl0 = l0;
+        gl1 = l1;
+    };
+    if constexpr (GEN) {
+        vb = a.v_b[0];
+        gu = a.u[0];
+        gn = a.nidx[0];
+        if (gf & GEN_WINDOW) gwin = a.win0[0];
+        if (gf & GEN_TA) {
+            gtb = a.ta_b[0];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) gtw[k] = a.ta_w[3 * tid + k];
+        }
+        gv0 = a.v[lane];
+        gv1 = a.v[lane + 64];
+        const int pe = rank + 32 * wave;
+        if (pe < L) {
+            gp0 = a.Pt[(int64_t)lane * a.Lcap + pe];
+            gp1 = a.Pt[(int64_t)(lane + 64) * a.Lcap + pe];
+        }
+        // padded rows: [0] the previous alpha (forward attention; read at step 0), [1] the initial
+        // attention_weights (the location input of step 0; step 0 then overwrites it)
+        for (int k = tid; k < GW_PAD; k += RES_THREADS) {
+            const int j = k - 16;
+            const bool ok = j >= 0 && j < L;
+            gw[k] = ok ? a.alpha[j] : 0.f;
+            gw[GW_PAD + k] = ok && (gf & GEN_LOCATION) ? a.att_w0[j] : 0.f;
+            gcum[k] = ok && (gf & GEN_LOCATION) ? a.att_cum0[j] : 0.f;
+        }
+        __syncthreads();
+        if (gf & GEN_LOCATION) gen_location(gw + GW_PAD);
     }
     const bool stop_lane = stop_cu && wave == 3 && lane == 0;
     if (stop_lane) {
@@ -370,7 +474,12 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
     int t = 0;
     for (;; ++t) {
         u64* G = a.gran + (t & 1) * GR_TOTAL;          // this step's granules
-        const unsigned E = (a.salt << 14) | ((unsigned)t * 8u);  // tags E+1 .. E+6, never 0
+        // tags E+1 .. E+7 (never 0): the step count wraps at 2048 inside its 11 bits (a granule
+        // slot is rewritten every second step, so only step t-2's tag can be stale there; runs
+        // reach the Synthesizer's 3000-step cap, server/synthesizer.py:66), the previous step's
+        // prenet-1 tag EP6 computed on its own wrapped count
+        const unsigned E = (a.salt << 14) | (((unsigned)t & 2047u) << 3);
+        const unsigned EP6 = ((a.salt << 14) | (((unsigned)(t - 1) & 2047u) << 3)) + 6u;
         // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}]
         float acc_a = 0.f;
 #pragma unroll
@@ -399,16 +508,16 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             } else {
                 float p0 = 0.f, p1 = 0.f;
                 if (wave < 2) {
-                    ok = sweep_pair(rg, gp + 2 * pk, true, E - 2, p0, p1, tmo);
+                    ok = sweep_pair(rg, gp + 2 * pk, true, EP6, p0, p1, tmo);
                     xp1[2 * pk] = p0;
                     xp1[2 * pk + 1] = p1;
                 } else {
-                    ok = sweep_pair(rg, lane == 0 ? gp + PRE : -1, false, E - 2, p0, p1, tmo);
+                    ok = sweep_pair(rg, lane == 0 ? gp + PRE : -1, false, EP6, p0, p1, tmo);
                     if (lane == 0 && ok && p0 == 0.f) flags[0] = 1;
                 }
             }
             RES_MARK(0);
-            if (lane == 0 && !ok) { flags[1] = 1; fail(a.status, 1); }
+            if (lane == 0 && !ok) { flags[1] = 1; fail(a.status, 1, t); }
         }
         __syncthreads();  // P1
         if (tid == 0) { RES_EV(t, 0) }
@@ -426,7 +535,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 const bool ok = sweep_pair(rg, s_x + (t & 1) * GR_TOTAL + 2 * pk, true, E + 1, q0, q1, tmo);
                 xpre[2 * pk] = q0;
                 xpre[2 * pk + 1] = q1;
-                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7); }
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7, t); }
             }
         }
         __syncthreads();  // B1
@@ -470,7 +579,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HATT + 2 * pk, true, E + 2, h0, h1, tmo);
             xh_att[2 * pk] = h0;
             xh_att[2 * pk + 1] = h1;
-            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2); }
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2, t); }
         }
         __syncthreads();  // B3
         if (tid == 0) { RES_EV(t, 3) }
@@ -499,6 +608,176 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         //    outputs (window weights, max(alpha), the window sum) need the energies of C only
         //    (<= 15 positions, duplicates harmless) whenever max over C >= 1e-8.  Step 0 (alpha
         //    initialised nonzero everywhere) and that rare case evaluate every position.
+        if constexpr (GEN) {
+            // 7') general attention form (resident.h).  This lane's encoder values of the context
+            // (channels 16 rank + 2 wave + {0, 1} at its positions; volatile: issued here, in flight
+            // across the query and energy hand-offs), then the query of this XCD's copy (waves 0-1)
+            float2 gen_e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ps = (i >> 1) * 128 + 2 * lane + (i & 1);
+                gen_e[i] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                    renc, ps < L ? (ps * ENC + 16 * rank + 2 * wave) * 4 : OOB_OFF, 0, VOLATILE_AUX));
+            }
+            if (wave < 2) {
+                float q0, q1;
+                const bool ok = sweep_pair(rg, s_q + (t & 1) * GR_TOTAL + 2 * pk, true, E + 3, q0, q1, tmo);
+                xq[pk] = q0 + q1;
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3, t); }
+            }
+            __syncthreads();  // G1
+            if (flags[1]) break;
+            // the energy of position rank + 32 wave: v . tanh(q [+ location] + P) + b_v
+            // (common_layers.py:166-182), published XCD-locally
+            if (rank + 32 * wave < L) {
+                float x0 = xq[lane], x1 = xq[lane + 64];
+                if (gf & GEN_LOCATION) {
+                    x0 += gl0;
+                    x1 += gl1;
+                }
+                const float e = wave_sum_dpp(gv0 * tanh_fast(x0 + gp0) + gv1 * tanh_fast(x1 + gp1));
+                if (lane == 0) publish_xcd(a.gran + (t & 1) * GR_TOTAL + s_e + rank + 32 * wave, E + 7, e + vb);
+            }
+            // every CU gathers the XCD's L energies (waves 0-1: positions 2 pk, 2 pk + 1)
+            if (wave < 2) {
+                const int p0 = 2 * pk;
+                float e0 = 0.f, e1 = 0.f;
+                const bool ok =
+                    sweep_pair(rg, p0 < L ? s_e + (t & 1) * GR_TOTAL + p0 : -1, p0 + 1 < L, E + 7, e0, e1, tmo);
+                geg[p0] = e0;
+                geg[p0 + 1] = e1;
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 8, t); }
+            }
+            __syncthreads();  // G2
+            if (flags[1]) break;
+            RES_MARK(6);
+            // the weights over all L positions, identically in every wave of every CU: lane holds
+            // positions ps[i] = (i >> 1) 128 + 2 lane + (i & 1), reductions are DPP wave reductions
+            const float* wold = gw + (t & 1) * GW_PAD + 16;  // previous step's weights (position j at j)
+            float* wnew = gw + ((t & 1) ^ 1) * GW_PAD + 16;
+            int ps[4];
+            bool in[4];
+            float e[4];
+            {
+                const float2 g0 = *reinterpret_cast<const float2*>(geg + 2 * lane);
+                const float2 g1 = *reinterpret_cast<const float2*>(geg + 128 + 2 * lane);
+                e[0] = g0.x; e[1] = g0.y; e[2] = g1.x; e[3] = g1.y;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ps[i] = (i >> 1) * 128 + 2 * lane + (i & 1);
+                in[i] = ps[i] < L;
+                if (!in[i]) e[i] = -INFINITY;
+            }
+            if (gf & GEN_WINDOW) {
+                // eval windowing (common_layers.py:184-197)
+                const int back = gwin - 2, front = gwin + 6;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (in[i] && ((back > 0 && ps[i] < back) || (front < L && ps[i] >= front))) e[i] = -INFINITY;
+                if (gwin == -1) {
+                    const float m = wave_max_dpp(fmaxf(fmaxf(e[0], e[1]), fmaxf(e[2], e[3])));
+                    if (lane == 0) e[0] = m;
+                }
+                float bv = e[0];
+                int bi = ps[0];
+#pragma unroll
+                for (int i = 1; i < 4; ++i)
+                    if (e[i] > bv) { bv = e[i]; bi = ps[i]; }
+                wave_argmax(bv, bi);
+                gwin = __builtin_amdgcn_readfirstlane(bi);
+            }
+            // normalisation (common_layers.py:239-245)
+            float al[4];
+            if (gf & GEN_SOFTMAX) {
+                const float m = wave_max_dpp(fmaxf(fmaxf(e[0], e[1]), fmaxf(e[2], e[3])));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) al[i] = in[i] ? expf(e[i] - m) : 0.f;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) al[i] = in[i] ? sigmoidf_(e[i]) : 0.f;
+            }
+            {
+                const float S = wave_sum_dpp((al[0] + al[1]) + (al[2] + al[3]));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) al[i] = al[i] / S;
+            }
+            if ((gf & GEN_LOCATION) && wave == 0) {  // update_location_attention (:163-164), own lanes' positions
+                float2* c01 = reinterpret_cast<float2*>(gcum + 16 + 2 * lane);
+                float2* c23 = reinterpret_cast<float2*>(gcum + 16 + 128 + 2 * lane);
+                const float2 o01 = *c01, o23 = *c23;
+                *c01 = float2{o01.x + al[0], o01.y + al[1]};
+                *c23 = float2{o23.x + al[2], o23.y + al[3]};
+            }
+            float w[4];
+            if (gf & GEN_FORWARD) {
+                // apply_forward_attention (:199-223); wold[-1] is the zero pad
+                float an[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float ao = wold[ps[i]], pv = wold[ps[i] - 1];
+                    const float mix = __fadd_rn(__fadd_rn(__fmul_rn(1.f - gu, ao), __fmul_rn(gu, pv)), 1e-8f);
+                    an[i] = in[i] ? __fmul_rn(mix, al[i]) : 0.f;
+                }
+                if (gf & GEN_MASK) {
+                    // eval mask (:207-213), Python slicing incl. the negative-index wrap for n < 2
+                    const float rmax = wave_max_dpp(fmaxf(fmaxf(in[0] ? an[0] : -INFINITY, in[1] ? an[1] : -INFINITY),
+                                                          fmaxf(in[2] ? an[2] : -INFINITY, in[3] ? an[3] : -INFINITY)));
+                    const int cx = gn >= 2 ? gn - 2 : gn - 2 + L, lo = gn >= 1 ? gn - 1 : L - 1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const bool keep = in[i] && ps[i] < gn + 3 && ps[i] >= lo;
+                        an[i] = ps[i] == cx ? 0.01f * rmax : (keep ? an[i] : 0.f);
+                    }
+                }
+                const float denom = wave_sum_dpp((an[0] + an[1]) + (an[2] + an[3]));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = in[i] ? an[i] / denom : 0.f;
+                if (gf & GEN_MASK) {
+                    // next n = argmax(prev_alpha) = 1 + first argmax of alpha[0..L-2] (0 when all zero)
+                    float bv = -1.f;
+                    int bi = 0x7fffffff;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (ps[i] <= L - 2 && w[i] > bv) { bv = w[i]; bi = ps[i]; }
+                    wave_argmax(bv, bi);
+                    gn = __builtin_amdgcn_readfirstlane(bv > 0.f ? bi + 1 : 0);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[i] = al[i];
+            }
+            RES_MARK(7);
+            const float tail = wave_sum_dpp(((ps[0] >= L - 2 && in[0] ? w[0] : 0.f) + (ps[1] >= L - 2 && in[1] ? w[1] : 0.f)) +
+                                            ((ps[2] >= L - 2 && in[2] ? w[2] : 0.f) + (ps[3] >= L - 2 && in[3] ? w[3] : 0.f)));
+            // context of this CU's channels (bmm, :217 / :253), published XCD-locally with the tail
+            float c0 = 0.f, c1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                c0 = fmaf(w[i], gen_e[i].x, c0);
+                c1 = fmaf(w[i], gen_e[i].y, c1);
+            }
+            c0 = wave_sum_dpp(c0);
+            c1 = wave_sum_dpp(c1);
+            {
+                u64* gcx = Gc + (t & 1) * GR_TOTAL;
+                if (lane < 2) publish_xcd(gcx + 16 * rank + 2 * wave + lane, E + 4, lane ? c1 : c0);
+                if (rank == 0 && wave == 0 && lane == 2) publish_xcd(gcx + ENC, E + 4, tail);
+            }
+            if (tid == 0) { RES_EV(t, 11) }
+            RES_MARK(8);
+            // this step's weights (next step's previous alpha / location input), cumulative weights,
+            // alignment row (tacotron2.py:262-266)
+            if (wave == 0) {
+                *reinterpret_cast<float2*>(wnew + 2 * lane) = float2{w[0], w[1]};
+                *reinterpret_cast<float2*>(wnew + 128 + 2 * lane) = float2{w[2], w[3]};
+                if (xlog && rank == 0 && t < a.hist_cap) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (ps[i] < a.Lalign) a.align_hist[(int64_t)t * a.Lalign + ps[i]] = w[i];
+                }
+            }
+        }
         if (att_cu) {
             const float* aold = abuf + (t & 1) * RES_LMAX;
             float* anew = abuf + ((t & 1) ^ 1) * RES_LMAX;
@@ -516,7 +795,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 float q0, q1;
                 const bool ok = sweep_pair(rg, s_q + (t & 1) * GR_TOTAL + 2 * pk, true, E + 3, q0, q1, tmo);
                 xq[pk] = q0 + q1;
-                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3); }
+                if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3, t); }
             }
             __syncthreads();  // A1
             if (tid == 0) { RES_EV(t, 9) }
@@ -651,7 +930,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             } else if (lane == 0) {
                 xctx[ENC] = c0;
             }
-            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4); }
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4, t); }
         }
         __syncthreads();  // B4
         if (tid == 0) { RES_EV(t, 4) }
@@ -674,6 +953,22 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 if (tid == 0) { RES_EV(t, 5) }
             }
         }
+        if constexpr (GEN) {
+            // off the critical path (the h_dec edge is in flight): the transition agent's wave
+            // partials of u = sigmoid(ta([ctx_t, h_att_t])) for the next step (common_layers.py:220-222)
+            // and the next step's location features (its input is this step's weights)
+            if (gf & GEN_TA) {
+                float pta = 0.f;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int idx = 3 * tid + k;
+                    pta = fmaf(gtw[k], idx < ENC ? xctx[idx] : xh_att[idx - ENC], pta);
+                }
+                pta = wave_sum_dpp(pta);
+                if (lane == 0) gts[wave] = pta;
+            }
+            if (gf & GEN_LOCATION) gen_location(gw + ((t & 1) ^ 1) * GW_PAD);
+        }
         // the attention CU's alpha (next step's prev_alpha) and alignment row, after its h_dec
         // publish: the eight attention CUs are the h_dec edge's last publishers
         if (att_cu) {
@@ -687,11 +982,19 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HDEC + 2 * pk, true, E + 5, h0, h1, tmo);
             xh_dec[2 * pk] = h0;
             xh_dec[2 * pk + 1] = h1;
-            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5); }
+            if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5, t); }
         }
         __syncthreads();  // B6
         if (tid == 0) { RES_EV(t, 6) }
         if (flags[1]) break;
+        if constexpr (GEN) {
+            if (gf & GEN_TA) {
+                float sta = gts[0];
+#pragma unroll
+                for (int k = 1; k < RES_WAVES; ++k) sta += gts[k];
+                gu = sigmoidf_(sta + gtb);
+            }
+        }
         RES_MARK(12);
         long long m0 = 0;  // prenet-1 / mel / stop row phase timing (wave 2, lane 0)
         if (prof && tid == 128) m0 = (long long)wall_clock64();
@@ -813,7 +1116,19 @@ __global__ void res_pack_bias(const float* abih, const float* abhh, const float*
     }
 }
 
+__global__ void res_pack_loc(const float* w, float* out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // out [2 c][NLOC f][32 k], k = 31 zero
+    if (idx >= 2 * NLOC * 32) return;
+    const int k = idx & 31, f = (idx >> 5) % NLOC, c = idx / (32 * NLOC);
+    out[idx] = k < KLOC ? w[(f * 2 + c) * KLOC + k] : 0.f;
+}
+
 }  // namespace
+
+hipError_t resident_pack_location(const float* w, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(res_pack_loc, dim3((2 * NLOC * 32 + 255) / 256), dim3(256), 0, s, w, out);
+    return hipGetLastError();
+}
 
 void resident_weight_floats(size_t* wa, size_t* wdl, size_t* wdc) {
     *wa = (size_t)RES_CUS * 14 * RES_THREADS * 4;
@@ -843,11 +1158,15 @@ hipError_t resident_pack(const ResSrc& s, const ResWeights& w, hipStream_t st) {
 size_t resident_smem_bytes() { return (size_t)SM_FLOATS * sizeof(float); }
 
 hipError_t resident_prepare() {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel<false>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&resident_decoder_kernel<true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
+    const void* fns[] = {reinterpret_cast<const void*>(&resident_decoder_kernel<false, false>),
+                         reinterpret_cast<const void*>(&resident_decoder_kernel<true, false>),
+                         reinterpret_cast<const void*>(&resident_decoder_kernel<false, true>),
+                         reinterpret_cast<const void*>(&resident_decoder_kernel<true, true>)};
+    for (const void* fn : fns) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)resident_smem_bytes());
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched) {
@@ -855,8 +1174,14 @@ hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched) {
     if (a.L < 2 || a.L > RES_LMAX || a.nmel > RES_CUS || a.nmel + PRE + 1 != a.nrows) return hipErrorInvalidValue;
     ResArgs arg = a;
     void* args[] = {&arg};
-    const void* fn = a.prof ? reinterpret_cast<const void*>(&resident_decoder_kernel<true>)
-                            : reinterpret_cast<const void*>(&resident_decoder_kernel<false>);
+    if (a.gen && ((a.gen & GEN_TA) && !(a.ta_w && a.ta_b))) return hipErrorInvalidValue;
+    if (a.gen && ((a.gen & GEN_LOCATION) && !(a.att_w0 && a.att_cum0 && a.loc_conv && a.loc_dense)))
+        return hipErrorInvalidValue;
+    if (a.gen && (a.gen & GEN_WINDOW) && !a.win0) return hipErrorInvalidValue;
+    const void* fn = a.gen ? (a.prof ? reinterpret_cast<const void*>(&resident_decoder_kernel<true, true>)
+                                     : reinterpret_cast<const void*>(&resident_decoder_kernel<false, true>))
+                           : (a.prof ? reinterpret_cast<const void*>(&resident_decoder_kernel<true, false>)
+                                     : reinterpret_cast<const void*>(&resident_decoder_kernel<false, false>));
     return launch_persistent(fn, dim3(RES_CUS), dim3(RES_THREADS), args, resident_smem_bytes(), s, launched);
 }
 
