@@ -2,7 +2,8 @@
 oracle.  Tolerances (north_star: "alignments/stop-tokens bit-exact, mel and waveform within
 1e-4 RMS"): integer/index outputs — frame count, per-step attention argmax, stop decisions — are
 compared exactly; float outputs of a different fp32 reduction order cannot be bitwise equal, so
-alignments/stop tokens are held to max-abs 1e-4 and mel / waveform to relative RMS 1e-4
+alignments/stop tokens are held to max-abs 4e-6 and mel to relative RMS 4e-6 (10x the measured
+worst case, profiles/r05_parity_report.jsonl), the waveform to north_star's relative RMS 1e-4
 (absolute RMS is vacuous here: the random-weight waveform has RMS ~1e-5)."""
 import glob
 import os
@@ -18,8 +19,12 @@ from oracle.tacotron2_oracle import Tacotron2Oracle
 pytestmark = pytest.mark.gpu
 
 T2_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2_*.npz")))
-MEL_RTOL = 1e-4
-ALIGN_ATOL = 1e-4
+# model half: about 10x the worst error measured over every reference fixture on every path
+# (profiles/r05_parity_report.jsonl: mel / mel_post relative RMS <= 3.1e-7, alignments <= 3.9e-7,
+# stop probabilities <= 1.2e-7 max-abs); the waveform keeps north_star's 1e-4 (Griffin-Lim amplifies
+# the fp32 rounding of its input about 100x over 60 iterations)
+MEL_RTOL = 4e-6
+ALIGN_ATOL = 4e-6
 WAV_RTOL = 1e-4
 
 

@@ -3,7 +3,7 @@ multi-launch path (TTS_RESIDENT=0 at create) and the oracle.
 
 Both implementations compute the same fp32 step in different reduction orders, so frame counts,
 attention argmax paths and stop decisions must be identical and mel / alignments agree to fp32
-rounding; the oracle tolerance is the parity suite's (mel relative RMS 1e-4)."""
+rounding; the oracle tolerance is the parity suite's (mel relative RMS 4e-6)."""
 import os
 
 import numpy as np
@@ -81,8 +81,8 @@ def test_resident_vs_oracle_long(models, L):
     T = out["frames"][0]
     assert T == ref["mel"].shape[0]
     np.testing.assert_array_equal(out["align"][0, :T, :L].cpu().numpy().argmax(1), ref["align"].argmax(1))
-    assert rel_rms(out["mel"][0, :T].cpu().numpy(), ref["mel"]) < 1e-4
-    assert rel_rms(out["mel_post"][0, :T].cpu().numpy(), ref["mel_post"]) < 1e-4
+    assert rel_rms(out["mel"][0, :T].cpu().numpy(), ref["mel"]) < 4e-6
+    assert rel_rms(out["mel_post"][0, :T].cpu().numpy(), ref["mel_post"]) < 4e-6
 
 
 def test_resident_deterministic_and_batches_unaffected(models):
@@ -104,14 +104,14 @@ def test_resident_deterministic_and_batches_unaffected(models):
         a, r = z["mel"][b, :int(T)].double(), zz["mel"][b, :int(T)].double()
         d = float((a - r).norm() / r.norm())
         assert d < 1e-5, (b, d)  # the encoder's reduction order only
-    # ... and both against the oracle: exact frame counts and attention argmax, mel at 1e-4
+    # ... and both against the oracle: exact frame counts and attention argmax, mel at 4e-6
     for b, x_ids in enumerate((ids, ids2)):
         ref = Tacotron2Oracle(w.tacotron2_weights(0), dtype=np.float32, **_flags()).inference(x_ids)
         T, L = int(z["frames"][b]), len(x_ids)
         assert T == ref["mel"].shape[0]
         for out in (z, zz):
             np.testing.assert_array_equal(out["align"][b, :T, :L].cpu().numpy().argmax(1), ref["align"].argmax(1))
-            assert rel_rms(out["mel"][b, :T].cpu().numpy(), ref["mel"]) < 1e-4
+            assert rel_rms(out["mel"][b, :T].cpu().numpy(), ref["mel"]) < 4e-6
     assert torch.equal(res.inference_batch([ids, ids2])["mel"], z["mel"])  # deterministic
     # and a batch-1 call afterwards is resident again and unchanged
     x2 = res.inference_batch([ids])

@@ -3,8 +3,9 @@ C-ABI, against the reference's own outputs (tests/golden/gst_*.npz, taco_*.npz, 
 tests/golden/make_golden.py from the reference models) and the numpy oracle.
 
 Tolerances as for Tacotron2 (north_star: alignments / stop tokens exact where they are decisions,
-mel and linear spectrogram within 1e-4 relative RMS): step counts, per-step attention argmax and
-the stop decisions are compared exactly; alignments and stop probabilities to max-abs 1e-4."""
+mel and linear spectrogram within 1e-4 relative RMS; held here to 4e-6, 10x the measured worst case):
+step counts, per-step attention argmax and the stop decisions are compared exactly; alignments and stop
+probabilities to max-abs 4e-6."""
 import glob
 import os
 
@@ -18,8 +19,8 @@ pytestmark = pytest.mark.gpu
 
 TACO_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gst_*.npz")) +
                     glob.glob(os.path.join(GOLDEN, "taco_*.npz")))
-RTOL = 1e-4
-ATOL = 1e-4
+RTOL = 4e-6  # 10x the worst measured (profiles/r05_parity_report.jsonl: mel / linear <= 3e-7)
+ATOL = 4e-6
 
 
 def _model(fl, **kw):
