@@ -42,6 +42,10 @@ sharding = importlib.import_module("your-voice-tts_amd.sharding")
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA peak (same table)
+# one hand-off edge of the resident decoder in isolation (tools/microbench/edge.hip, round 4: one
+# 16-byte granule pair per lane; device-wide 1024 granules on 8 waves, XCD-local 256 on 2 waves)
+EDGE_DEVICE_US = 1.60
+EDGE_XCD_US = 0.47
 FP64_VECTOR_PEAK_TF = 78.6  # fp64 vector FMA peak (same table)
 # one GL frame-iteration: forward + inverse 1024-point complex FFT (5 N log2 N each) plus the
 # real-FFT split / merge and the phase projection (~20 flops per bin each way)
@@ -666,18 +670,24 @@ def main():
             # weights stay in VGPRs / LDS): state what actually bounds it
             flops = decoder_step_flops(Lmean) * steps
             ph = kdom["phases_us_per_step"]["cu0"]
-            edges = {k: ph[k] for k in ("att_early_wait_pre1", "att_cell_gather", "dec_cell_gather")}
+            # round 4 made the prenet-1 edge XCD-local: two device-wide edges (h_att, h_dec: every
+            # CU's LSTM rows need all of h) and four XCD-local ones (pre1, prenet-2, query, context)
+            dev_edges = {k: ph[k] for k in ("att_cell_gather", "dec_cell_gather")}
+            xcd_edges = {k: ph[k] for k in ("att_early_wait_pre1", "wait_prenet2", "wait_query", "wait_ctx")}
             us = kdom["us_per_decoder_step"]
+            floor = 2 * EDGE_DEVICE_US + 4 * EDGE_XCD_US
             roofline["diagnostics"] = dict(
-                limiter="device-wide hand-off latency (3 all-to-all edges per step); weights on chip",
+                limiter="hand-off latency: 2 device-wide + 4 XCD-local edges per step; weights on chip",
                 fp32_flops_per_launch=flops, fp32_tflops=flops / (dec_ms * 1e-3) / 1e12,
                 fp32_compute_frac=flops / (dec_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF,
-                device_wide_edges_us_per_step=edges, handoff_floor_us_per_step=sum(edges.values()),
-                us_per_step=us, handoff_share_of_step=sum(edges.values()) / us)
+                device_wide_edges_us_per_step=dev_edges, xcd_local_edges_us_per_step=xcd_edges,
+                edge_microbench_us=dict(device_wide=EDGE_DEVICE_US, xcd_local=EDGE_XCD_US,
+                                        source="tools/microbench/edge.hip (one 16-byte granule pair per lane)"),
+                latency_floor_us=floor, step_over_floor=us / floor, us_per_step=us)
     # the headline workload's paths, before any other region runs on the same handles
     paths = dict(decoder="resident" if model.last_timing.get("resident") else "multi-launch",
                  encoder_bilstm={1: "resident", 2: "resident-batched"}.get(model.last_timing.get("encoder_path", 0), "per-step")
-                 if not gst else "per-step",
+                 if not gst else "bigru_kernel (the CBHG / GST recurrences: one launch each; the only path)",
                  griffin_lim=ap.last_gl_path())
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

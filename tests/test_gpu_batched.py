@@ -171,10 +171,17 @@ def test_config4_gst_batch32_full_cap_linear_griffin_lim_vs_oracle():
     assert rel_rms(wav[b, :nb], ref) < WAV_RTOL, (b, T)
 
 
-def test_synthesizer_tts_vs_oracle_chain(audio_cfg):
-    """Synthesizer.tts (server/synthesizer.py:128-162) on a 3-sentence text with the reference's
+@pytest.mark.parametrize("txt,sens_ref,dispatch", [
+    ("It took me quite a long time. Dr. Smith spoke! Ok? Then we left.",
+     ["It took me quite a long time.", "Dr. Smith spoke!", "Ok?", "Then we left."], "batch"),
+    ("It took me quite a long time. Dr. Smith spoke! Then we left.",
+     ["It took me quite a long time.", "Dr. Smith spoke!", "Then we left."], "serial-resident")])
+def test_synthesizer_tts_vs_oracle_chain(audio_cfg, txt, sens_ref, dispatch):
+    """Synthesizer.tts (server/synthesizer.py:128-162) on a multi-sentence text with the reference's
     numpy phases: split, drop len < 3, per-sentence Tacotron2 (cap 3000) + GL in order, 10 000-zero
-    gaps, one global peak -> int16, vs the oracle chain doing exactly that one sentence at a time."""
+    gaps, one global peak -> int16, vs the oracle chain doing exactly that one sentence at a time.
+    Four sentences decode as one batch, three as serial resident batch-1 calls (synthesis.py:
+    SERIAL_RESIDENT_MAX); Griffin-Lim is one batch either way."""
     import scipy.io.wavfile
     text = load_pkg("text")
     synth = load_pkg("synthesis")
@@ -183,11 +190,11 @@ def test_synthesizer_tts_vs_oracle_chain(audio_cfg):
     ap = load_pkg("audio").AudioProcessor(**a)
     adapter = lambda s: text.text_to_sequence(s, ["basic_cleaners"])  # noqa: E731
     s = synth.Synthesizer(m, ap, cfg, input_adapter=adapter)
-    txt = "It took me quite a long time. Dr. Smith spoke! Ok? Then we left."
     sens = s.sentences(txt)
-    assert sens == ["It took me quite a long time.", "Dr. Smith spoke!", "Ok?", "Then we left."]
+    assert sens == sens_ref
     np.random.seed(77)
     buf = s.tts(txt)
+    assert bool(m.last_timing["resident"]) == (dispatch == "serial-resident")
     buf.seek(0)
     sr, pcm = scipy.io.wavfile.read(buf)
     assert sr == 22050 and pcm.dtype == np.int16

@@ -62,6 +62,42 @@ def wav_to_int16(wav):
 
 
 # ------------------------------------------------------------------ batched pipeline
+# Requests of at most this many Tacotron2 sentences decode one sentence at a time on the resident
+# batch-1 decoder instead of as one multi-launch batch (tools/dispatch_crossover.py,
+# profiles/r05_dispatch_crossover.json: 3 sentences 102.6 vs 128.8 ms under the Synthesizer's
+# mask-off 3000-step configuration, 8.5 vs 12.7 ms under synthesize.py's mask; from 4 on the batch
+# wins).  Postnet per sentence, Griffin-Lim still one batch.  TTS_SERIAL_MAX overrides (0: off).
+SERIAL_RESIDENT_MAX = int(os.environ.get("TTS_SERIAL_MAX", "3"))
+
+
+def _decode(model, ids_list, speaker_ids=None):
+    """Tacotron2 decode of a request: serial resident calls below the crossover, else one batch."""
+    B = len(ids_list)
+    if B == 1 or B > SERIAL_RESIDENT_MAX or max(len(x) for x in ids_list) > 256:
+        out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
+        out["dispatch"] = "batch"
+        return out
+    from .tacotron2 import _speaker_array
+    spk = None if speaker_ids is None else _speaker_array(speaker_ids, B)
+    outs = []
+    for b, x in enumerate(ids_list):
+        outs.append(model.inference_batch([x], speaker_ids=None if spk is None else spk[b:b + 1]))
+        if b == 0 and not model.last_timing.get("resident"):
+            # no resident decoder on this handle: the rest as one batch is cheaper
+            outs.append(model.inference_batch(ids_list[1:], speaker_ids=None if spk is None else spk[1:]))
+            break
+    frames = [f for o in outs for f in o["frames"]]
+    steps = [n for o in outs for n in o["steps"]]
+    T = max(frames)
+    mel_post = torch.zeros(B, T, outs[0]["mel_post"].shape[2], device=outs[0]["mel_post"].device)
+    b = 0
+    for o in outs:
+        for k in range(len(o["frames"])):
+            mel_post[b, :o["frames"][k]] = o["mel_post"][k, :o["frames"][k]]
+            b += 1
+    return dict(mel_post=mel_post, frames=frames, steps=steps, dispatch="serial-resident")
+
+
 @torch.no_grad()
 def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed=0, phase="device",
                      iters=None, keep_outputs=False, style_mel=None):
@@ -72,7 +108,12 @@ def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed
     when it synthesises the sentences one after another.  Returns (wavs: list of float64 numpy
     arrays, info dict)."""
     linear = hasattr(model, "linear_dim")  # Tacotron / TacotronGST: linear-spectrogram GL
-    out = model.inference_batch(ids_list, speaker_ids=speaker_ids, **({"style_mel": style_mel} if linear else {}))
+    if linear:
+        out = model.inference_batch(ids_list, speaker_ids=speaker_ids, style_mel=style_mel)
+    elif keep_outputs:
+        out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
+    else:
+        out = _decode(model, ids_list, speaker_ids)
     frames = out["frames"]
     mel_post = out["linear"] if linear else out["mel_post"]
     phase_u = None
@@ -84,7 +125,8 @@ def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed
     mode = _native.TTS_GL_FROM_LINEAR if linear else _native.TTS_GL_FROM_MEL
     wav = ap.griffin_lim_batch(mel_post, frames, mode=mode, phase_u=phase_u, seed=seed, iters=iters)
     lens = [ap.hop_length * (T - 1) for T in frames]
-    info = dict(frames=frames, steps=out["steps"], samples=lens, **model.last_timing, **ap.last_gl_timing())
+    info = dict(frames=frames, steps=out["steps"], samples=lens, decoder_dispatch=out.get("dispatch", "batch"),
+                **model.last_timing, **ap.last_gl_timing())
     if keep_outputs:
         info.update(out)
         info["wav_dev"] = wav
