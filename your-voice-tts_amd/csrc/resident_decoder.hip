@@ -909,8 +909,20 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             wdef = tid < L ? weight(tid) : 0.f;
             n_prev = n;
             n = bi >= 0 ? bi + 1 : 0;  // argmax(prev_alpha) of the next step (its loads: h_att wait)
-#pragma unroll 2
-            for (int i = 0; i < 8; ++i) acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_att + i * 128 + ks * 4), acc_d);
+            // the deferred decoder-LSTM h_att half is on this CU's h_dec path: four chunks' LDS
+            // operands in flight at a time (the two-chunk loop waited out eight LDS round trips)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                float4 wv[4], xv4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    wv[j] = wdl[((4 * h + j) * 16 + r) * 32 + ks];
+                    xv4[j] = ld4(xh_att + (4 * h + j) * 128 + ks * 4);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc_d = dot4(wv[j], xv4[j], acc_d);
+                asm volatile("" ::: "memory");
+            }
             RES_MARK(9);
         }
         // this wave's prenet-1 row weights (step 11) from the XCD's L2, in flight while the context
