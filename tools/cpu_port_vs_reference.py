@@ -72,7 +72,7 @@ def main(out_path):
     res = {"workload": "configs[1] model half: Tacotron2 inference, one L=100 sentence (222 frames)",
            "cpu_model": _cpu_model(), "model": {}, "griffin_lim": {}}
     mel_post = None
-    for threads in (8, 1):
+    for threads in (8, 4, 1):
         torch.set_num_threads(threads)
 
         def ref_run():
@@ -80,8 +80,12 @@ def main(out_path):
                 return model.inference(x)
 
         with threadpool_limits(limits=threads, user_api="blas"):
-            tr, _ = median_time(ref_run, 5 if threads > 1 else 3)
-            tp, _ = median_time(lambda: port.inference(ids), 5 if threads > 1 else 3)
+            # interleaved medians (this host's 8 threads are noisy): reference, port, reference, port
+            trs, tps = [], []
+            for _ in range(2):
+                trs += median_time(ref_run, 4 if threads > 1 else 2)[1]
+                tps += median_time(lambda: port.inference(ids), 4 if threads > 1 else 2)[1]
+            tr, tp = statistics.median(trs), statistics.median(tps)
             tn, _ = median_time(lambda: port_np.inference(ids), 3)
         if mel_post is None:
             mel_post = ref_run()[1][0].numpy()
@@ -126,4 +130,4 @@ def _cpu_model():
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "cpu_port_vs_reference_r04.json"))
+    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "cpu_port_vs_reference_r05.json"))

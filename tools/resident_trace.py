@@ -26,9 +26,10 @@ EV = ("P1", "B1", "hatt_pub", "B3", "B4", "hdec_pub", "B6", "pre1_pub", "q_pub",
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=100)
+ap.add_argument("--nomask", action="store_true", help="Synthesizer.tts()'s configuration (general form)")
 args = ap.parse_args()
 cfg = gu.default_config("config_tacotron2.json")
-cfg.forward_attn_mask = True
+cfg.forward_attn_mask = not args.nomask
 m = gu.setup_model(130, cfg, max_batch=1, max_len=256)
 m.load_state_dict({k: torch.from_numpy(v) for k, v in weights.tacotron2_weights(0).items()})
 m.cuda().eval()
@@ -48,13 +49,15 @@ for t in steps:
     for k, name in enumerate(EV):
         v = tr[:, t, k]
         v = v[v > 0]
+        if v.size == 0:  # (an event this form does not record)
+            continue
         r = v - t0
         rel[name].append((r.min(), np.median(r), r.max()))
         if name in last:
             last[name][int(np.argmax(tr[:, t, k]))] += 1
 rec = {"us_per_step_trace": float(np.median(period)),
        "events_rel_step_start_us(min,median,max)": {k: [round(float(x), 2) for x in np.median(np.array(v), 0)]
-                                                    for k, v in rel.items()},
+                                                    for k, v in rel.items() if v},
        "last_cu": {k: v.most_common(6) for k, v in last.items()},
        "phases": ph}
 print(json.dumps(rec, indent=1))
