@@ -254,16 +254,18 @@ def _physical_cores():
     return max(1, n), "; ".join(how)
 
 
-def _port_over_reference():
+def _port_over_reference(section="model"):
     """The committed CPU port vs reference timing (tools/cpu_port_vs_reference.py, build container:
-    the reference cannot run on the GPU box)."""
+    the reference cannot run on the GPU box); section "model" (Tacotron2) or "gst_model"."""
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "cpu_port_vs_reference_r*.json")), reverse=True):
         try:
             d = json.load(open(p))
         except Exception:
             continue
-        out = {f"model_{k}": round(v["port_over_reference"], 3) for k, v in d.get("model", {}).items()}
-        if "griffin_lim" in d:
+        if section not in d:
+            continue
+        out = {f"model_{k}": round(v["port_over_reference"], 3) for k, v in d[section].items()}
+        if "griffin_lim" in d and section == "model":
             out["griffin_lim_60"] = round(d["griffin_lim"]["port_over_reference"], 3)
         out["source"] = os.path.relpath(p, REPO) + " (" + d.get("cpu_model", "?") + ")"
         return out
@@ -271,28 +273,41 @@ def _port_over_reference():
 
 
 def cpu_baseline_gst(args):
-    """Oracle TacotronGST (fp32) + linear GL (fp64) on the host for ONE config-5 sentence (sentence 0:
-    its L, speaker 0, style mel 0), full 500-step cap and 60 GL iterations."""
+    """The reference's CPU path for configs[4] restated on the host: TacotronGST as torch-CPU modules
+    (oracle/tacotron_torch.py, the reference's module tree and op order) on the process's physical
+    cores + the linear Griffin-Lim restatement (fp64, scipy.fftpack, single-threaded) for ONE config-5
+    sentence (sentence 0: its L, speaker 0, style mel 0), full 500-step cap and 60 GL iterations."""
     from oracle.griffin_lim_oracle import AudioOracle
-    from oracle.tacotron_oracle import TacotronOracle
+    from oracle.tacotron_torch import TacotronTorchCPU
     cfg = gu.default_config("config_tacotron_gst.json")
-    o = TacotronOracle(weights.tacotron_gst_weights(0, num_speakers=4), dtype=np.float32, r=cfg.r,
-                       memory_size=cfg.memory_size, attn_norm=cfg.attention_norm, forward_attn=cfg.use_forward_attn,
-                       trans_agent=cfg.transition_agent, forward_attn_mask=cfg.forward_attn_mask,
-                       location_attn=cfg.location_attn, attn_win=cfg.windowing, max_decoder_steps=500)
+    o = TacotronTorchCPU(weights.tacotron_gst_weights(0, num_speakers=4), r=cfg.r, memory_size=cfg.memory_size,
+                         attn_norm=cfg.attention_norm, forward_attn=cfg.use_forward_attn,
+                         trans_agent=cfg.transition_agent, forward_attn_mask=cfg.forward_attn_mask,
+                         location_attn=cfg.location_attn, attn_win=cfg.windowing, max_decoder_steps=500)
     ap = AudioOracle(**{**cfg.audio, "griffin_lim_iters": args.iters})
     L = int(weights.synthetic_lengths(1, 4)[0])
     ids = weights.synthetic_ids(L, 200)
     style = np.random.Generator(np.random.PCG64(4)).uniform(0, 1, size=(1, 200, 80)).astype(np.float32)[0]
-    t0 = time.time()
-    res = o.inference(ids, 0, style)
-    np.random.seed(0)
-    ap.inv_spectrogram(res["linear"].T)
-    dt = time.time() - t0
+    threads, how = _physical_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        o.inference(ids[:8], 0, style)  # warm (allocator, thread pool)
+        t0 = time.time()
+        res = o.inference(ids, 0, style)
+        t_model = time.time() - t0
+        np.random.seed(0)
+        ap.inv_spectrogram(res["linear"].T)
+        dt = time.time() - t0
+    finally:
+        torch.set_num_threads(prev_threads)
     T = res["mel"].shape[0]
-    return dict(value=T / dt, unit="mel-frames/s", cores=int(_threads()), kind="port", cpu_model=_cpu_model(),
-                sample=f"1 config-5 sentence (L={L}, {T} frames): numpy oracle TacotronGST (fp32) + linear GL "
-                       f"{args.iters} iters (fp64, scipy.fftpack) on the host, {dt:.1f} s",
+    return dict(value=T / dt, unit="mel-frames/s", cores=int(threads), cores_how=how, kind="port",
+                cpu_model=_cpu_model(),
+                sample=f"1 config-5 sentence (L={L}, {T} frames): torch-CPU TacotronGST (fp32, {threads} threads, "
+                       f"{t_model:.2f} s) + linear GL {args.iters} iters (fp64, scipy.fftpack, single-threaded) on the "
+                       f"host, {dt:.1f} s",
+                model_half_frames_per_s=T / t_model, port_over_reference=_port_over_reference("gst_model"),
                 rtf=dt / (275 * (T - 1) / 22050.0))
 
 

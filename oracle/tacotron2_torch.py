@@ -98,10 +98,13 @@ class _Attention(nn.Module):
         self.v = _Wrapped(_t(sd[a + "v.linear_layer.weight"]), _t(sd[a + "v.linear_layer.bias"]))
         if owner.location_attn:
             cw = _t(sd[a + "location_layer.location_conv.weight"])
-            self.location_conv = nn.Conv1d(2, cw.shape[0], cw.shape[2], padding=(cw.shape[2] - 1) // 2, bias=False)
+            self.location_layer = nn.Module()
+            self.location_layer.location_conv = nn.Conv1d(2, cw.shape[0], cw.shape[2], padding=(cw.shape[2] - 1) // 2,
+                                                          bias=False)
             with torch.no_grad():
-                self.location_conv.weight.copy_(cw)
-            self.location_dense = _Wrapped(_t(sd[a + "location_layer.location_dense.linear_layer.weight"]))
+                self.location_layer.location_conv.weight.copy_(cw)
+            self.location_layer.location_dense = _Wrapped(
+                _t(sd[a + "location_layer.location_dense.linear_layer.weight"]))
         if owner.trans_agent:
             self.ta = nn.Linear(_t(sd[a + "ta.weight"]).shape[1], 1)
             with torch.no_grad():
@@ -123,7 +126,8 @@ class _Attention(nn.Module):
         pq = self.query_layer(query.unsqueeze(1))
         if o.location_attn:
             cat = torch.cat((self.attention_weights.unsqueeze(1), self.attention_weights_cum.unsqueeze(1)), 1)
-            loc = self.location_dense(self.location_conv(cat).transpose(1, 2))
+            ll = self.location_layer
+            loc = ll.location_dense(ll.location_conv(cat).transpose(1, 2))
             energies = self.v(torch.tanh(pq + loc + processed_inputs)).squeeze(-1)
         else:
             energies = self.v(torch.tanh(pq + processed_inputs)).squeeze(-1)

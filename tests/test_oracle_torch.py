@@ -26,3 +26,30 @@ def test_torch_cpu_restatement_matches_reference(case):
     assert rel_rms(res["mel"], z["mel"]) < 1e-4
     assert rel_rms(res["mel_post"], z["mel_post"]) < 1e-4
     assert np.abs(res["align"] - z["align"]).max() < 1e-4
+
+
+TACO_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gst_*.npz")) +
+                    glob.glob(os.path.join(GOLDEN, "taco_*.npz")))
+
+
+@pytest.mark.parametrize("case", TACO_CASES)
+def test_tacotron_torch_cpu_restatement_matches_reference(case):
+    """The configs[4] CPU baseline's model (oracle/tacotron_torch.py) vs the reference's own outputs."""
+    from oracle.tacotron_torch import TacotronTorchCPU
+    z = golden(case)
+    fl = dict(golden_flags(z))
+    bn = fl.get("prenet_type", "original") == "bn"
+    sd = weights_mod().tacotron_gst_weights(0, num_speakers=fl["num_speakers"], r=fl["r"],
+                                            memory_size=fl["memory_size"], location_attn=fl["location_attn"],
+                                            trans_agent=fl["trans_agent"], gst=fl["model"] == "TacotronGST",
+                                            prenet_bn=bn)
+    o = TacotronTorchCPU(sd, **fl)
+    sid = int(z["speaker_id"])
+    res = o.inference(z["ids"], None if sid < 0 else sid, z["style_mel"] if "style_mel" in z else None)
+    assert rel_rms(res["enc"], z["enc"]) < 1e-5
+    assert res["align"].shape == z["align"].shape, "step count differs from the reference"
+    np.testing.assert_array_equal(res["align"].argmax(1), z["align"].argmax(1))
+    np.testing.assert_array_equal(res["stop"] > 0.6, z["stop"] > 0.6)
+    assert rel_rms(res["mel"], z["mel"]) < 1e-4
+    assert rel_rms(res["linear"], z["linear"]) < 1e-4
+    assert np.abs(res["align"] - z["align"]).max() < 1e-4

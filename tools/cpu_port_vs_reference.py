@@ -93,6 +93,40 @@ def main(out_path):
                                                   numpy_oracle_s=tn, numpy_over_reference=tn / tr)
         print(threads, "threads: reference", tr, "torch port", tp, "ratio", tp / tr, "numpy", tn, flush=True)
 
+    # configs[4]'s model half: the reference TacotronGST (config_tacotron_gst.json, 4 speakers) on
+    # config-5 sentence 0 (its L, speaker 0, style mel 0, 500-step cap) vs oracle/tacotron_torch.py
+    from oracle.tacotron_torch import TacotronTorchCPU
+    Cg = load_config(os.path.join(mg.REF, "config_tacotron_gst.json"))
+    Cg.num_speakers = 4
+    gmodel = setup_model(130, 4, Cg)
+    gsd = mg.weights.tacotron_gst_weights(0, num_speakers=4)
+    gmodel.load_state_dict({k: torch.from_numpy(v) for k, v in gsd.items()})
+    gmodel.eval()
+    gport = TacotronTorchCPU(gsd, r=Cg.r, memory_size=Cg.memory_size, attn_norm=Cg.attention_norm,
+                             forward_attn=Cg.use_forward_attn, trans_agent=Cg.transition_agent,
+                             forward_attn_mask=Cg.forward_attn_mask, location_attn=Cg.location_attn,
+                             attn_win=Cg.windowing, max_decoder_steps=500)
+    Lg = int(mg.weights.synthetic_lengths(1, 4)[0])
+    gids = mg.weights.synthetic_ids(Lg, 200)
+    style = np.random.Generator(np.random.PCG64(4)).uniform(0, 1, size=(1, 200, 80)).astype(np.float32)
+    gx, gstyle, gspk = torch.from_numpy(gids)[None], torch.from_numpy(style), torch.tensor([0])
+    res["gst_workload"] = f"configs[4] model half: TacotronGST inference, one L={Lg} sentence, 500-step cap"
+    res["gst_model"] = {}
+    for threads in (8, 4, 1):
+        torch.set_num_threads(threads)
+
+        def gref():
+            with torch.no_grad():
+                return gmodel.inference(gx, speaker_ids=gspk, style_mel=gstyle)
+
+        trs, tps = [], []
+        for _ in range(2):
+            trs += median_time(gref, 2 if threads > 1 else 1)[1]
+            tps += median_time(lambda: gport.inference(gids, 0, style[0]), 2 if threads > 1 else 1)[1]
+        tr, tp = statistics.median(trs), statistics.median(tps)
+        res["gst_model"][f"threads_{threads}"] = dict(reference_s=tr, port_s=tp, port_over_reference=tp / tr)
+        print("GST", threads, "threads: reference", tr, "torch port", tp, "ratio", tp / tr, flush=True)
+
     # Griffin-Lim 60: reference AudioProcessor glue (librosa = the restatement) vs AudioOracle
     a = dict(tacotron2_config()["audio"])
     a["griffin_lim_iters"] = 60
