@@ -124,6 +124,16 @@ def build(args, device):
     return cfg, model, ap
 
 
+def build_server_model(args):
+    """Synthesizer.tts()'s model (server/synthesizer.py:46-66): config_tacotron2.json as it is (forward
+    attention, sigmoid, eval mask OFF) with the 3000-step decoder cap; same generator weights."""
+    cfg = gu.default_config("config_tacotron2.json")
+    model = gu.setup_model(130, cfg, max_batch=1, max_len=max(args.L, 256))
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in weights.tacotron2_weights(0).items()})
+    model.decoder.max_decoder_steps = 3000
+    return model.cuda().eval()
+
+
 def make_job(args, world, rank, max_steps, model=None, batch=None, lengths=None, seed=None):
     """The whole job's sentences (world x batch) and this rank's LPT share (sharding.py)."""
     model = args.model if model is None else model
@@ -707,6 +717,22 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+    server = None
+    if world == 1 and not gst and not args.no_share:
+        # the Synthesizer.tts() configuration on the same L=100 sentence (mask off: it runs to the
+        # 3000-step cap under random weights), one sentence per step through the same one-call path;
+        # bounded to 3 timed steps (~35 ms each)
+        sm = build_server_model(args)
+        sargs = argparse.Namespace(**{**vars(args), "steps": min(args.steps, 3), "warmup": 1})
+        tm = timed_region(lambda seed: run_step(sm, ap, ids, [0], 1, seed=seed)[0], sargs, 1, device, ap.hop_length,
+                          ap.sample_rate)
+        collect_status(sm)
+        server = share_record(tm, 1)
+        server.update(steps=sargs.steps, decoder="resident" if sm.last_timing.get("resident") else "multi-launch",
+                      note="Synthesizer.tts()'s model (config_tacotron2.json: forward attention, sigmoid, mask off, "
+                           "3000-step cap; server/synthesizer.py:46-66), one L=100 sentence per step, GL "
+                           f"{args.iters} iters: the general-form resident decoder")
+        del sm
     share = None
     if world == 1 and not gst and not args.no_share:
         # the driver's N=8 line runs configs[3]'s 64-sentence share per rank: time that same share
@@ -759,6 +785,8 @@ def main():
         "kernels_rank0": kernels,
     }
     rec.update(scaling_keys(timing, ref, world, share))
+    if server is not None:
+        rec["synthesizer_config_1rank"] = server
     print(json.dumps(rec))
     if world > 1:
         dist.barrier()
