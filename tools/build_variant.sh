@@ -7,7 +7,8 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 W=$R/your-voice-tts_amd/csrc_var_$name
 rm -rf "$W" && cp -r "$R/your-voice-tts_amd/csrc" "$W" && rm -rf "$W/build"
 for kv in "$@"; do cp "${kv#*=}" "$W/${kv%%=*}"; done
-mkdir -p "$R/variants"
-make -C "$W" -j8 OUT="$R/variants/lib_$name.so" >/dev/null
+OUTD=${OUTD:-variants}
+mkdir -p "$R/$OUTD"
+make -C "$W" -j8 OUT="$R/$OUTD/lib_$name.so" >/dev/null
 rm -rf "$W"
-echo "variants/lib_$name.so"
+echo "$OUTD/lib_$name.so"

@@ -802,7 +802,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             if (flags[1]) break;
             RES_MARK(6);
             bool full = t == 0;
-            float rm = -INFINITY;
+            float rm = -INFINITY, cand = -INFINITY;
             if (!full) {
                 float part = 0.f;
 #pragma unroll
@@ -821,11 +821,10 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 __syncthreads();  // A2
                 if (tid == 0) { RES_EV(t, 10) }
                 RES_MARK(14);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float4 v4 = reinterpret_cast<const float4*>(candv)[k];
-                    rm = fmaxf(rm, fmaxf(fmaxf(v4.x, v4.y), fmaxf(v4.z, v4.w)));
-                }
+                // one LDS read per lane (slot lane % 16), the max by DPP, the window slots 1-4 by
+                // readlane below: no chain of dependent LDS reads
+                cand = candv[lane & 15];
+                rm = wave_max_dpp(cand);
                 full = !(rm >= 1e-8f);  // uniform
             }
             if (full) {
@@ -865,9 +864,14 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             }
             RES_MARK(7);
             // the surviving window [n-1, n+2] without (n-2) mod L: its unnormalised weights once
+            // the surviving window's unnormalised weights: candidate slots 1-4 hold exactly an[clo + k]
+            // (the same lane wrote both); the full-L path reads them from an[]
             float aw[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) aw[k] = (clo + k <= chi && clo + k != cx) ? an[clo + k] : 0.f;
+            for (int k = 0; k < 4; ++k) {
+                const float c = full ? an[clo + k] : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), 1 + k));
+                aw[k] = (clo + k <= chi && clo + k != cx) ? c : 0.f;
+            }
             const float rs = ((aw[0] + aw[1]) + aw[2]) + aw[3];  // index order
             const float vx = 0.01f * rm;  // alpha[n-2] = 0.01 * val
             const float denom = rs + vx;
