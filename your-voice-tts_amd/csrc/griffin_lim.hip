@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <map>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -145,100 +146,249 @@ __device__ double2* fft1024(double2* src, double2* dst, const FftTw& tw) {
 // 4-way bank conflicts; contiguous reads stay a permutation of one row.
 __device__ __forceinline__ int swz(int i) { return i ^ (5 * ((i >> 4) & 3)); }
 
-// fft1024 with register edges: thread j enters with z[j + 256 r] (r = 0..3) in v -- the operands of
-// its first radix-4 butterfly (Ns = 1, untwiddled) -- so the first pass reads no LDS; with TO_REGS
-// the last pass (Ns = 256, whose outputs of thread j are z[j + 256 r] again) leaves its results in v
-// instead of LDS (returns null).  Same operations in the same order as fft1024: bitwise equal.
-// The buffers hold point i at swz(i).
-// Pass 0 writes `dst`; the caller's previous readers of both buffers must have passed a barrier.
-template <bool INV, bool TO_REGS>
-__device__ double2* fft1024_regs(double2 (&v)[4], double2* src, double2* dst, const FftTw& tw) {
-    const int j = threadIdx.x;
-#pragma unroll
-    for (int Ns = 1, p = -1; Ns < NH; Ns *= 4, ++p) {
-        const int k = j & (Ns - 1);
-        if (Ns > 1) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = src[swz(j + r * 256)];
-#pragma unroll
-            for (int r = 1; r < 4; ++r) {
-                double2 w = tw.w[p][r - 1];
-                if (INV) w = cconj(w);
-                v[r] = cmul(v[r], w);
-            }
-        }
-        const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
-        const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
-        const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
-        const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
-        const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
-        v[0] = double2{a0.x + a2.x, a0.y + a2.y};
-        v[1] = double2{a1.x + m3.x, a1.y + m3.y};
-        v[2] = double2{a0.x - a2.x, a0.y - a2.y};
-        v[3] = double2{a1.x - m3.x, a1.y - m3.y};
-        if (TO_REGS && Ns == NH / 4) return nullptr;  // idxD = j: v[r] is z[j + 256 r]
-        const int idxD = (j / Ns) * Ns * 4 + k;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[swz(idxD + r * Ns)] = v[r];
-        __syncthreads();
-        double2* t = src;
-        src = dst;
-        dst = t;
-    }
-    return src;
+// ---- two-level 1024-point complex FFT of one 256-thread workgroup (round 5).  1024 = 4 x 256:
+// one radix-4 step ACROSS the four waves, thread-local in registers, and one 256-point Stockham
+// radix-4 FFT per wave whose three LDS exchanges stay inside that wave's own 256-slot region.  A
+// wave's LDS operations execute in issue order, so the wave-local exchanges need no barrier: the
+// transform has ONE workgroup barrier (the cross-wave hand-over) instead of four.
+//   layout A (thread t = 64 w + l):  v[r] = z[t + 256 r]          (edge_sample: STFT input, iSTFT output)
+//   layout B (wave w, lane l):        v[r] = Z[4 (l + 64 r) + w]   (the spectrum's bins)
+// Forward, decimation in frequency, A -> B:
+//   u_q[m] = W1024^(m q) sum_s z[m + 256 s] W4^(s q)  (thread m: a butterfly over its registers),
+//   Z[4 k1 + q] = sum_m u_q[m] W256^(m k1)            (wave q: 256-point FFT over m = l + 64 r);
+// inverse, decimation in time, B -> A: the same two steps in reverse order with conjugate twiddles.
+// Region q of a buffer is slots [256 q, 256 q + 256), points XOR-swizzled by swz (the Stockham
+// store patterns of a 256-point pass are the first three of the 1024-point one).
+// threadIdx.x through an opaque copy: LDS addresses derived from it are recomputed per transform
+// instead of hoisted out of the persistent loop, where dozens of them would stay live (and spill)
+__device__ __forceinline__ int tid_opaque() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
 }
+template <bool INV>
+__device__ __forceinline__ void bfly4(double2 (&v)[4]) {
+    const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
+    const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
+    const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
+    const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
+    // -i*a3 = (a3.y, -a3.x); +i*a3 = (-a3.y, a3.x)
+    const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
+    v[0] = double2{a0.x + a2.x, a0.y + a2.y};
+    v[1] = double2{a1.x + m3.x, a1.y + m3.y};
+    v[2] = double2{a0.x - a2.x, a0.y - a2.y};
+    v[3] = double2{a1.x - m3.x, a1.y - m3.y};
+}
+// Twiddles of the two-level FFT (entries of the 2048-point table tw[m] = W2048^m):
+//   fx(q)     = W1024^(t q), q = 1..3            (forward cross-wave step, thread t)
+//   ix(r)     = W1024^((l + 64 r) w)             (inverse cross-wave step, wave w, lane l)
+//   ps(p, r)  = W_(4 Ns)^(r (l mod Ns)), r = 1..3 (wave pass p = 0, 1, 2: Ns = 4, 16, 64)
+// TwRegs holds all 16 in registers for the kernel's lifetime (the persistent loop: one wave per
+// SIMD, registers to spare); TwTable reads the L2-resident table where they are used (the
+// register-budget forms).  Same values either way, so the forms are bitwise equal.
+struct TwRegs {
+    double2 f[3], i[4], p[3][3];
+    __device__ __forceinline__ void load(const double2* __restrict__ tw) {
+        const int t = threadIdx.x, l = t & 63, w = t >> 6;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) f[q - 1] = tw[2 * t * q];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) i[r] = tw[2 * (l + 64 * r) * w];
+#pragma unroll
+        for (int ps = 0; ps < 3; ++ps) {
+            const int Ns = 4 << (2 * ps);
+#pragma unroll
+            for (int r = 1; r < 4; ++r) p[ps][r - 1] = tw[(l & (Ns - 1)) * r * (512 / Ns)];
+        }
+    }
+    __device__ __forceinline__ double2 tw_at(int) const { return double2{0.0, 0.0}; }  // (TwTable only)
+    __device__ __forceinline__ double2 fx(int q) const { return f[q - 1]; }
+    __device__ __forceinline__ double2 ix(int r) const { return i[r]; }
+    __device__ __forceinline__ double2 ps(int p_, int r) const { return p[p_][r - 1]; }
+};
+// TwMix (the two-per-CU persistent form's register budget): the forward cross-wave twiddles in
+// registers, the wave passes' from a 252-entry LDS copy (pt: [pass][l mod Ns][r - 1], 4 KB), the
+// inverse cross-wave ones from the table (fetched ahead of the wave FFT).
+constexpr int TW_LDS = 3 * (4 + 16 + 64);
+__device__ __forceinline__ int tw_lds_base(int p_) { return p_ == 0 ? 0 : p_ == 1 ? 12 : 60; }
+typedef __attribute__((address_space(1))) const double g_d;  // global
+typedef __attribute__((address_space(3))) const double l_d;  // LDS
+struct TwMix {
+    g_d* tw;  // (address-space-qualified scalars: the table reads stay global / LDS loads)
+    l_d* pt;
+    double2 f[3];
+    __device__ __forceinline__ void load(const double2* __restrict__ t) {
+        const int j = threadIdx.x;
+        tw = (g_d*)t;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) f[q - 1] = t[2 * j * q];
+    }
+    // fill the LDS copy (every thread; the caller's barrier orders it before the first use)
+    __device__ __forceinline__ static void fill(double2* lds, const double2* __restrict__ t) {
+        for (int e = threadIdx.x; e < TW_LDS; e += blockDim.x) {
+            const int p_ = e < 12 ? 0 : e < 60 ? 1 : 2, o = e - tw_lds_base(p_);
+            const int Ns = 4 << (2 * p_), k = o / 3, r = o % 3 + 1;
+            lds[e] = t[k * r * (512 / Ns)];
+        }
+    }
+    __device__ __forceinline__ double2 tw_at(int k) const { return double2{tw[2 * k], tw[2 * k + 1]}; }
+    __device__ __forceinline__ double2 fx(int q) const { return f[q - 1]; }
+    __device__ __forceinline__ double2 ix(int r) const {
+        return tw_at(2 * (((int)threadIdx.x & 63) + 64 * r) * ((int)threadIdx.x >> 6));
+    }
+    __device__ __forceinline__ double2 ps(int p_, int r) const {
+        const int Ns = 4 << (2 * p_), e = tw_lds_base(p_) + ((int)threadIdx.x & (Ns - 1)) * 3 + r - 1;
+        return double2{pt[2 * e], pt[2 * e + 1]};
+    }
+};
+struct TwTable {
+    const double2* __restrict__ tw;
+    __device__ __forceinline__ double2 tw_at(int k) const { return tw[k]; }
+    __device__ __forceinline__ double2 fx(int q) const { return tw[2 * (int)threadIdx.x * q]; }
+    __device__ __forceinline__ double2 ix(int r) const {
+        return tw[2 * (((int)threadIdx.x & 63) + 64 * r) * ((int)threadIdx.x >> 6)];
+    }
+    __device__ __forceinline__ double2 ps(int p_, int r) const {
+        const int Ns = 4 << (2 * p_);
+        return tw[((int)threadIdx.x & (Ns - 1)) * r * (512 / Ns)];
+    }
+};
 
-// fft1024_regs with the twiddles read from the global table pass by pass (each pass's three
-// issued one pass ahead, so only the first waits on memory) instead of living in 48 VGPRs for the
-// whole kernel: the occupancy form of gl_iter_kernel.  Same values, same operations: bitwise
-// equal to fft1024_regs.
-template <bool INV, bool TO_REGS>
-__device__ double2* fft1024_regs_gtw(double2 (&v)[4], double2* src, double2* dst, const double2* __restrict__ tw) {
-    const int j = threadIdx.x;
+// 256-point Stockham radix-4 FFT of one wave, in place in its region rg: enters with v[r] =
+// u[l + 64 r] (the first pass's operands, so it reads no LDS), leaves v[r] = U[l + 64 r] (the last
+// pass's outputs stay in registers).  Each pass's twiddles are fetched one pass ahead.
+template <bool INV, class TW>
+__device__ __forceinline__ void wave_fft256(double2 (&v)[4], double2* rg, int l, const TW& tw) {
+    asm volatile("" : "+v"(l));
     double2 w[3];
 #pragma unroll
-    for (int r = 1; r < 4; ++r) w[r - 1] = tw[(j & 3) * r * 128];  // Ns = 4: 512 / Ns = 128
+    for (int r = 1; r < 4; ++r) w[r - 1] = tw.ps(0, r);
 #pragma unroll
-    for (int Ns = 1; Ns < NH; Ns *= 4) {
-        const int k = j & (Ns - 1);
-        if (Ns > 1) {
+    for (int p = -1; p < 3; ++p) {
+        const int Ns = 1 << (2 * (p + 1));
+        if (p >= 0) {
             double2 wn[3];
-            if (Ns < NH / 4) {  // next pass's twiddles (Ns' = 4 Ns, stride 512 / Ns')
-                const int k2 = j & (4 * Ns - 1);
+            if (p < 2) {
 #pragma unroll
-                for (int r = 1; r < 4; ++r) wn[r - 1] = tw[k2 * r * (128 / Ns)];
+                for (int r = 1; r < 4; ++r) wn[r - 1] = tw.ps(p + 1, r);
             }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = src[swz(j + r * 256)];
+            for (int r = 0; r < 4; ++r) v[r] = rg[swz(l + 64 * r)];
 #pragma unroll
             for (int r = 1; r < 4; ++r) v[r] = cmul(v[r], INV ? cconj(w[r - 1]) : w[r - 1]);
-            if (Ns < NH / 4) {
+            if (p < 2) {
 #pragma unroll
                 for (int r = 0; r < 3; ++r) w[r] = wn[r];
             }
         }
-        const double2 a0 = double2{v[0].x + v[2].x, v[0].y + v[2].y};
-        const double2 a1 = double2{v[0].x - v[2].x, v[0].y - v[2].y};
-        const double2 a2 = double2{v[1].x + v[3].x, v[1].y + v[3].y};
-        const double2 a3 = double2{v[1].x - v[3].x, v[1].y - v[3].y};
-        const double2 m3 = INV ? double2{-a3.y, a3.x} : double2{a3.y, -a3.x};
-        v[0] = double2{a0.x + a2.x, a0.y + a2.y};
-        v[1] = double2{a1.x + m3.x, a1.y + m3.y};
-        v[2] = double2{a0.x - a2.x, a0.y - a2.y};
-        v[3] = double2{a1.x - m3.x, a1.y - m3.y};
-        if (TO_REGS && Ns == NH / 4) return nullptr;
-        const int idxD = (j / Ns) * Ns * 4 + k;
+        bfly4<INV>(v);
+        if (p == 2) return;  // Ns = 64: lane l's outputs are U[l + 64 r]
+        const int idxD = (l / Ns) * Ns * 4 + (l & (Ns - 1));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dst[swz(idxD + r * Ns)] = v[r];
-        __syncthreads();
-        double2* t = src;
-        src = dst;
-        dst = t;
+        for (int r = 0; r < 4; ++r) rg[swz(idxD + r * Ns)] = v[r];
+        __builtin_amdgcn_wave_barrier();  // (code motion only: the wave's LDS ops run in order)
     }
-    return src;
+}
+// Forward two-level FFT, layout A -> B.  Writes every region of wr (the caller's earlier readers
+// of wr must be past a barrier); one barrier.
+template <class TW>
+__device__ __forceinline__ void fft2l_fwd(double2 (&v)[4], double2* wr, const TW& tw) {
+    const int t = tid_opaque(), l = t & 63, w = threadIdx.x >> 6;
+    bfly4<false>(v);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) v[q] = cmul(v[q], tw.fx(q));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wr[256 * q + swz(t)] = v[q];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = wr[256 * w + swz(l + 64 * r)];
+    wave_fft256<false>(v, wr + 256 * w, l, tw);
+}
+// Inverse two-level FFT, layout B -> A (unnormalised).  Uses region w of wr first (the caller's
+// earlier readers of that region must be past a barrier), then reads every region; one barrier.
+template <class TW>
+__device__ __forceinline__ void fft2l_inv(double2 (&v)[4], double2* wr, const TW& tw) {
+    const int t = tid_opaque(), l = t & 63, w = threadIdx.x >> 6;
+    double2* rg = wr + 256 * w;
+    double2 iw[4];  // (fetched ahead of the wave FFT: in flight during it when read from the table)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) iw[r] = tw.ix(r);
+    wave_fft256<true>(v, rg, l, tw);
+    if (w != 0) {  // (wave 0's twiddles are 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = cmul(v[r], cconj(iw[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rg[swz(l + 64 * r)] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = wr[256 * q + swz(t)];
+    bfly4<true>(v);
 }
 
-// Real sample i (0..7) of thread j at the register edges of fft1024_regs: complex point j + 256 (i/2),
+// Bin k of the thread's register r in layout B
+__device__ __forceinline__ int bin2l(int t, int r) { return 4 * ((t & 63) + 64 * r) + (t >> 6); }
+__device__ __forceinline__ int bin2l(int r) { return bin2l((int)threadIdx.x, r); }
+// STFT value of bin k from zk = Z[k mod 1024] and zm = Z[(1024 - k) mod 1024] (real-FFT split),
+// rounded to complex64 (librosa stft dtype), then |S| exp(i angle X) (angle(0) = 0) in float64
+// (utils/audio.py:187-188) by one reciprocal square root (the float-rounded components square
+// exactly in double): no divisions on the iteration's critical path.  Im = 0 at DC and Nyquist
+// (istft: .real of the Hermitian extension).
+__device__ __forceinline__ double2 spec_bin(double2 zk, double2 zm, double2 t, double s, bool edge) {
+    const double2 zc = cconj(zm);
+    const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
+    const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};  // -i (zk - zc) / 2
+    const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
+    const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
+    const double m2 = xre * xre + xim * xim;
+    const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
+    double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
+    if (edge) xv.y = 0.0;
+    return xv;
+}
+// Forward spectrum step in layout B: v = Z on entry, X = |S| X/|X| on return; the Nyquist bin
+// X[1024] goes to xnyq of thread 0 (wave 0, lane 0: it holds Z[0] and is the only reader of
+// X[1024]).  zb: 1024 slots (one barrier after the Z stores; the caller's earlier readers of zb
+// must be past a barrier).  tk(r) = W2048^k and sk(r) = |S|[k] for the thread's bins k = bin2l(r);
+// tnyq / snyq: the same for k = 1024 (thread 0).
+template <class TK, class SK>
+__device__ __forceinline__ void spectrum2l(double2 (&v)[4], double2* zb, TK tk, SK sk, double2 tnyq, double snyq,
+                                           double2& xnyq) {
+    const int t = tid_opaque();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zb[swz(bin2l(t, r))] = v[r];
+    __syncthreads();
+    if (threadIdx.x == 0) xnyq = spec_bin(v[0], v[0], tnyq, snyq, true);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int k = bin2l(t, r);
+        v[r] = spec_bin(v[r], zb[swz((NH - k) & (NH - 1))], tk(r), sk(r), k == 0);
+    }
+}
+// Inverse real-FFT pre-split in layout B: v = X on entry, z'[k] = E + i O on return
+// (E = (X[k] + conj X[N-k]) / 2, O = (X[k] - conj X[N-k]) / 2 * conj(t)); xb: 1024 slots (one
+// barrier after the X stores; the caller's earlier readers of xb must be past a barrier).
+template <class TK>
+__device__ __forceinline__ void presplit2l(double2 (&v)[4], double2* xb, TK tk, double2 xnyq) {
+    const int t = tid_opaque();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xb[swz(bin2l(t, r))] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int k = bin2l(t, r);
+        const double2 xk = v[r];
+        double2 xm = xb[swz((NH - k) & (NH - 1))];
+        if (r == 0 && k == 0) xm = xnyq;  // (bin 0 pairs with the Nyquist bin: thread 0, register 0)
+        const double2 xc = cconj(xm);
+        const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
+        const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
+        const double2 O = cmul(D, cconj(tk(r)));
+        v[r] = double2{E.x - O.y, E.y + O.x};  // E + i O
+    }
+}
+
+// Real sample i (0..7) of thread j in layout A (fft2l_fwd's input, fft2l_inv's output): complex point j + 256 (i/2),
 // real part (i even) or imaginary part (i odd) = real sample 2 j + 512 (i/2) + (i & 1).
 __device__ __forceinline__ int edge_sample(int j, int i) { return 2 * j + 512 * (i >> 1) + (i & 1); }
 
@@ -320,9 +470,9 @@ struct MagArgs {
     int signal_norm, symmetric, clip;
 };
 
-// _denormalize (utils/audio.py:96-112) then _db_to_amp(x + ref_level_db) (:125-126), in float32
-// as numpy computes them on the float32 network output.
-__device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) {
+// _denormalize (utils/audio.py:96-112) then the exponent of _db_to_amp(x + ref_level_db)
+// (:125-126), in float32 as numpy computes them on the float32 network output.
+__device__ __forceinline__ float denorm_db(float x, const MagArgs& a) {
     float d = x;
     if (a.signal_norm) {
         if (a.symmetric) {
@@ -333,8 +483,11 @@ __device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) {
             d = (d * -a.min_db / a.max_norm) + a.min_db;
         }
     }
-    return powf(10.f, (d + a.ref_db) * 0.05f);
+    return (d + a.ref_db) * 0.05f;
 }
+// the amplitude 10^e: powf (the mel path: 80 values per frame) or exp10f (the linear path: 1025)
+__device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) { return powf(10.f, denorm_db(x, a)); }
+__device__ __forceinline__ float amp_of_db(float x, const MagArgs& a) { return exp10f(denorm_db(x, a)); }
 
 // Tile = MAG_KT bins x MAG_FT frames per workgroup: the pinv columns of the tile's bins staged in
 // LDS once, the frames' amplitudes (float, as numpy has them) computed into LDS, then lane = bin,
@@ -350,10 +503,16 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     const int tid = threadIdx.x;
     const int k0 = blockIdx.x * MAG_KT;
     if (a.mode == TTS_GL_FROM_LINEAR) {
-        // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160)
+        // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160).
+        // The two float32 steps as numpy has them, each within an ulp or two of its powf: the
+        // amplitude 10^e by exp10f, and power 1.5 (the reference configs) as a * sqrt(a).  The
+        // two powf chains made this launch VALU-bound (788 us at configs[4], round 4).
         for (int i = tid; i < nf * MAG_KT; i += blockDim.x) {
             const int f = i / MAG_KT, k = k0 + i % MAG_KT;
-            if (k < NB) S[(int64_t)f * NB + k] = (spec_t)powf(denorm_to_amp(sp[(int64_t)f * NB + k], a), a.power);
+            if (k < NB) {
+                const float amp = amp_of_db(sp[(int64_t)f * NB + k], a);
+                S[(int64_t)f * NB + k] = (spec_t)(a.power == 1.5f ? amp * sqrtf(amp) : powf(amp, a.power));
+            }
         }
         return;
     }
@@ -461,36 +620,31 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
     const int tid = threadIdx.x;
     if (INIT && tid == 0 && a.zero_flags)  // the persistent loop that follows reads tags of frames < F[b] only
         a.zero_flags[(int64_t)b * a.Fmax + f] = 0u;
-    __shared__ __align__(16) double2 buf0[NH];
-    __shared__ __align__(16) double2 buf1[NH];
-    // the spectrum X[0, 1024) reuses buf0 (free once the forward FFT's last pass has read it; the
-    // inverse FFT writes it again only after every thread has read X), and the Nyquist bin
-    // X[1024] stays in a register of thread 0, the thread that writes and reads it: 32 KB of LDS
-    double2* const X = buf0;
+    __shared__ __align__(16) double2 buf0[NH];  // forward wave regions, then the spectrum X
+    __shared__ __align__(16) double2 buf1[NH];  // Z, then the inverse wave regions
+    // (the Nyquist bin X[1024] stays in a register of thread 0, its only writer and reader)
     double2 xnyq = double2{0.0, 0.0};
+    const TwTable twt{a.c.tw};
     const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     // ---- phase 0: the frame's global operands are issued before anything waits: window, |S|,
-    // split twiddles, the input samples (the FFT twiddles follow pass by pass, fft1024_regs_gtw)
-    constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;   // bins per thread (5)
-    constexpr int PN = NFFT / GL_THREADS;                    // samples per thread (8)
-    // |S| (streamed from HBM) is issued here; the split twiddles (an L2-resident table) are read
-    // where they are used: holding them across the forward FFT would cost a wave per SIMD
-    double sk[PK];
+    // the input samples (the FFT and split twiddles, an L2-resident table, are read where used:
+    // holding them across the forward FFT would cost a wave per SIMD)
+    constexpr int PN = NFFT / GL_THREADS;  // samples per thread (8)
+    // |S| of the thread's bins k = bin2l(r) (layout B), and of the Nyquist bin on thread 0
+    double sk[4];
 #pragma unroll
-    for (int i = 0; i < PK; ++i) {
-        const int k = tid + i * GL_THREADS;
-        sk[i] = k < NB ? (double)Sf[k] : 0.0;
-    }
-    // the padded Hann at this thread's samples: the analysis window of the STFT input (the first
-    // butterfly's register operands) and the synthesis window of the iSTFT output (the last
-    // butterfly's) sit at the same sample indices
+    for (int r = 0; r < 4; ++r) sk[r] = (double)Sf[bin2l(r)];
+    const double snyq = tid == 0 ? (double)Sf[NH] : 0.0;
+    // the padded Hann at this thread's samples: the analysis window of the STFT input (the
+    // forward FFT's layout-A registers) and the synthesis window of the iSTFT output (the inverse
+    // FFT's, layout A again) sit at the same sample indices
     double wo[PN];
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
         const int m = edge_sample(tid, i), n = m - g.woff;
         wo[i] = n >= 0 && n < g.win ? a.c.win[m] : 0.0;
     }
-
+    double2 v[4];
     if (!INIT) {
         // ---- STFT frame f of the previous iteration's float32 signal (librosa stft, centre reflect pad)
         const int N = g.hop * (Fb - 1);
@@ -498,7 +652,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
         float yi[PN];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
-            const int n = edge_sample(tid, i);  // the first butterfly's operands stay in registers
+            const int n = edge_sample(tid, i);  // the forward FFT's operands stay in registers
             const bool sup = n >= g.woff && n < g.woff + g.win;  // the padded Hann's support
             if (FUSED) {
                 const FT* fb = static_cast<const FT*>(a.prev) + (int64_t)b * a.Fmax * g.winp;
@@ -508,66 +662,31 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
                 yi[i] = sup ? yb[reflect_idx(f * g.hop + n - NFFT / 2, N)] : 0.f;
             }
         }
-        double2 v[4];  // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
+        // z[n] = x[2n] + i x[2n+1] == real x[0..2047]
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = double2{wo[2 * r] * (double)yi[2 * r], wo[2 * r + 1] * (double)yi[2 * r + 1]};
-        const double2* Z = fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw);
-        // real-FFT split; the STFT value is stored complex64 (librosa stft dtype) and its phase
-        // exp(i angle(X)) (angle(0) = 0) is applied to |S| in float64 (utils/audio.py:187-188)
-#pragma unroll
-        for (int i = 0; i < PK; ++i) {
-            const int k = tid + i * GL_THREADS;
-            if (k >= NB) break;
-            const double2 zk = Z[swz(k & (NH - 1))];
-            const double2 zc = cconj(Z[swz((NH - k) & (NH - 1))]);
-            const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
-            const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};  // -i (zk - zc) / 2
-            const double2 t = a.c.tw[k];
-            const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
-            const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
-            // unit phase X / |X| by one reciprocal square root (the float-rounded components
-            // square exactly in double): no divisions on the iteration's critical path
-            const double m2 = xre * xre + xim * xim;
-            const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
-            const double s = sk[i];
-            double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
-            if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
-            if (k == NH) xnyq = xv;
-            else X[k] = xv;
-        }
+        fft2l_fwd(v, buf0, twt);
+        spectrum2l(v, buf1, [&](int r) { return a.c.tw[bin2l(r)]; }, [&](int r) { return sk[r]; }, a.c.tw[NH], snyq,
+                   xnyq);
     } else {
-        // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183)
-#pragma unroll
-        for (int i = 0; i < PK; ++i) {
-            const int k = tid + i * GL_THREADS;
-            if (k >= NB) break;
+        // ---- initial phases exp(2 pi i U), U ~ U[0,1)  (utils/audio.py:183), per bin of layout B
+        auto init_bin = [&](int k, double sv) {
             const double u = a.phase_u ? a.phase_u[((int64_t)b * NB + k) * a.Fmax + f]
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
             sincos(2.0 * M_PI * u, &sn, &cs);
-            const double sv = sk[i];
-            const double2 xv = double2{sv * cs, (k == 0 || k == NB - 1) ? 0.0 : sv * sn};
-            if (k == NH) xnyq = xv;
-            else X[k] = xv;
-        }
-    }
-    __syncthreads();
-    // ---- inverse real FFT (istft: ifft of the Hermitian-extended spectrum, .real => Im X_0 = Im X_N/2 = 0,
-    // set where X is written); the first butterfly's operands z[tid + 256 i] stay in registers
-    double2 v[4];
+            return double2{sv * cs, (k == 0 || k == NB - 1) ? 0.0 : sv * sn};
+        };
 #pragma unroll
-    for (int i = 0; i < NH / GL_THREADS; ++i) {
-        const int k = tid + i * GL_THREADS;
-        const double2 xk = X[k];
-        const double2 xc = cconj(k == 0 ? xnyq : X[NH - k]);
-        const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
-        const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
-        const double2 O = cmul(D, cconj(a.c.tw[k]));
-        v[i] = double2{E.x - O.y, E.y + O.x};  // E + i O
+        for (int r = 0; r < 4; ++r) v[r] = init_bin(bin2l(r), sk[r]);
+        if (tid == 0) xnyq = init_bin(NH, snyq);
     }
-    fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
+    // ---- inverse real FFT (istft: ifft of the Hermitian-extended spectrum, .real => Im X_0 =
+    // Im X_N/2 = 0, set where X is formed)
+    presplit2l(v, buf0, [&](int r) { return a.c.tw[bin2l(r)]; }, xnyq);
+    fft2l_inv(v, buf1, twt);
     // ---- window and store the support [woff, woff+win) in float64 (ytmp of librosa istft), from
-    // the last butterfly's registers
+    // the inverse FFT's registers
     FT* out = static_cast<FT*>(a.next) + ((int64_t)b * a.Fmax + f) * g.winp;
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
@@ -1025,12 +1144,8 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     if ((int)blockIdx.x >= Fb) return;  // (a speculative batch-1 run sizes the grid as an upper bound)
     const Geo g = a.g;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // (TWO: X in buf0 -- the forward FFT ends in buf1, and the inverse FFT's first LDS writes go to
-    // buf1, its second pass to buf0 after a barrier that follows every read of X)
-    __shared__ __align__(16) double2 buf0[TWO ? NB + 1 : NH];
-    __shared__ __align__(16) double2 buf1[NH];
-    __shared__ __align__(16) double2 Xs[TWO ? 1 : NB + 1];
-    double2* const X = TWO ? buf0 : Xs;
+    __shared__ __align__(16) double2 buf0[NH];  // forward wave regions, then the spectrum X
+    __shared__ __align__(16) double2 buf1[NH];  // Z, then the inverse wave regions
     __shared__ int sh[4];  // frame, local stores, abort
     auto fail = [&](int code) {
         __hip_atomic_store((gi32_t*)p.status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1089,22 +1204,27 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     if (sh[2]) return;
     const int f = sh[0];
     const bool local = sh[1];
-    constexpr int PK = (NB + GL_THREADS - 1) / GL_THREADS;
     constexpr int PN = NFFT / GL_THREADS;
     // ---- iteration-invariant operands
     const spec_t* Sf = a.S + ((int64_t)b * a.Fmax + f) * NB;
     // the FFT twiddles in registers for the whole loop (one wave per SIMD: no occupancy to lose;
-    // the per-pass table reads of fft1024_regs_gtw cost 0.25 us of each forward FFT here)
-    FftTw ftw;
-    if (!TWO) ftw = load_fft_tw(a.c.tw);
-    double2 tk[PK];
-    spec_t sk[PK];  // (|S| in its float storage: widened where it is used)
+    // table reads where used cost latency on every pass here); TWO: read from the table
+    std::conditional_t<TWO, TwMix, TwRegs> twf;
+    twf.load(a.c.tw);  // (TWO: the table pointers are re-laundered every iteration: no hoisted pass reads)
+    __shared__ __align__(16) double2 tw_pass[TWO ? TW_LDS : 1];
+    if constexpr (TWO) TwMix::fill(tw_pass, a.c.tw);  // (ordered before its first use by the barriers below)
+    // split twiddles (TWO: read from the table where used) and |S| of the thread's bins
+    // k = bin2l(r) (layout B); thread 0 also holds the Nyquist bin's
+    double2 tk[4];
+    spec_t sk[4];  // (|S| in its float storage: widened where it is used)
 #pragma unroll
-    for (int i = 0; i < PK; ++i) {
-        const int k = tid + i * GL_THREADS;
-        tk[i] = k < NB ? a.c.tw[k] : double2{1.0, 0.0};
-        sk[i] = k < NB ? Sf[k] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+        tk[r] = a.c.tw[bin2l(r)];
+        sk[r] = Sf[bin2l(r)];
     }
+    auto tkf = [&](int r) { return tk[r]; };
+    const double2 tnyq = !TWO && tid == 0 ? a.c.tw[NH] : double2{0.0, 0.0};  // (TWO: from the table)
+    const spec_t snyq = tid == 0 ? Sf[NH] : 0.f;
     // STFT input sample i of this thread: n = edge_sample(tid, i); its overlap-add contributors and
     // window sum-square, as ola_sample.  A contributor is an index into the gather buffer og: slot
     // s = fi - f + GL_DMAX holds frame fi's granule values (every contributor lies within GL_DMAX
@@ -1120,8 +1240,11 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
     if (tid < 2) og[og_zero + tid] = 0.f;
     __syncthreads();
     double wi[PN];  // the window at this thread's samples: analysis (input) and synthesis (output) alike
-    int off[PN][OLA_MAX];
+    // contributor LDS indices, two 16-bit halves per register (og_zero < 65536: checked below)
+    constexpr int OP = (OLA_MAX + 1) / 2;
+    unsigned offp[PN][OP];
     float wssv[PN];
+    if (og_zero > 0xFFFF) fail(6);
 #pragma unroll
     for (int i = 0; i < PN; ++i) {
         const int n = edge_sample(tid, i);
@@ -1135,6 +1258,8 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
         const bool any = sup && q >= g.woff;
         float wss = 0.f;
 #pragma unroll
+        for (int k = 0; k < OP; ++k) offp[i][k] = 0u;
+#pragma unroll
         for (int k = 0; k < OLA_MAX; ++k) {
             const int fi = ilo + k;
             const int o = q - fi * g.hop;
@@ -1142,7 +1267,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             const int sl = fi - f + GL_DMAX, gg = o - g.fb;
             if (ok && (sl < 0 || sl >= GL_SLOTS)) fail(4);  // (never: contributors are within GL_DMAX)
             const bool in = ok && sl >= 0 && sl < GL_SLOTS;
-            off[i][k] = in ? sl * g.winp + gg : og_zero;
+            offp[i][k >> 1] |= (unsigned)(in ? sl * g.winp + gg : og_zero) << (16 * (k & 1));
             if (in) {
                 atomicMin(&rlo[sl], gg);
                 atomicMax(&rhi[sl], gg);
@@ -1168,29 +1293,37 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
         if (acc > GL_PAIRS * GL_THREADS) fail(5);
     }
     __syncthreads();
-    int goff[GL_PAIRS];
+    // (a listed pair needs at least one of its granules; its source offset is the LDS index
+    // rebased to frame f - GL_DMAX: slot sl of the gather buffer mirrors frame f + sl - GL_DMAX)
     unsigned gdst[GL_PAIRS];
 #pragma unroll
     for (int m = 0; m < GL_PAIRS; ++m) {
         const int u = tid + m * GL_THREADS;
-        goff[m] = GL_OOB_OFF;
         gdst[m] = (unsigned)og_zero;
         if (u < rpre[GL_SLOTS]) {
             int sl = 0;
             while (u >= rpre[sl + 1]) ++sl;
             const int g0 = (rlo[sl] & ~1) + 2 * (u - rpre[sl]);
-            goff[m] = ((f + sl - GL_DMAX) * g.winp + g0) * 8;
             gdst[m] = (unsigned)(sl * g.winp + g0) | (g0 >= rlo[sl] ? 1u << 30 : 0u) | (g0 + 1 <= rhi[sl] ? 1u << 31 : 0u);
         }
     }
-    // byte offset of output sample i's granule in the frame slot; samples outside the window
-    // support take an out-of-range offset (the buffer store drops them)
-    int soff[PN];
+    const int gbase = (f - GL_DMAX) * g.winp * 8;
+    auto goff = [&](int m) {
+        return (gdst[m] >> 30) ? gbase + (int)(gdst[m] & 0x3FFFFFFFu) * 8 : GL_OOB_OFF;
+    };
+    // byte offset of output sample i's granule in the frame slot (computed where stored); samples
+    // outside the window support take an out-of-range offset (the buffer store drops them)
+    // (TWO: computed where stored, from an opaque thread index: held, they would not fit)
+    auto soff_of = [&](int t, int i) {
+        const int e = edge_sample(t, i);
+        return (unsigned)(e - g.woff) < (unsigned)g.win ? (e - g.fb) * 8 : GL_OOB_OFF;
+    };
+    int soffv[TWO ? 1 : PN];
+    if constexpr (!TWO) {
 #pragma unroll
-    for (int i = 0; i < PN; ++i) {
-        const int n = edge_sample(tid, i) - g.woff;
-        soff[i] = n >= 0 && n < g.win ? (n + g.woff - g.fb) * 8 : GL_OOB_OFF;
+        for (int i = 0; i < PN; ++i) soffv[i] = soff_of(tid, i);
     }
+    auto soff = [&](int i) { if constexpr (TWO) return soff_of(tid_opaque(), i); else return soffv[i]; };
     const bool timed = p.prof && f == p.prof_f && b == 0 && tid == 0;
     long long ph[6] = {0, 0, 0, 0, 0, 0};
     long long tp = timed ? (long long)wall_clock64() : 0;
@@ -1205,6 +1338,12 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
         const gran_t* src = p.frames + (it & 1) * p.fstride + (int64_t)b * a.Fmax * g.winp;
         gran_t* dst = p.frames + ((it + 1) & 1) * p.fstride + ((int64_t)b * a.Fmax + f) * g.winp;
         const unsigned want = tag0 | (unsigned)it;
+        if constexpr (TWO) {  // an opaque copy of the table pointer per iteration: loop-invariant table
+            int z = 0;  // an opaque zero offset (the pointers keep their address spaces): table
+            asm volatile("" : "+v"(z));  // reads hoisted out of the loop would not fit the registers
+            twf.tw = (g_d*)a.c.tw + z;
+            twf.pt = (l_d*)tw_pass + z;
+        }
         // ---- gather: the workgroup's granule pairs (each thread <= GL_PAIRS 16-byte sc1 loads, all in
         // flight at once), re-read until every needed tag is this iteration's, then into LDS
         {
@@ -1214,7 +1353,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             for (int spin = 0;; ++spin) {
 #pragma unroll
                 for (int m = 0; m < GL_PAIRS; ++m)
-                    x[m] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rG, goff[m], 0, GL_SC1_VOLATILE));
+                    x[m] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rG, goff(m), 0, GL_SC1_VOLATILE));
                 bool ok = true;
 #pragma unroll
                 for (int m = 0; m < GL_PAIRS; ++m)
@@ -1239,7 +1378,7 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
         if (sh[2]) return;
         GL_PHASE(0)
         // ---- overlap-add sums (librosa istft: float64 contributions into a float32 signal, frame
-        // order) straight into the first butterfly's registers
+        // order) straight into the forward FFT's layout-A registers
         double2 v[4];
 #pragma unroll
         for (int i = 0; i < PN; ++i) {
@@ -1247,49 +1386,19 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             // which is never -0.0)
             float y = 0.f;
 #pragma unroll
-            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (double)og[off[i][k]]);
+            for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (double)og[(offp[i][k >> 1] >> (16 * (k & 1))) & 0xFFFFu]);
             const float yv = y / wssv[i];
             if (i & 1) v[i >> 1].y = wi[i] * (double)yv;
             else v[i >> 1].x = wi[i] * (double)yv;
         }
         GL_PHASE(1)
-        const double2* Z = TWO ? fft1024_regs_gtw<false, false>(v, buf0, buf1, a.c.tw)
-                               : fft1024_regs<false, false>(v, buf0, buf1, ftw);
+        fft2l_fwd(v, buf0, twf);
         GL_PHASE(2)
-#pragma unroll
-        for (int i = 0; i < PK; ++i) {
-            const int k = tid + i * GL_THREADS;
-            if (k >= NB) break;
-            const double2 zk = Z[swz(k & (NH - 1))];
-            const double2 zc = cconj(Z[swz((NH - k) & (NH - 1))]);
-            const double2 E = double2{0.5 * (zk.x + zc.x), 0.5 * (zk.y + zc.y)};
-            const double2 O = double2{0.5 * (zk.y - zc.y), -0.5 * (zk.x - zc.x)};
-            const double2 t = tk[i];
-            const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
-            const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
-            // unit phase X / |X| by one reciprocal square root (the float-rounded components
-            // square exactly in double): no divisions on the iteration's critical path
-            const double m2 = xre * xre + xim * xim;
-            const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
-            const double s = (double)sk[i];
-            double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
-            if (k == 0 || k == NB - 1) xv.y = 0.0;  // istft: .real of the Hermitian extension
-            X[k] = xv;
-        }
-        __syncthreads();
+        double2 xnyq = double2{0.0, 0.0};
+        spectrum2l(v, buf1, tkf, [&](int r) { return (double)sk[r]; }, TWO ? twf.tw_at(NH) : tnyq, (double)snyq, xnyq);
+        presplit2l(v, buf0, tkf, xnyq);
         GL_PHASE(3)
-#pragma unroll
-        for (int i = 0; i < NH / GL_THREADS; ++i) {
-            const int k = tid + i * GL_THREADS;
-            const double2 xk = X[k];
-            const double2 xc = cconj(X[NH - k]);
-            const double2 E = double2{0.5 * (xk.x + xc.x), 0.5 * (xk.y + xc.y)};
-            const double2 D = double2{0.5 * (xk.x - xc.x), 0.5 * (xk.y - xc.y)};
-            const double2 O = cmul(D, cconj(tk[i]));
-            v[i] = double2{E.x - O.y, E.y + O.x};
-        }
-        if (TWO) fft1024_regs_gtw<true, true>(v, buf0, buf1, a.c.tw);
-        else fft1024_regs<true, true>(v, buf0, buf1, ftw);
+        fft2l_inv(v, buf1, twf);
         GL_PHASE(4)
         if (b == 0 && f == p.drop_f) return;  // fault injection only: never stores iteration 1
         // ---- the frame's samples, tagged with the next iteration: XCD-local (workgroup-scope store,
@@ -1301,8 +1410,8 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
             const u32x2 gv = u32x2{__float_as_uint((float)(wi[i] * (zv * (1.0 / NH)))), nt};
             // plain (workgroup-scope) store: the line stays in this XCD's L2; sc1: written through
-            if (local) __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0);
-            else __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff[i], 0, 0x10);
+            if (local) __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff(i), 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff(i), 0, 0x10);
         }
         GL_PHASE(5)
     }
