@@ -341,7 +341,10 @@ __device__ __forceinline__ double2 spec_bin(double2 zk, double2 zm, double2 t, d
     const double xre = (double)(float)(E.x + (t.x * O.x - t.y * O.y));
     const double xim = (double)(float)(E.y + (t.x * O.y + t.y * O.x));
     const double m2 = xre * xre + xim * xim;
-    const double ri = m2 > 0.0 ? rsqrt(m2) : 0.0;
+    // the hardware reciprocal square root (~2^-23) and one Newton step (~2^-45): the reference's
+    // unit phase is itself complex64 (np.exp(1j * np.angle(X)) on a complex64 X)
+    double ri = __builtin_amdgcn_rsq(m2);
+    ri = fma(0.5 * ri, fma(-m2 * ri, ri, 1.0), ri);
     double2 xv = m2 > 0.0 ? double2{s * (xre * ri), s * (xim * ri)} : double2{s, 0.0};
     if (edge) xv.y = 0.0;
     return xv;
