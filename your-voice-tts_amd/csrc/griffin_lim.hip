@@ -492,6 +492,33 @@ __device__ __forceinline__ float denorm_db(float x, const MagArgs& a) {
 __device__ __forceinline__ float denorm_to_amp(float x, const MagArgs& a) { return powf(10.f, denorm_db(x, a)); }
 __device__ __forceinline__ float amp_of_db(float x, const MagArgs& a) { return exp10f(denorm_db(x, a)); }
 
+// inv_spectrogram's |S|: S (float32) ** power in float32, then widened (utils/audio.py:156-160).
+// The two float32 steps as numpy has them, each within an ulp or two of its powf: the amplitude
+// 10^e by exp10f, and power 1.5 (the reference configs) as a * sqrt(a).  A streaming launch with
+// no LDS, LIN_PER elements per thread (round 4's tile launch with two powf per bin: 788 us at
+// configs[4], dispatch- and VALU-bound).
+constexpr int LIN_PER = 16;
+__global__ __launch_bounds__(256) void gl_linear_magnitude_kernel(const MagArgs a) {
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)a.F[b] * NB;  // the sentence's frames < F[b], each a 1025-bin row
+    const int64_t base = (int64_t)blockIdx.x * (256 * LIN_PER) + threadIdx.x;
+    if (base >= n) return;
+    const float* sp = a.spec + (int64_t)b * a.Fmax * NB;
+    spec_t* S = a.S + (int64_t)b * a.Fmax * NB;
+    float x[LIN_PER];
+#pragma unroll
+    for (int i = 0; i < LIN_PER; ++i) {
+        const int64_t e = base + i * 256;
+        x[i] = e < n ? sp[e] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < LIN_PER; ++i) {
+        const int64_t e = base + i * 256;
+        const float amp = amp_of_db(x[i], a);
+        if (e < n) S[e] = (spec_t)(a.power == 1.5f ? amp * sqrtf(amp) : powf(amp, a.power));
+    }
+}
+
 // Tile = MAG_KT bins x MAG_FT frames per workgroup: the pinv columns of the tile's bins staged in
 // LDS once, the frames' amplitudes (float, as numpy has them) computed into LDS, then lane = bin,
 // each wave MAG_FT / 4 frames, every (bin, frame) dot product summed over mels in order.
@@ -505,20 +532,6 @@ __global__ __launch_bounds__(256) void gl_magnitude_kernel(const MagArgs a) {
     spec_t* S = a.S + ((int64_t)b * a.Fmax + f0) * NB;
     const int tid = threadIdx.x;
     const int k0 = blockIdx.x * MAG_KT;
-    if (a.mode == TTS_GL_FROM_LINEAR) {
-        // inv_spectrogram: S (float32) ** power in float32, then widened (utils/audio.py:156-160).
-        // The two float32 steps as numpy has them, each within an ulp or two of its powf: the
-        // amplitude 10^e by exp10f, and power 1.5 (the reference configs) as a * sqrt(a).  The
-        // two powf chains made this launch VALU-bound (788 us at configs[4], round 4).
-        for (int i = tid; i < nf * MAG_KT; i += blockDim.x) {
-            const int f = i / MAG_KT, k = k0 + i % MAG_KT;
-            if (k < NB) {
-                const float amp = amp_of_db(sp[(int64_t)f * NB + k], a);
-                S[(int64_t)f * NB + k] = (spec_t)(a.power == 1.5f ? amp * sqrtf(amp) : powf(amp, a.power));
-            }
-        }
-        return;
-    }
     __shared__ double pw[80][MAG_KT];
     __shared__ float amp[MAG_FT][80];
     // fixed trip counts (n_in <= 80): every staging load of the tile is in flight at once
@@ -677,7 +690,7 @@ __global__ __launch_bounds__(GL_THREADS, 4) void gl_iter_kernel(const IterArgs a
             const double u = a.phase_u ? a.phase_u[((int64_t)b * NB + k) * a.Fmax + f]
                                        : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
             double sn, cs;
-            sincos(2.0 * M_PI * u, &sn, &cs);
+            sincospi(2.0 * u, &sn, &cs);  // (exp(2 pi i u) without rounding 2 pi u first)
             return double2{sv * cs, (k == 0 || k == NB - 1) ? 0.0 : sv * sn};
         };
 #pragma unroll
@@ -872,7 +885,8 @@ __device__ __forceinline__ double2 unit_phase(double2 X, double s) {
     const double m2 = fma(xre, xre, xim * xim);
     double r = __builtin_amdgcn_rsq(m2);
     r = fma(0.5 * r, fma(-m2 * r, r, 1.0), r);
-    return m2 > 0.0 ? double2{s * (xre * r), s * (xim * r)} : double2{s, 0.0};
+    const double sr = s * r;  // (|S| folded into the reciprocal: one product per component)
+    return m2 > 0.0 ? double2{xre * sr, xim * sr} : double2{s, 0.0};
 }
 // inverse real-FFT pre-split, times 2: z'[k] = E + i O, 2E = X[k] + conj X[N-k],
 // 2O = (X[k] - conj X[N-k]) * conj(t) (the factor 1/2 is folded into the output scale)
@@ -1032,8 +1046,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             xk.y = 0.0;
             xm.y = 0.0;
         }
-        v[m] = inv_presplit2(xk, xm, tk);
-        const double2 vm = inv_presplit2(xm, xk, double2{-tk.x, tk.y});
+        // the pair's two pre-splits share E, D and O: the partner's (conj t' = -t of bin 1024 - k)
+        // is (E.x + O.y, O.x - E.y), E = X[k] + conj X[N-k], O = (X[k] - conj X[N-k]) conj(t)
+        const double2 Ep = double2{xk.x + xm.x, xk.y - xm.y};
+        const double2 Op = cmulcf(double2{xk.x - xm.x, xk.y + xm.y}, tk);
+        v[m] = double2{Ep.x - Op.y, Ep.y + Op.x};
+        const double2 vm = double2{Ep.x + Op.y, Op.x - Ep.y};
         lds[mb + 64 * (15 - m)] = vm.x;
         vmy[m] = vm.y;
         zki = zki_n;
@@ -2061,8 +2079,13 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     ma.signal_norm = g->cfg.signal_norm;
     ma.symmetric = g->cfg.symmetric_norm;
     ma.clip = g->cfg.clip_norm;
-    hipLaunchKernelGGL(gl_magnitude_kernel, dim3((NB + MAG_KT - 1) / MAG_KT, (Fmax + MAG_FT - 1) / MAG_FT, B), dim3(256),
-                       0, s, ma);
+    if (mode == TTS_GL_FROM_LINEAR)
+        hipLaunchKernelGGL(gl_linear_magnitude_kernel,
+                           dim3((unsigned)(((int64_t)Fmax * NB + 256 * LIN_PER - 1) / (256 * LIN_PER)), B), dim3(256), 0, s,
+                           ma);
+    else
+        hipLaunchKernelGGL(gl_magnitude_kernel, dim3((NB + MAG_KT - 1) / MAG_KT, (Fmax + MAG_FT - 1) / MAG_FT, B),
+                           dim3(256), 0, s, ma);
     TTS_HIP(hipGetLastError());
     const size_t fstride = (size_t)B * Fmax * geo.winp;
     // the persistent loop reads and writes two slots of tagged granules (gl_persistent_kernel);
