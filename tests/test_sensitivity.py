@@ -37,11 +37,13 @@ def test_reference_sensitivity_fixture_reproduces():
 @pytest.mark.gpu
 def test_gpu_chain_vs_float64_chain(audio_cfg):
     """The GPU's mel_post and waveform for the T=342 sentence (batch-1 resident path and inside
-    configs[3]'s 64-sentence share, device phases seed 40 at the sentence's batch row), against the
-    float64 chain.  Measured on MI355X: mel_post 3.3e-7 (batch 64) / 1.6e-7 (batch 1) and waveform
-    4.1e-5 / 3.7e-5, against the float32 oracle's 3.3e-7 / 5.0e-5: the GPU chain is as close to the
-    exact one as the reference's own precision allows.  Bounds: 2x (mel_post) and 1.25x (waveform)
-    those float32 floors."""
+    configs[3]'s 64-sentence share) against the float64 chain, read against the float32 oracle's
+    own distance to it.  mel_post: one comparison (MI355X: 3.3e-7 batch 64, 2.7e-7 batch 1, against
+    the float32 oracle's 3.3e-7; bound 2x).  Waveform: Griffin-Lim amplifies a ~3e-7 mel difference
+    chaotically, so one phase draw is one realization (round 5: 2.5e-5 to 6.4e-5 on single draws
+    of the same-size mel error, against the oracle's 5.0e-5); the test averages four draws of the
+    device phases (seeds 40..43, the sentence's batch row) for the GPU chain and for the float32
+    oracle alike (GL on the fixture's float32 mel_post), bound 1.25x that mean."""
     z = golden("sens_t342")
     fl = golden_flags(golden("t2_fwdmask_L100"))
     gu = load_pkg("generic_utils")
@@ -59,19 +61,22 @@ def test_gpu_chain_vs_float64_chain(audio_cfg):
     np.testing.assert_array_equal(share[b], z["ids"])
     T = 342
     ao = AudioOracle(**audio_cfg)
-    w64 = ao.inv_mel_spectrogram(z["mel_post64"].T, device_phase_u(int(z["phase_seed"]), b, T))
+    seeds = (40, 41, 42, 43)
+    pus = [device_phase_u(s, b, T) for s in seeds]
+    w64 = [ao.inv_mel_spectrogram(z["mel_post64"].T, pu) for pu in pus]
     floor_mel = float(z["mel_rel_32_64"])
-    floor_wav = float(z["wav_rel_32_64"])
+    floor_wav = float(np.mean([rel_rms(ao.inv_mel_spectrogram(z["mel_post32"].T, pu), r) for pu, r in zip(pus, w64)]))
     report = {}
     for name, batch, row in (("batch64", share, b), ("batch1", [z["ids"]], 0)):
         out = m.inference_batch(batch)
         assert out["frames"][row] == T
         mp = out["mel_post"][row, :T].cpu().numpy()
         np.testing.assert_array_equal(out["align"][row, :T, :len(z["ids"])].cpu().numpy().argmax(1), z["align_argmax64"])
-        # Griffin-Lim on the GPU's own mel_post with the phases of row b of a seed-40 batch
-        pu = torch.from_numpy(device_phase_u(int(z["phase_seed"]), b, T)[None])
-        wav = ap.griffin_lim_batch(out["mel_post"][row:row + 1, :T], [T], phase_u=pu).cpu().numpy()[0]
-        report[name] = dict(mel=rel_rms(mp, z["mel_post64"]), wav=rel_rms(wav, w64))
+        errs = []
+        for pu, r in zip(pus, w64):
+            wav = ap.griffin_lim_batch(out["mel_post"][row:row + 1, :T], [T], phase_u=torch.from_numpy(pu[None]))
+            errs.append(rel_rms(wav.cpu().numpy()[0], r))
+        report[name] = dict(mel=rel_rms(mp, z["mel_post64"]), wav=float(np.mean(errs)), wav_draws=errs)
     print("sensitivity", report, "floors", floor_mel, floor_wav)
     for name, r in report.items():
         assert r["mel"] < 2 * floor_mel, (name, r)

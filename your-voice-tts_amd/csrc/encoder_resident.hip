@@ -148,7 +148,7 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         acc += dpp_move<0xB1, 0xf>(acc, 0.f);  // quad_perm [1,0,3,2]
         acc += dpp_move<0x4E, 0xf>(acc, 0.f);  // quad_perm [2,3,0,1]
         const float pre = acc + xcur;
-        const float act = gate == 2 ? tanhf(pre) : sigmoidf_(pre);
+        const float act = gate == 2 ? tanh_cell(pre) : sigmoid_cell(pre);
         const float f = dpp_move<0x104, 0xf>(act, 0.f);  // row_shl:4  -> gate 1 of this unit
         const float g = dpp_move<0x108, 0xf>(act, 0.f);  // row_shl:8  -> gate 2
         const float o = dpp_move<0x10C, 0xf>(act, 0.f);  // row_shl:12 -> gate 3
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         u64* gh = a.gran + GR_H + (par * 2 + dir) * H;
         if ((tid & 15) == 0) {
             cs = f * cs + act * g;  // c' = s(f) c + s(i) tanh(g)
-            const float h = o * tanhf(cs);
+            const float h = o * tanh_cell(cs);
             hlast = h;
             pub_xcd(gh + unit, (a.salt << 14) | (unsigned)(s + 1), h);
             const int pos = dir == 0 ? s : L - 1 - s;
@@ -286,8 +286,8 @@ __global__ __launch_bounds__(EB_THREADS, 1) void encoder_resident_batch_kernel(c
             const float gi = sum[0] + xg[0], gf = sum[1] + xg[1], gg = sum[2] + xg[2], go = sum[3] + xg[3];
             load_xi(s + 1);  // next step's input projection, in flight during the hand-off
             if (act) {
-                const float c2 = sigmoidf_(gf) * cs + sigmoidf_(gi) * tanhf(gg);
-                const float h = sigmoidf_(go) * tanhf(c2);
+                const float c2 = sigmoid_cell(gf) * cs + sigmoid_cell(gi) * tanh_cell(gg);
+                const float h = sigmoid_cell(go) * tanh_cell(c2);
                 cs = c2;
                 hprev = h;
                 const int pos = dir ? Ln - 1 - s : s;

@@ -121,19 +121,20 @@ __device__ __forceinline__ bool sweep_pair(__amdgpu_buffer_rsrc_t r, int slot, b
 
 // LSTM cell of units 4c..4c+3 from the 16 gate sums (row g*4 + u, torch order i, f, g, o): lanes
 // 0..15 evaluate one gate nonlinearity each in parallel; lanes 0..3 pull f, g, o from lanes u+4,
-// u+8, u+12 by DPP row shifts and update (c, h) exactly as the sgemm LSTM epilogue does.
+// u+8, u+12 by DPP row shifts and update (c, h) as the sgemm LSTM epilogue does (its nonlinearities
+// by the hardware-exp2 forms sigmoid_cell / tanh_cell, common.h).
 // Call with lanes 0..15 of wave 0 active; returns h in lanes 0..3 and updates c there.
 __device__ __forceinline__ float lstm_cell16(float pre, float& c) {
     const int k = threadIdx.x;
-    const float act = (k >> 2) == 2 ? tanhf(pre) : sigmoidf_(pre);
+    const float act = (k >> 2) == 2 ? tanh_cell(pre) : sigmoid_cell(pre);
     const float f = dpp_move<0x104, 0xf>(act, 0.f);   // row_shl:4
     const float g = dpp_move<0x108, 0xf>(act, 0.f);   // row_shl:8
     const float o = dpp_move<0x10C, 0xf>(act, 0.f);   // row_shl:12
     const float c2 = f * c + act * g;
     c = c2;
-    return o * tanhf(c2);
+    return o * tanh_cell(c2);
 }
-// sigmoid from the hardware exp2 / reciprocal (attention energies only; ~1e-7 relative)
+// sigmoid from the hardware exp2 / reciprocal for the attention energies (sigmoid_cell's form)
 __device__ __forceinline__ float sigmoid_fast(float x) {
     return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-x * 1.4426950408889634f));
 }

@@ -458,9 +458,9 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             const float R = __shfl(tot, 4 * (lane & 3), 64), Z = __shfl(tot, 4 * (4 + (lane & 3)), 64),
                         N = __shfl(tot, 4 * (8 + (lane & 3)), 64), Q = __shfl(tot, 4 * (12 + (lane & 3)), 64);
             if (lane < ns) {
-                const float rg = sigmoidf_(R + bias[0]);
-                const float zg = sigmoidf_(Z + bias[1]);
-                const float ng = tanhf((N + bias[2]) + rg * (Q + bias[3]));
+                const float rg = sigmoid_cell(R + bias[0]);
+                const float zg = sigmoid_cell(Z + bias[1]);
+                const float ng = tanh_cell((N + bias[2]) + rg * (Q + bias[3]));
                 publish(G + G_HATT + lane * TD + U, E + P_HATT, (hatt_prev[lane * TD + U] - ng) * zg + ng);
             }
         }
@@ -658,9 +658,9 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                 const float R = __shfl(tot, 4 * (lane & 3), 64), Z = __shfl(tot, 4 * (4 + (lane & 3)), 64),
                             N = __shfl(tot, 4 * (8 + (lane & 3)), 64), Q = __shfl(tot, 4 * (12 + (lane & 3)), 64);
                 if (lane < ns) {
-                    const float rg = sigmoidf_(R + bias[4 + 4 * g]);
-                    const float zg = sigmoidf_(Z + bias[5 + 4 * g]);
-                    const float ng = tanhf((N + bias[6 + 4 * g]) + rg * (Q + bias[7 + 4 * g]));
+                    const float rg = sigmoid_cell(R + bias[4 + 4 * g]);
+                    const float zg = sigmoid_cell(Z + bias[5 + 4 * g]);
+                    const float ng = tanh_cell((N + bias[6 + 4 * g]) + rg * (Q + bias[7 + 4 * g]));
                     const float hn = (Hp[lane * TD + U] - ng) * zg + ng;
                     publish(gg + lane * TD + U, tg, hn);
                     publish(gg + TR_SPX * TD + lane * TD + U, tg, hn + X[lane * TD + U]);

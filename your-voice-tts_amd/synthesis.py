@@ -110,9 +110,7 @@ def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed
     linear = hasattr(model, "linear_dim")  # Tacotron / TacotronGST: linear-spectrogram GL
     if linear:
         out = model.inference_batch(ids_list, speaker_ids=speaker_ids, style_mel=style_mel)
-    elif keep_outputs:
-        out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
-    else:
+    else:  # (keep_outputs or not: the same dispatch, so a sharded rank decodes as the single process does)
         out = _decode(model, ids_list, speaker_ids)
     frames = out["frames"]
     mel_post = out["linear"] if linear else out["mel_post"]
