@@ -45,7 +45,11 @@ LABELS = [
     (r"preemph_scan_kernel", "preemph"),
     (r"gl_ola_kernel", "gl_ola"),
     (r"project_inputs_kernel", "project_inputs"),
+    (r"resident_decoder_kernel<(?:false|true), true>", "resident_decoder_general"),
     (r"resident_decoder_kernel", "resident_decoder"),
+    (r"gl_linear_magnitude_kernel", "gl_linear_magnitude"),
+    (r"gl_persistent2_kernel", "gl_persistent2"),
+    (r"encoder_resident_batch_kernel", "enc_lstm_resident_batch"),
 ]
 
 
