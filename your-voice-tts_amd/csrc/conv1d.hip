@@ -466,7 +466,13 @@ __global__ __launch_bounds__(256) void conv_vl_kernel(const ConvArgs a, int nb) 
 // the packed [Cin][KW][co_pad] layout into registers, CS_PR k-step pairs ahead, and no barrier until
 // the waves' partial tiles are summed (fixed order) for the epilogue.
 constexpr int CS_BM = 16, CS_BN = 32, CS_PR = 8, CS_WAVES = 8, CS_THREADS = 64 * CS_WAVES;
-template <int KW>
+// TAP (Cin = 512, weights from conv_pack_frag_tap): wave w takes input channels [64 w, 64 w + 64)
+// for every tap instead of a slice of the channel-major K, so a tap's 16 k-steps are one round
+// whose A operands sit at compile-time offsets from one LDS address and whose weights are 8
+// consecutive fragment pairs: no per-k-step index arithmetic (round 5: it was the loop's limiter,
+// ~9 VALU per A operand beside the MFMAs).
+constexpr int CS_TAP_CIN = 8 * CS_WAVES * CS_PR;  // 512
+template <int KW, bool TAP>
 __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a) {
     constexpr int PAD = (KW - 1) / 2;
     constexpr int XR = CS_BM + KW - 1;
@@ -490,8 +496,14 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     const int p_beg = wave * np / CS_WAVES, p_end = (wave + 1) * np / CS_WAVES;
     const float4* Wf = reinterpret_cast<const float4*>(a.Wf) + (int64_t)ct * np * 64 + lane;
     float4 wr[CS_PR];
+    const int pw = wave * (CS_TAP_CIN / CS_WAVES) / 8;  // (TAP: this wave's first pair of tap 0)
+    if constexpr (!TAP) {
 #pragma unroll
-    for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)min(p_beg + i, p_end - 1) * 64];
+        for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)min(p_beg + i, p_end - 1) * 64];
+    } else {
+#pragma unroll
+        for (int i = 0; i < CS_PR; ++i) wr[i] = Wf[(int64_t)(pw + i) * 64];
+    }
     {
         // every load of the stage is issued before the first LDS store (one memory round trip, beside the
         // first weight loads)
@@ -520,6 +532,28 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     __syncthreads();
     // lane supplies A[row][q] = x[t0 + row + tap - PAD][ci] and B[q][n] = W[k][c0 + 16 j + n] for
     // k = 4 s + q = ci * KW + tap
+    floatx4 acc0 = floatx4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    if constexpr (TAP) {
+        // pairs of tap t for this wave: (t Cin + 64 w) / 8 + [0, CS_PR) (tap 0's issued before the staging)
+        const float* xrow = xs + row * ldx + wave * (CS_TAP_CIN / CS_WAVES) + q;
+        // (fully unrolled: a loop header would drain the weight ring's loads every tap)
+#pragma unroll
+        for (int tap = 0; tap < KW; ++tap) {
+            float xa[2 * CS_PR];
+#pragma unroll
+            for (int i = 0; i < 2 * CS_PR; ++i) xa[i] = xrow[tap * ldx + 4 * i];
+            const int pn = (tap + 1) * (CS_TAP_CIN / 8) + pw;
+#pragma unroll
+            for (int i = 0; i < CS_PR; ++i) {
+                acc0 = mfma16x16x4(xa[2 * i], wr[i].x, acc0);
+                acc1 = mfma16x16x4(xa[2 * i], wr[i].y, acc1);
+                acc0 = mfma16x16x4(xa[2 * i + 1], wr[i].z, acc0);
+                acc1 = mfma16x16x4(xa[2 * i + 1], wr[i].w, acc1);
+                if (tap + 1 < KW) wr[i] = Wf[(int64_t)(pn + i) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    } else {
     int k0 = 8 * p_beg + q;
     int ci = k0 / KW, tap = k0 - ci * KW;
     auto next4 = [&]() {  // k += 4
@@ -535,7 +569,6 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
             }
         }
     };
-    floatx4 acc0 = floatx4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
     auto round = [&](int pc) {
         // the round's A operands first (every LDS read in flight together), then per pair its MFMAs
         // and the reload of its ring slot, in that order (sched_barrier)
@@ -563,6 +596,7 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     for (int pc = p_beg; pc < p_end; pc += 2 * CS_PR) {
         round(pc);
         if (pc + CS_PR < p_end) round(pc + CS_PR);
+    }
     }
     __syncthreads();  // every wave is done with the input rows: reuse them for the partial tiles
     float* red = xs;  // [wave][j][lane][r]
@@ -600,7 +634,12 @@ bool launch_small(const ConvArgs& a, int B, int frames_hint, hipStream_t s, hipE
     const int Tt = a.Ttile ? a.Ttile : a.Tmax;
     const size_t smem = sizeof(float) * std::max((size_t)(CS_BM + KW - 1) * (a.Cin + 1), (size_t)2 * 256 * CS_WAVES);
     const dim3 grid(((Tt + CS_BM - 1) / CS_BM) * (a.co_pad / CS_BN) * B);
-    hipLaunchKernelGGL(conv_small_kernel<KW>, grid, dim3(CS_THREADS), smem, s, a);
+    if (a.wf_tap && a.Cin == CS_TAP_CIN)
+        hipLaunchKernelGGL((conv_small_kernel<KW, true>), grid, dim3(CS_THREADS), smem, s, a);
+    else if (a.wf_tap)
+        return false;  // (tap-major weights for another Cin: never packed so, conv_pack_frag_tap refuses)
+    else
+        hipLaunchKernelGGL((conv_small_kernel<KW, false>), grid, dim3(CS_THREADS), smem, s, a);
     *err = hipGetLastError();
     return true;
 }
@@ -627,6 +666,22 @@ __global__ void conv_pack_frag_kernel(const float* W, int K, int co_pad, float* 
     const int q = lane >> 4, r = lane & 15;
     const int k = 8 * p + 4 * (e >> 1) + q, co = 32 * ct + 16 * (e & 1) + r;
     out[i] = W[(int64_t)k * co_pad + co];
+}
+
+// packed [Cin * KW][co_pad] (k = ci KW + tap) -> the tap-major fragment order of conv_small_kernel's
+// TAP form: k' = tap Cin + ci, then as conv_pack_frag over k'
+__global__ void conv_pack_frag_tap_kernel(const float* W, int Cin, int KW, int co_pad, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int K = Cin * KW;
+    if (i >= (int64_t)K * co_pad) return;
+    const int e = i & 3, lane = (i >> 2) & 63;
+    const int64_t rest = i >> 8;
+    const int np = K >> 3;
+    const int p = rest % np, ct = rest / np;
+    const int q = lane >> 4, r = lane & 15;
+    const int kt = 8 * p + 4 * (e >> 1) + q, co = 32 * ct + 16 * (e & 1) + r;
+    const int tap = kt / Cin, ci = kt - tap * Cin;
+    out[i] = W[(int64_t)(ci * KW + tap) * co_pad + co];
 }
 
 __global__ void conv_pack_bank_kernel(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad,
@@ -755,6 +810,15 @@ hipError_t conv_pack_frag(const float* W, int K, int co_pad, float* out, hipStre
     hipLaunchKernelGGL(conv_pack_frag_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, K, co_pad, out);
     return hipGetLastError();
 }
+
+hipError_t conv_pack_frag_tap(const float* W, int Cin, int KW, int co_pad, float* out, hipStream_t s) {
+    if (Cin != CS_TAP_CIN || (co_pad % CS_BN)) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)Cin * KW * co_pad;
+    hipLaunchKernelGGL(conv_pack_frag_tap_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, Cin, KW, co_pad,
+                       out);
+    return hipGetLastError();
+}
+bool conv_frag_tap_ok(int Cin) { return Cin == CS_TAP_CIN; }
 
 hipError_t conv_pack_bank(const float* W, int Cout, int Cin, int k, int KWmax, int co_off, int co_pad, float* out,
                           hipStream_t s) {

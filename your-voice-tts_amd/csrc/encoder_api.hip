@@ -93,6 +93,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.out = bufs[l & 1];
         a.W = e->Wc[l];
         a.Wf = e->Wcf[l];
+        a.wf_tap = conv_frag_tap_ok(EDIM) ? 1 : 0;
         a.scale = e->sc[l];
         a.shift = e->sh[l];
         a.T = e->T;
@@ -111,6 +112,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.out = e->xi;
         a.W = e->Wp;
         a.Wf = e->Wpf;
+        a.wf_tap = conv_frag_tap_ok(EDIM) ? 1 : 0;
         a.shift = e->bp;
         a.T = e->T;
         a.Tmax = Lmax;
@@ -256,7 +258,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         CK(emalloc(e, &e->sh[l], EDIM));
         HK(conv_pack(w, EDIM, EDIM, 5, e->Wc[l], s));
         CK(emalloc(e, &e->Wcf[l], (size_t)EDIM * 5 * EDIM));
-        HK(conv_pack_frag(e->Wc[l], EDIM * 5, EDIM, e->Wcf[l], s));
+        HK(conv_frag_tap_ok(EDIM) ? conv_pack_frag_tap(e->Wc[l], EDIM, 5, EDIM, e->Wcf[l], s)
+                                  : conv_pack_frag(e->Wc[l], EDIM * 5, EDIM, e->Wcf[l], s));
         HK(fold_bn(bias, g, be, mu, var, EDIM, 1e-5f, e->sc[l], e->sh[l], s));
     }
     CK(emalloc(e, &e->Wp, (size_t)EDIM * 2 * EG));
@@ -276,7 +279,8 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         HK(sgemm_pack(whh, EH, nullptr, 0, EG, ROWMAP_LSTM, EH, e->Whh + d * sgemm_packed_floats(EG, EH), s));
     }
     CK(emalloc(e, &e->Wpf, (size_t)EDIM * 2 * EG));
-    HK(conv_pack_frag(e->Wp, EDIM, 2 * EG, e->Wpf, s));
+    HK(conv_frag_tap_ok(EDIM) ? conv_pack_frag_tap(e->Wp, EDIM, 1, 2 * EG, e->Wpf, s)
+                              : conv_pack_frag(e->Wp, EDIM, 2 * EG, e->Wpf, s));
     e->Bcap = max_batch;
     e->Lcap = max_len;
     const size_t BL = (size_t)max_batch * max_len;

@@ -141,9 +141,11 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
     for (int s = 0; s < L; ++s) {
         const float xnext = s + 1 < L ? xi_at(s + 1) : 0.f;  // in flight during this step
         const float* hs = hsb[s & 1];
-        float acc = 0.f;
+        // four independent accumulators (a 16-FMA dependency chain each instead of one of 64)
+        float a4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc = dot4(w[i], *reinterpret_cast<const float4*>(hs + kq * 64 + 4 * i), acc);
+        for (int i = 0; i < 16; ++i) a4[i & 3] = dot4(w[i], *reinterpret_cast<const float4*>(hs + kq * 64 + 4 * i), a4[i & 3]);
+        float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         // quad sum (k quarters), then gate pre-activation
         acc += dpp_move<0xB1, 0xf>(acc, 0.f);  // quad_perm [1,0,3,2]
         acc += dpp_move<0x4E, 0xf>(acc, 0.f);  // quad_perm [2,3,0,1]

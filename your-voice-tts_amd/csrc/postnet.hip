@@ -16,6 +16,7 @@ struct tts_postnet {
     int cin[5], cout[5], co_pad[5];
     float* W[5] = {};
     float* Wf[5] = {};  // fragment-order copies (conv_pack_frag): the small-batch conv kernel
+    int wf_tap[5] = {};  // ... in the tap-major order of its Cin = 512 form (conv_pack_frag_tap)
     float* scale[5] = {};
     float* shift[5] = {};
     float* buf[2] = {};
@@ -79,7 +80,10 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
             return TTS_ERR_NOMEM;
         }
         hipError_t e = conv_pack(w, co, ci, 5, p->W[l], s);
-        if (e == hipSuccess) e = conv_pack_frag(p->W[l], ci * 5, p->co_pad[l], p->Wf[l], s);
+        p->wf_tap[l] = conv_frag_tap_ok(ci) ? 1 : 0;
+        if (e == hipSuccess)
+            e = p->wf_tap[l] ? conv_pack_frag_tap(p->W[l], ci, 5, p->co_pad[l], p->Wf[l], s)
+                             : conv_pack_frag(p->W[l], ci * 5, p->co_pad[l], p->Wf[l], s);
         if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, 1e-5f, p->scale[l], p->shift[l], s);
         if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     }
@@ -147,6 +151,7 @@ tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const
         a.out = l == 4 ? out : p->buf[l & 1];
         a.W = p->W[l];
         a.Wf = p->Wf[l];
+        a.wf_tap = p->wf_tap[l];
         a.scale = p->scale[l];
         a.shift = p->shift[l];
         a.resid = l == 4 ? mel : nullptr;
