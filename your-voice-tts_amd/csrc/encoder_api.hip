@@ -366,21 +366,31 @@ tts_status tts_encoder_run_state(tts_encoder* e, const int32_t* ids, const int32
     if (!(try_resident && !state_in)) {
         if (tts_status st = init_state()) return st;
     }
+    // the batch-1 convs are enqueued directly: a graph launch followed by the resident launch left
+    // the GPU idle ~8.7 us between them (configs[1] timeline, round 5); TTS_ENC_GRAPH=1 restores it
+    static const bool conv_graph = [] {
+        const char* v = getenv("TTS_ENC_GRAPH");
+        return v && v[0] == '1';
+    }();
     if (try_resident) {
-        auto rit = e->rgraphs.find(Lmax);
-        if (rit == e->rgraphs.end()) {
-            hipGraph_t g = nullptr;
-            TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-            tts_status st = enqueue_encoder(e, 1, Lmax, Lmax, s, true);
-            hipError_t ee = hipStreamEndCapture(s, &g);
-            if (st) return st;
-            TTS_HIP(ee);
-            hipGraphExec_t exec = nullptr;
-            TTS_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
-            TTS_HIP(hipGraphDestroy(g));
-            rit = e->rgraphs.emplace(Lmax, exec).first;
+        if (!conv_graph) {
+            if (tts_status st = enqueue_encoder(e, 1, Lmax, Lmax, s, true)) return st;
+        } else {
+            auto rit = e->rgraphs.find(Lmax);
+            if (rit == e->rgraphs.end()) {
+                hipGraph_t g = nullptr;
+                TTS_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                tts_status st = enqueue_encoder(e, 1, Lmax, Lmax, s, true);
+                hipError_t ee = hipStreamEndCapture(s, &g);
+                if (st) return st;
+                TTS_HIP(ee);
+                hipGraphExec_t exec = nullptr;
+                TTS_HIP(hipGraphInstantiate(&exec, g, nullptr, nullptr, 0));
+                TTS_HIP(hipGraphDestroy(g));
+                rit = e->rgraphs.emplace(Lmax, exec).first;
+            }
+            TTS_HIP(hipGraphLaunch(rit->second, s));
         }
-        TTS_HIP(hipGraphLaunch(rit->second, s));
         bool launched = false;
         {
             tts_status st = enqueue_encoder_resident(e, Lmax, !state_in, s, &launched);

@@ -156,7 +156,9 @@ tts_status synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, cons
     const int cap = max_steps + 21;  // decoder steps_cap (>= max_steps + 20)
     const size_t T = (size_t)cap * s->r;
     tts_status st;
-    // buffers are only (re)allocated with nothing of this pipeline in flight
+    hipStream_t cs = static_cast<hipStream_t>(stream);
+    // buffers are only (re)allocated with nothing of this pipeline in flight (a batch-1 run works on
+    // the caller's stream: synth_stages)
     const bool regrow = (size_t)B * Lmax > s->ids_n || (size_t)B * Lmax * 512 > s->enc_n ||
                         (size_t)B * T * s->nmel > s->mel_n || (size_t)B * cap > s->stop_n;
     const int par = s->calls & 1;
@@ -164,6 +166,7 @@ tts_status synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, cons
     if (regrow || pin_need > s->pin_n[par]) {
         TTS_HIP(hipStreamSynchronize(ss));
         TTS_HIP(hipStreamSynchronize(s->gl_stream));
+        TTS_HIP(hipStreamSynchronize(cs));
     }
     if ((st = grow(&s->ids, s->ids_n, (size_t)B * Lmax))) return st;
     if ((st = grow(&s->enc, s->enc_n, (size_t)B * Lmax * 512))) return st;
@@ -200,6 +203,7 @@ tts_status synth_run(tts_synth* s, const int32_t* ids, const int32_t* lens, cons
     if (st) {
         (void)hipStreamSynchronize(s->stream);
         (void)hipStreamSynchronize(s->gl_stream);
+        (void)hipStreamSynchronize(cs);
         return st;
     }
     ++s->calls;  // only now: a failed call leaves the parity (and its drained buffers) to the next
@@ -222,14 +226,24 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
                         int Lmax, int max_steps, int gl_iters, uint64_t seed, double* wav, int64_t wav_cap,
                         int32_t* frames, void* stream) {
     hipStream_t cs = static_cast<hipStream_t>(stream);
-    hipStream_t ss = s->stream;
+    // a batch-1 run (the latency path) works on the caller's stream itself: every stage in stream
+    // order behind the caller's earlier work, and no cross-stream event between this call's stages
+    // or against the next call (each record / wait held the GPU ~6 us: the first Griffin-Lim
+    // launch waited on the caller's stream, the next call's first launch on the previous call's
+    // end-of-run event).  TTS_SYNTH_OWN_STREAM=1 restores the handle's own stream.
+    static const bool own_stream = [] {
+        const char* v = getenv("TTS_SYNTH_OWN_STREAM");
+        return v && v[0] == '1';
+    }();
+    hipStream_t ss = B == 1 && !own_stream ? cs : s->stream;
     const int cap = max_steps + 21;
     const size_t T = (size_t)cap * s->r;
     tts_status st;
     const int par = s->calls & 1;
     PipelineScope scope(s);
-    // the front stages do not wait for the caller's stream (they read host inputs and write this
-    // handle's buffers only), nor for the previous call's Griffin-Lim.  The persistent Griffin-Lim
+    // batch > 1: the front stages do not wait for the caller's stream (they read host inputs and
+    // write this handle's buffers only), nor for the previous call's Griffin-Lim (batch 1 runs on
+    // the caller's stream, in its order).  The persistent Griffin-Lim
     // (whose workgroups wait on each other) only runs on this same stream (<= 512 frames, below),
     // so it never shares the device with this call's resident launches.  A cross-stream Griffin-Lim
     // is the non-persistent per-iteration form; if its workgroups keep a resident encoder /
@@ -297,10 +311,10 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
         const int32_t Tcap[1] = {h->Tp};
         h->st = tts::postnet_run_dev(h->s->p, h->hist, h->mel_tmax, h->n_dev, h->s->r, Tcap, 1, h->T, h->post, q);
         if (h->st || !h->spec_gl) return;
-        // Griffin-Lim writes the caller's waveform: after the caller's stream.  An idle caller stream
-        // needs no cross-stream wait (its marker would hold the GPU ~5.8 us before the first
-        // Griffin-Lim launch)
-        const hipError_t idle = hipStreamQuery(h->cs);
+        // Griffin-Lim writes the caller's waveform: after the caller's stream (the same stream: in
+        // order already).  An idle caller stream needs no cross-stream wait (its marker would hold
+        // the GPU ~5.8 us before the first Griffin-Lim launch)
+        const hipError_t idle = q == h->cs ? hipSuccess : hipStreamQuery(h->cs);
         if (idle != hipSuccess && idle != hipErrorNotReady) {
             h->st = TTS_ERR_HIP;
             tts::set_error("tts_synth_run: caller stream query failed");
@@ -379,24 +393,28 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
     const bool same = frames_total <= 512;
     hipStream_t gs = same ? ss : s->gl_stream;
     if (gl_done) {  // enqueued behind the decoder already (hook_fn)
-        TTS_HIP(hipEventRecord(s->ev_out, ss));
-        TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+        if (ss != cs) {
+            TTS_HIP(hipEventRecord(s->ev_out, ss));
+            TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+        }
         return TTS_OK;
     }
-    TTS_HIP(hipEventRecord(s->ev_in, cs));
+    if (gs != cs) TTS_HIP(hipEventRecord(s->ev_in, cs));
     if (!same) {
         TTS_HIP(hipEventRecord(s->ev_post, ss));
         TTS_HIP(hipStreamWaitEvent(gs, s->ev_post, 0));
     }
-    TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
+    if (gs != cs) TTS_HIP(hipStreamWaitEvent(gs, s->ev_in, 0));
     // shorter sentences leave their waveform tail unwritten: zero it
     if (B > 1) TTS_HIP(hipMemsetAsync(wav, 0, sizeof(double) * (size_t)B * s->hop * (Fmax - 1), gs));
     // at r = 1 the decoder's device step counts are the frame counts: no upload
     if ((st = tts::gl_run_dev(s->g, TTS_GL_FROM_MEL, spec, h_frames, s->r == 1 ? n_dev : nullptr, B, Fmax, nullptr, seed,
                               gl_iters, wav, gs)))
         return st;
-    TTS_HIP(hipEventRecord(s->ev_out, gs));
-    TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+    if (gs != cs) {
+        TTS_HIP(hipEventRecord(s->ev_out, gs));
+        TTS_HIP(hipStreamWaitEvent(cs, s->ev_out, 0));
+    }
     return TTS_OK;
 }
 }  // namespace
