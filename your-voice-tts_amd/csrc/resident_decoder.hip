@@ -482,19 +482,23 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         const unsigned E = (a.salt << 14) | (((unsigned)t & 2047u) << 3);
         const unsigned EP6 = ((a.salt << 14) | (((unsigned)(t - 1) & 2047u) << 3)) + 6u;
         // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}]
-        float acc_a = 0.f;
+        // (two accumulators each: dependency chains of 24 and 16 FMAs instead of 48 and 32, ahead
+        // of the pre1 poll)
+        float aa[2] = {0.f, 0.f};
 #pragma unroll
-        for (int i = 2; i < 6; ++i) acc_a = dot4(wa[i], ld4(xctx + (i - 2) * 128 + ks * 4), acc_a);
+        for (int i = 2; i < 6; ++i) aa[i & 1] = dot4(wa[i], ld4(xctx + (i - 2) * 128 + ks * 4), aa[i & 1]);
 #pragma unroll
-        for (int i = 6; i < 10; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
+        for (int i = 6; i < 10; ++i) aa[i & 1] = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), aa[i & 1]);
         asm volatile("" ::: "memory");  // bound the hoisted LDS loads (register pressure)
 #pragma unroll
-        for (int i = 10; i < 14; ++i) acc_a = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), acc_a);
+        for (int i = 10; i < 14; ++i) aa[i & 1] = dot4(wa[i], ld4(xh_att + (i - 6) * 128 + ks * 4), aa[i & 1]);
+        float acc_a = aa[0] + aa[1];
         // decoder LSTM over h_dec_{t-1}, also while pre1 is in flight
-        float acc_d = 0.f;
+        float ad[2] = {0.f, 0.f};
 #pragma unroll 2
         for (int i = 8; i < 16; ++i)
-            acc_d = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), acc_d);
+            ad[i & 1] = dot4(wdl[(i * 16 + r) * 32 + ks], ld4(xh_dec + (i - 8) * 128 + ks * 4), ad[i & 1]);
+        float acc_d = ad[0] + ad[1];
         // 2) prenet layer 2: wave 0 gathers this XCD's pre1_t (+ the previous step's continue flag);
         //    every wave computes its row of this XCD's copy, publishes it XCD-locally; wave 0 gathers
         // (waves 0, 1: the 256 rows as pairs; wave 2, lane 0: the flag)
