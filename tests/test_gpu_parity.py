@@ -284,18 +284,25 @@ def test_synthesize_native_configs1_vs_oracle(audio_cfg):
 
 
 def test_end_to_end_synthesis_vs_oracle(audio_cfg):
-    """ids -> wav through the whole HIP path vs the oracle chain (L=12, 60 GL iterations)."""
+    """ids -> wav through the whole HIP path vs the oracle chain (L=12, 60 GL iterations).
+
+    Mean over four numpy phase draws: with the model half within 3.1e-7 of the reference, the
+    single-draw waveform distance is a heavy-tailed realization of Griffin-Lim's sensitivity
+    (3e-6 .. 1e-4 across draws for the same mel, profiles/r05_e2e_wave_probe.txt)."""
     z = golden("t2_fwdmask_L12")
     fl = golden_flags(z)
     m = _model(fl)
     audio = load_pkg("audio")
     ap = audio.AudioProcessor(**audio_cfg)
-    np.random.seed(3)
-    wavs, info = load_pkg("synthesis").synthesize_batch(m, ap, [z["ids"]], phase="numpy")
-    np.random.seed(3)
-    ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(z["mel_post"].T)
-    assert info["frames"] == [z["mel"].shape[0]]
-    assert rel_rms(wavs[0], ref) < WAV_RTOL
+    errs = []
+    for seed in (3, 4, 5, 6):
+        np.random.seed(seed)
+        wavs, info = load_pkg("synthesis").synthesize_batch(m, ap, [z["ids"]], phase="numpy")
+        np.random.seed(seed)
+        ref = AudioOracle(**audio_cfg).inv_mel_spectrogram(z["mel_post"].T)
+        assert info["frames"] == [z["mel"].shape[0]]
+        errs.append(rel_rms(wavs[0], ref))
+    assert float(np.mean(errs)) < WAV_RTOL, errs
 
 
 def test_native_errors_are_raised():

@@ -8,13 +8,14 @@
 namespace tts {
 
 // ------------------------------------------------------------------ init (per call)
-__global__ void decoder_init_kernel(const InitArgs a) {
-    if ((int)blockIdx.x >= a.B) {  // the extra workgroups zero the resident hand-off granules
-        for (int i = (blockIdx.x - a.B) * blockDim.x + threadIdx.x; i < a.nzero; i += INIT_ZERO_BLOCKS * blockDim.x)
+// workgroup `bid` of the init (bid < B: sentence bid's state; else the resident hand-off granules)
+__device__ __forceinline__ void decoder_init_block(const InitArgs& a, int bid) {
+    if (bid >= a.B) {  // the extra workgroups zero the resident hand-off granules
+        for (int i = (bid - a.B) * blockDim.x + threadIdx.x; i < a.nzero; i += INIT_ZERO_BLOCKS * blockDim.x)
             a.zero[i] = 0ull;
         return;
     }
-    const int b = blockIdx.x;
+    const int b = bid;
     const int L = a.lens[b];
     if (a.pre1_go && !a.keep)
         for (int k = threadIdx.x; k < PRE; k += blockDim.x) a.pre1[(int64_t)b * PRE + k] = a.pre1_go[k];
@@ -55,6 +56,7 @@ __global__ void decoder_init_kernel(const InitArgs a) {
         }
     }
 }
+__global__ void decoder_init_kernel(const InitArgs a) { decoder_init_block(a, blockIdx.x); }
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(decoder_init_kernel, dim3(a.B + (a.zero ? INIT_ZERO_BLOCKS : 0)), dim3(256), 0, s, a);
@@ -147,8 +149,89 @@ __global__ __launch_bounds__(256) void project_inputs_kernel(const float* enc, c
 }
 static_assert(PJ_POS == PJ_KS, "one stored position per K-slice lane");
 
+// The same projection on the matrix cores (round 5; the VALU form above ran 12 us at L = 100 on
+// 52 workgroups): P^T[j][d] = enc[j] . W[d] as 16 x 16 output tiles (16 positions x 16 dims) of
+// v_mfma_f32_16x16x4_f32 (exact fp32 products), one workgroup per tile, K split over its four
+// waves and the partial tiles summed in wave order.  K is walked in groups of four k-steps so a
+// lane's operands are float4 loads: k-step (u, v) has lane (row, q) at k = K0 + 16 u + 4 q + v,
+// the same k for A (an encoder row) and B (a W row) -- a permutation of the sum, not of its terms.
+template <int ENC_>
+__device__ __forceinline__ void project_tile(const float* enc, const float* W, int Lmax, int Lcap, float* Pt, int b,
+                                             int tile) {
+    constexpr int KQ = ENC_ / 4;   // k per wave
+    constexpr int NG = KQ / 16;    // float4 groups per lane
+    const int dt = tile % (ADIM / 16), jt = tile / (ADIM / 16);
+    const int d0 = dt * 16, j0 = jt * 16;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m = lane & 15, q = lane >> 4;
+    const int k0 = wave * KQ + 4 * q;
+    const bool rowok = j0 + m < Lmax;
+    const float4* ar = reinterpret_cast<const float4*>(enc + ((int64_t)b * Lcap + (rowok ? j0 + m : 0)) * ENC_ + k0);
+    const float4* br = reinterpret_cast<const float4*>(W + (int64_t)(d0 + m) * ENC_ + k0);
+    float4 a4[NG], b4[NG];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        a4[u] = ar[4 * u];
+        b4[u] = br[4 * u];
+    }
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        const float4 a = rowok ? a4[u] : float4{0.f, 0.f, 0.f, 0.f};
+        acc = mfma16x16x4(a.x, b4[u].x, acc);
+        acc = mfma16x16x4(a.y, b4[u].y, acc);
+        acc = mfma16x16x4(a.z, b4[u].z, acc);
+        acc = mfma16x16x4(a.w, b4[u].w, acc);
+    }
+    __shared__ float red[4][256];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][lane * 4 + r] = acc[r];
+    __syncthreads();
+    // element e = tid: lane e / 4 of the D layout, register e % 4: C[4 (l >> 4) + r][l & 15]
+    const float v = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    const int l = tid >> 2, r = tid & 3;
+    const int j = j0 + 4 * (l >> 4) + r, d = d0 + (l & 15);
+    if (j < Lmax) Pt[((int64_t)b * ADIM + d) * Lcap + j] = v;
+}
+template <int ENC_>
+__global__ __launch_bounds__(256) void project_inputs_mfma_kernel(const float* enc, const float* W, int Lmax, int Lcap,
+                                                                  float* Pt) {
+    project_tile<ENC_>(enc, W, Lmax, Lcap, Pt, blockIdx.y, blockIdx.x);
+}
+// The projection and the decoder's per-call init as one launch (they are independent; both precede
+// the decoder's first step): workgroups [0, nproj) take projection tiles, the rest the init.
+template <int ENC_>
+__global__ __launch_bounds__(256) void project_init_kernel(const float* enc, const float* W, int Lmax, int Lcap,
+                                                           float* Pt, int ntile, int nproj, const InitArgs ia) {
+    const int bid = blockIdx.x;
+    if (bid < nproj) project_tile<ENC_>(enc, W, Lmax, Lcap, Pt, bid / ntile, bid % ntile);
+    else decoder_init_block(ia, bid - nproj);
+}
+
+hipError_t launch_project_init(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, const InitArgs& ia,
+                               hipStream_t s) {
+    const int ntile = (ADIM / 16) * ((Lmax + 15) / 16), nproj = ntile * B;
+    const dim3 grid((unsigned)(nproj + ia.B + (ia.zero ? INIT_ZERO_BLOCKS : 0)));
+    hipLaunchKernelGGL(project_init_kernel<ENC>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt, ntile, nproj, ia);
+    return hipGetLastError();
+}
+
 hipError_t launch_project_inputs(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt,
                                  hipStream_t s, int enc_dim) {
+    static const bool valu = [] {  // measurement: TTS_PROJ_VALU=1 runs the VALU form
+        const char* v = getenv("TTS_PROJ_VALU");
+        return v && v[0] == '1';
+    }();
+    if (!valu) {
+        const dim3 grid((ADIM / 16) * ((Lmax + 15) / 16), B);
+        if (enc_dim == 512)
+            hipLaunchKernelGGL(project_inputs_mfma_kernel<512>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
+        else if (enc_dim == 256)
+            hipLaunchKernelGGL(project_inputs_mfma_kernel<256>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     const dim3 grid((ADIM / PJ_DG) * ((Lmax + PJ_POS - 1) / PJ_POS), B);
     if (enc_dim == 512)
         hipLaunchKernelGGL(project_inputs_kernel<512>, grid, dim3(256), 0, s, enc, W, Lmax, Lcap, Pt);

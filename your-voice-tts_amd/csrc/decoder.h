@@ -118,6 +118,9 @@ hipError_t launch_query_energy(const QEArgs& a, int B, hipStream_t s);
 bool attention_uses_epart(const AttnArgs& a);
 
 hipError_t launch_decoder_init(const InitArgs& a, hipStream_t s);
+// launch_project_inputs (ENC = 512) and launch_decoder_init as one launch
+hipError_t launch_project_init(const float* enc, const float* W, int B, int Lmax, int Lcap, float* Pt, const InitArgs& ia,
+                               hipStream_t s);
 // teacher forcing: mem[b] = teacher row step-1 of frames[b] (ldb floats per sentence), go frame at step 0
 hipError_t launch_teacher_memory(const float* frames, int64_t ldb, int width, const int* step, float* mem, int B,
                                  hipStream_t s);

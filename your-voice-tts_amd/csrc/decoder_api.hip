@@ -717,7 +717,13 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                                  B, hipMemcpyDeviceToDevice, s));
     const int* lens_dev = direct && d->io_lens ? d->io_lens : d->lens;
     if (lens_dev == d->lens) TTS_HIP(hipMemcpyAsync(d->lens, lens, sizeof(int) * B, hipMemcpyHostToDevice, s));
-    TTS_HIP(launch_project_inputs(direct ? enc : d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
+    // (the memory projection goes out with the init launch below, unless the VALU form is asked for)
+    static const bool proj_valu = [] {  // measurement: TTS_PROJ_VALU=1, the VALU projection launch
+        const char* v = getenv("TTS_PROJ_VALU");
+        return v && v[0] == '1';
+    }();
+    const bool proj_fused = !proj_valu;
+    if (!proj_fused) TTS_HIP(launch_project_inputs(direct ? enc : d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, s));
     d->last_enc_direct = direct ? enc : nullptr;
     d->last_len_direct = lens[0];
     InitArgs ia{};
@@ -752,7 +758,8 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ia.pre1 = d->pre1;
         ia.pre1_go = d->pre1_go_ok ? d->pre1_go : nullptr;
     }
-    TTS_HIP(launch_decoder_init(ia, s));
+    if (proj_fused) TTS_HIP(launch_project_init(direct ? enc : d->enc, d->W_in, B, Lmax, d->Lcap, d->Pt, ia, s));
+    else TTS_HIP(launch_decoder_init(ia, s));
     if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
     if (!keep && !ia.pre1_go) {
         tts_status st = enqueue_prenet_go(d, B, s);
