@@ -67,7 +67,7 @@ def test_resident_decoder_and_encoder_fallback_match_multilaunch():
         ml = _t2()
         want = ml.inference_batch(ids)
         assert not ml.last_timing["resident"] and not ml.last_timing["encoder_resident"]
-    with _env(TTS_CU_CAP=64):
+    with _env(TTS_CU_CAP=8):  # (the encoder's 128-thread workgroups fit 256 on 64 CUs)
         fb = _t2()
         got = fb.inference_batch(ids)
         assert not fb.last_timing["resident"] and not fb.last_timing["encoder_resident"]

@@ -4,7 +4,7 @@
 
 namespace tts {
 
-constexpr int ENC_RES_STATUS_PLACEMENT = 50;  // fewer than 16 workgroups on CU 0's XCD
+constexpr int ENC_RES_STATUS_PLACEMENT = 50;  // fewer than the roles' workgroups on the XCD(s) they take
 
 struct EncResArgs {
     const float4* w;     // packed W_hh of both directions (encoder_resident_pack)

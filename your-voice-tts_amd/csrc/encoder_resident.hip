@@ -1,15 +1,22 @@
 // Resident batch-1 encoder BiLSTM (Encoder.inference's nn.LSTM, layers/tacotron2.py:56-61, 82):
 // the whole recurrence of both directions as ONE launch instead of L dependent step launches.
 //
-// 256 workgroups are launched; each reads its XCC id and the 256-entry table of all of them, and
-// the first 16 workgroups (by index) of CU 0's XCD take the roles direction = rank / 8, slot =
-// rank % 8; the rest exit.  A role holds W_hh rows of 32 hidden units (x 4 gates, 128 rows x 256,
-// 128 KiB) in VGPRs; thread (row r = tid / 4, k quarter q = tid % 4) owns W_hh[row][64q .. 64q+64).
-// Rows are unit-major (r = 4 u + gate) so the 16 lanes of a unit hold its 4 gate sums after the
-// quad reduction, and one lane per unit updates (c, h) like the sgemm ENC_LSTM epilogue.  Per
-// step every role publishes its 32 h values as 8-byte {tag, value} granules with a
-// workgroup-scope store (the line stays in the XCD's L2) and gathers its direction's 256 values
-// with agent-scope loads: XCD-local hand-offs, no fences.  Waits are bounded (status on timeout).
+// 256 workgroups are launched; each reads its XCC id and the 256-entry table of all of them.  The
+// forward direction takes the first 32 workgroups (by index) of workgroup 0's XCD, the backward
+// direction the first 32 of the next XCD (slot = rank in the XCD); the rest exit.  A role holds
+// W_hh rows of 8 hidden units (x 4 gates, 32 rows x 256, 32 KiB) in VGPRs; thread (row r = tid / 4,
+// k quarter q = tid % 4) owns W_hh[row][64q .. 64q+64).  Rows are unit-major (r = 4 u + gate) so
+// the 16 lanes of a unit hold its 4 gate sums after the quad reduction, and one lane per unit
+// updates (c, h) like the sgemm ENC_LSTM epilogue.  Per step every role publishes its 8 h values
+// as 8-byte {tag, value} granules with a workgroup-scope store (the line stays in the XCD's L2)
+// and gathers its direction's 256 values with agent-scope loads: XCD-local hand-offs, no fences.
+// Waits are bounded (status on timeout).
+//
+// Geometry (ENC_RES_WIDE, measured at L = 100 per encoder call, round 5): 0 = both directions on
+// one XCD, 16 workgroups x 512 threads (32 units each): 257 us; 1 = one XCD, 32 x 256: 221 us;
+// 2 (default) = one XCD per direction, 64 x 128: 202 us.  The step is the dot products' issue
+// (one wave per SIMD) plus the XCD-local edge, so spreading the rows over more CUs pays until
+// the edge dominates.
 #include "encoder_resident.h"
 
 #ifndef ENC_SLEEP
@@ -23,9 +30,13 @@ typedef unsigned long long u64;
 typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) int gint;
 
-constexpr int ER_THREADS = 512;
-constexpr int ER_SLOTS = 8;    // workgroups per direction
-constexpr int ER_UNITS = 32;   // hidden units per workgroup
+#ifndef ENC_RES_WIDE
+#define ENC_RES_WIDE 2
+#endif
+constexpr int ER_THREADS = ENC_RES_WIDE == 2 ? 128 : ENC_RES_WIDE ? 256 : 512;
+constexpr int ER_SLOTS = ENC_RES_WIDE == 2 ? 32 : ENC_RES_WIDE ? 16 : 8;  // workgroups per direction
+constexpr int ER_UNITS = ER_THREADS / 16;                                   // hidden units per workgroup
+constexpr bool ER_SPLIT = ENC_RES_WIDE == 2;  // one XCD per direction (else both on CU 0's XCD)
 constexpr int H = 256, G4 = 4 * H;
 constexpr int GR_TABLE = 0, GR_H = 256;  // granules: table [256], h [2 parity][2 dir][256]
 
@@ -94,16 +105,32 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         float v[4];
         const bool ok = sweep4(a.gran + GR_TABLE, setup_tag, v, a.tmo);
         const int xref = __builtin_amdgcn_readfirstlane(__float_as_int(v[0]) & 7);
-        int rank = 0, nref = 0;
+        // ER_SPLIT: the backward direction on the XCD of the first workgroup off xref's XCD
+        int first = 1 << 20;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u64 m = __ballot((__float_as_int(v[i]) & 7) != xref);
+            if (m) first = min(first, 4 * __builtin_ctzll(m) + i);
+        }
+        const int xref1 = ER_SPLIT && first < 256 ? __float_as_int(__uint_as_float((unsigned)peek(a.gran + GR_TABLE + first))) & 7 : xref;
+        const int xmine = ER_SPLIT && xcc == xref1 ? xref1 : xref;
+        int rank = 0, nref = 0, nref1 = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int x = __float_as_int(v[i]) & 7;
             nref += __popcll(__ballot(x == xref));
-            rank += __popcll(__ballot(x == xref && lane * 4 + i < c));
+            nref1 += __popcll(__ballot(x == xref1));
+            rank += __popcll(__ballot(x == xmine && lane * 4 + i < c));
+        }
+        if (ER_SPLIT) {
+            if (xref1 == xref) nref = 0;  // one XCD only: no placement for the split form
+            nref = min(nref, nref1) * 2;  // the roles need ER_SLOTS on each of the two XCDs
         }
         if (lane == 0) {
             info[0] = ok ? 1 : 0;
-            info[1] = xcc == xref ? rank : -1;
+            info[1] = !ER_SPLIT ? (xcc == xref ? rank : -1)
+                                : xcc == xref ? rank : xcc == xref1 ? ER_SLOTS + rank : -1;
+            if (ER_SPLIT && rank >= ER_SLOTS) info[1] = -1;
             info[2] = nref;
             info[3] = 0;
             // status word = salt << 8 | code (res_status_code): no clearing between launches
