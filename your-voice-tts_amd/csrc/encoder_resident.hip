@@ -4,9 +4,9 @@
 // 256 workgroups are launched; each reads its XCC id and the 256-entry table of all of them.  The
 // forward direction takes the first 32 workgroups (by index) of workgroup 0's XCD, the backward
 // direction the first 32 of the next XCD (slot = rank in the XCD); the rest exit.  A role holds
-// W_hh rows of 8 hidden units (x 4 gates, 32 rows x 256, 32 KiB) in VGPRs; thread (row r = tid / 4,
-// k quarter q = tid % 4) owns W_hh[row][64q .. 64q+64).  Rows are unit-major (r = 4 u + gate) so
-// the 16 lanes of a unit hold its 4 gate sums after the quad reduction, and one lane per unit
+// W_hh rows of 8 hidden units (x 4 gates, 32 rows x 256, 32 KiB) in VGPRs; thread (row r = tid / 8,
+// k slice q = tid % 8) owns W_hh[row][32q .. 32q+32).  Rows are unit-major (r = 4 u + gate) so
+// the 32 lanes of a unit hold its 4 gate sums after the 8-lane reduction, and one lane per unit
 // updates (c, h) like the sgemm ENC_LSTM epilogue.  Per step every role publishes its 8 h values
 // as 8-byte {tag, value} granules with a workgroup-scope store (the line stays in the XCD's L2)
 // and gathers its direction's 256 values with agent-scope loads: XCD-local hand-offs, no fences.
@@ -14,8 +14,9 @@
 //
 // Geometry (ENC_RES_WIDE, measured at L = 100 per encoder call, round 5): 0 = both directions on
 // one XCD, 16 workgroups x 512 threads (32 units each): 257 us; 1 = one XCD, 32 x 256: 221 us;
-// 2 (default) = one XCD per direction, 64 x 128: 202 us.  The step is the dot products' issue
-// (one wave per SIMD) plus the XCD-local edge, so spreading the rows over more CUs pays until
+// 2 = one XCD per direction, 64 x 128 (4 k slices per row): 202-212 us; 3 (default) = the same
+// with 8 k slices per row, 64 x 256 (every SIMD of the CU issues): 191-203 us.  The step is the
+// dot products' issue plus the XCD-local edge, so spreading the rows over more SIMDs pays until
 // the edge dominates.
 #include "encoder_resident.h"
 
@@ -31,13 +32,15 @@ typedef __attribute__((address_space(1))) u64 gu64;
 typedef __attribute__((address_space(1))) int gint;
 
 #ifndef ENC_RES_WIDE
-#define ENC_RES_WIDE 2
+#define ENC_RES_WIDE 3
 #endif
-constexpr int ER_THREADS = ENC_RES_WIDE == 2 ? 128 : ENC_RES_WIDE ? 256 : 512;
-constexpr int ER_SLOTS = ENC_RES_WIDE == 2 ? 32 : ENC_RES_WIDE ? 16 : 8;  // workgroups per direction
-constexpr int ER_UNITS = ER_THREADS / 16;                                   // hidden units per workgroup
-constexpr bool ER_SPLIT = ENC_RES_WIDE == 2;  // one XCD per direction (else both on CU 0's XCD)
+constexpr int ER_THREADS = ENC_RES_WIDE == 2 ? 128 : ENC_RES_WIDE == 1 || ENC_RES_WIDE == 3 ? 256 : 512;
+constexpr int ER_SLOTS = ENC_RES_WIDE >= 2 ? 32 : ENC_RES_WIDE ? 16 : 8;  // workgroups per direction
+constexpr int ER_KS = ENC_RES_WIDE == 3 ? 8 : 4;                           // threads (k slices) per gate row
+constexpr int ER_UNITS = ER_THREADS / (4 * ER_KS);                         // hidden units per workgroup
+constexpr bool ER_SPLIT = ENC_RES_WIDE >= 2;  // one XCD per direction (else both on CU 0's XCD)
 constexpr int H = 256, G4 = 4 * H;
+constexpr int ER_NW = H / 4 / ER_KS;  // float4 weights per thread
 constexpr int GR_TABLE = 0, GR_H = 256;  // granules: table [256], h [2 parity][2 dir][256]
 
 __device__ __forceinline__ void pub_dev(u64* g, unsigned tag, float v) {
@@ -144,13 +147,13 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
     const int role = info[1];
     if (!info[0] || info[2] < 2 * ER_SLOTS || role < 0 || role >= 2 * ER_SLOTS) return;
     const int dir = role / ER_SLOTS, slot = role % ER_SLOTS;
-    const int row = tid >> 2, kq = tid & 3;  // row = 4 * unit_local + gate
+    const int row = tid / ER_KS, kq = tid % ER_KS;  // row = 4 * unit_local + gate
     const int ul = row >> 2, gate = row & 3;
     const int unit = slot * ER_UNITS + ul;
-    float4 w[16];
-    const float4* wp = a.w + ((size_t)(dir * ER_SLOTS + slot) * 16) * ER_THREADS + tid;
+    float4 w[ER_NW];
+    const float4* wp = a.w + ((size_t)(dir * ER_SLOTS + slot) * ER_NW) * ER_THREADS + tid;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = wp[(size_t)i * ER_THREADS];
+    for (int i = 0; i < ER_NW; ++i) w[i] = wp[(size_t)i * ER_THREADS];
     // initial state
     for (int k = tid; k < H; k += ER_THREADS) hsb[0][k] = a.h0 ? a.h0[dir * a.hdir + k] : 0.f;
     float cs = 0.f;  // cell of `unit` (lanes with row & 3 == 0 && kq == 0)
@@ -171,19 +174,28 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         // four independent accumulators (a 16-FMA dependency chain each instead of one of 64)
         float a4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) a4[i & 3] = dot4(w[i], *reinterpret_cast<const float4*>(hs + kq * 64 + 4 * i), a4[i & 3]);
+        for (int i = 0; i < ER_NW; ++i)
+            a4[i & 3] = dot4(w[i], *reinterpret_cast<const float4*>(hs + kq * (H / ER_KS) + 4 * i), a4[i & 3]);
         float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-        // quad sum (k quarters), then gate pre-activation
+        // sum over the row's k slices, then gate pre-activation
         acc += dpp_move<0xB1, 0xf>(acc, 0.f);  // quad_perm [1,0,3,2]
         acc += dpp_move<0x4E, 0xf>(acc, 0.f);  // quad_perm [2,3,0,1]
+        if constexpr (ER_KS == 8) acc += dpp_move<0x141, 0xf>(acc, 0.f);  // row_half_mirror: the other quad
         const float pre = acc + xcur;
         const float act = gate == 2 ? tanh_cell(pre) : sigmoid_cell(pre);
-        const float f = dpp_move<0x104, 0xf>(act, 0.f);  // row_shl:4  -> gate 1 of this unit
-        const float g = dpp_move<0x108, 0xf>(act, 0.f);  // row_shl:8  -> gate 2
-        const float o = dpp_move<0x10C, 0xf>(act, 0.f);  // row_shl:12 -> gate 3
+        float f, g, o;
+        if constexpr (ER_KS == 4) {
+            f = dpp_move<0x104, 0xf>(act, 0.f);  // row_shl:4  -> gate 1 of this unit
+            g = dpp_move<0x108, 0xf>(act, 0.f);  // row_shl:8  -> gate 2
+            o = dpp_move<0x10C, 0xf>(act, 0.f);  // row_shl:12 -> gate 3
+        } else {  // gate rows 8 lanes apart: gates 2, 3 sit in the next DPP row (lane ^ 16 swizzle)
+            f = dpp_move<0x108, 0xf>(act, 0.f);  // row_shl:8 -> gate 1
+            g = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, act), 0x401F));
+            o = __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, f), 0x401F));
+        }
         const int par = s & 1;
         u64* gh = a.gran + GR_H + (par * 2 + dir) * H;
-        if ((tid & 15) == 0) {
+        if ((tid & (4 * ER_KS - 1)) == 0) {
             cs = f * cs + act * g;  // c' = s(f) c + s(i) tanh(g)
             const float h = o * tanh_cell(cs);
             hlast = h;
@@ -208,7 +220,7 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
         __syncthreads();
         if (info[3] == 1) return;
     }
-    if ((tid & 15) == 0 && L > 0) {
+    if ((tid & (4 * ER_KS - 1)) == 0 && L > 0) {
         a.h_fin[dir * a.hdir + unit] = hlast;
         a.c_fin[dir * a.hdir + unit] = cs;
     }
@@ -370,13 +382,13 @@ __global__ __launch_bounds__(EB_THREADS, 1) void encoder_resident_batch_kernel(c
 
 __global__ void enc_res_pack_kernel(const float* whh_f, const float* whh_b, float4* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)2 * ER_SLOTS * 16 * ER_THREADS) return;
-    const int tid = i % ER_THREADS, i4 = (i / ER_THREADS) % 16, slot = (i / (16 * ER_THREADS)) % ER_SLOTS;
-    const int dir = i / (16 * ER_THREADS * ER_SLOTS);
-    const int row = tid >> 2, kq = tid & 3, ul = row >> 2, gate = row & 3;
+    if (i >= (int64_t)2 * ER_SLOTS * ER_NW * ER_THREADS) return;
+    const int tid = i % ER_THREADS, i4 = (i / ER_THREADS) % ER_NW, slot = (i / (ER_NW * ER_THREADS)) % ER_SLOTS;
+    const int dir = i / (ER_NW * ER_THREADS * ER_SLOTS);
+    const int row = tid / ER_KS, kq = tid % ER_KS, ul = row >> 2, gate = row & 3;
     const int ref = gate * H + slot * ER_UNITS + ul;
     const float* W = dir ? whh_b : whh_f;
-    const float* p = W + (int64_t)ref * H + kq * 64 + 4 * i4;
+    const float* p = W + (int64_t)ref * H + kq * (H / ER_KS) + 4 * i4;
     out[i] = float4{p[0], p[1], p[2], p[3]};
 }
 
@@ -393,7 +405,7 @@ hipError_t launch_encoder_resident_batch(const EncResBatchArgs& a, hipStream_t s
                              args, 0, s, launched);
 }
 
-size_t encoder_resident_weight_float4() { return (size_t)2 * ER_SLOTS * 16 * ER_THREADS; }
+size_t encoder_resident_weight_float4() { return (size_t)2 * ER_SLOTS * ER_NW * ER_THREADS; }
 size_t encoder_resident_granules() { return GR_H + 4 * H + 2; }
 
 hipError_t encoder_resident_pack(const float* whh_f, const float* whh_b, float4* out, hipStream_t s) {
