@@ -23,6 +23,7 @@ struct ConvArgs {
     const float* W;      // packed [Cin][KW][co_pad]
     const float* Wf;     // optional fragment-order copy of W (conv_pack_frag): small batches use it
     int wf_tap;          // Wf is in conv_pack_frag_tap's tap-major order (Cin = 512)
+    const float* Wf16;   // optional conv_pack_frag_tap16 copy (with wf_tap): small grids take 16-channel tiles
     const float* scale;  // [Cout] (null = 1)
     const float* shift;  // [Cout] (null = 0)
     const float* resid;  // [B][Tmax][out_ld] or null: out = resid + y (CONV_HIGHWAY: the layer input)
@@ -62,6 +63,8 @@ hipError_t conv_pack_bank(const float* W, int Cout, int Cin, int k, int KWmax, i
 hipError_t conv_pack_frag(const float* W, int K, int co_pad, float* out, hipStream_t s);
 // the tap-major fragment order (k' = tap Cin + ci) of the small-batch conv's TAP form; Cin = 512 only
 hipError_t conv_pack_frag_tap(const float* W, int Cin, int KW, int co_pad, float* out, hipStream_t s);
+// the same for 16-column tiles (the small-batch conv's 16-channel form)
+hipError_t conv_pack_frag_tap16(const float* W, int Cin, int KW, int co_pad, float* out, hipStream_t s);
 bool conv_frag_tap_ok(int Cin);
 // W [Cout][Cin] (Linear layout, rows stacked into Cout) -> packed [Cin][1][co_pad]
 hipError_t linear_pack_as_conv(const float* W, int Cout, int Cin, int co_offset, int co_pad, float* out,

@@ -12,6 +12,7 @@
 // convs), BM=16 (1x4 waves of 16x16) so that a single sentence still spreads over >= 100 workgroups.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv1d.h"
 
@@ -472,16 +473,22 @@ constexpr int CS_BM = 16, CS_BN = 32, CS_PR = 8, CS_WAVES = 8, CS_THREADS = 64 *
 // consecutive fragment pairs: no per-k-step index arithmetic (round 5: it was the loop's limiter,
 // ~9 VALU per A operand beside the MFMAs).
 constexpr int CS_TAP_CIN = 8 * CS_WAVES * CS_PR;  // 512
-template <int KW, bool TAP>
+// N16 (TAP only, weights from conv_pack_frag_tap16): 16 output channels per workgroup, for grids
+// that would leave CUs idle at 32 (the batch-1 encoder convs: 7 frame tiles x 16 channel tiles =
+// 112 workgroups at L = 100).  Its accumulator chain is the 32-wide form's acc0 for the same
+// channels (same MFMAs in the same order): bitwise the same outputs.
+template <int KW, bool TAP, bool N16>
 __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a) {
+    static_assert(TAP || !N16, "the 16-channel form is tap-major only");
+    constexpr int BN = N16 ? 16 : CS_BN;
     constexpr int PAD = (KW - 1) / 2;
     constexpr int XR = CS_BM + KW - 1;
     extern __shared__ float xs[];  // [XR][Cin + 1] input rows; then the waves' partial tiles
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int Tt = a.Ttile ? a.Ttile : a.Tmax;
-    const int nct = a.co_pad / CS_BN, mtiles = (Tt + CS_BM - 1) / CS_BM;
+    const int nct = a.co_pad / BN, mtiles = (Tt + CS_BM - 1) / CS_BM;
     const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
-    const int b = rest / mtiles, t0 = (rest % mtiles) * CS_BM, c0 = ct * CS_BN;
+    const int b = rest / mtiles, t0 = (rest % mtiles) * CS_BM, c0 = ct * BN;
     const int Tb = a.tmul > 1 ? a.T[b] * a.tmul : a.T[b];
     if (t0 >= Tb) return;
     const int Cin = a.Cin, ldx = Cin + 1;
@@ -494,8 +501,9 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     const int q = lane >> 4, row = lane & 15;
     const int np = nks >> 1;  // pairs (K is a multiple of 8)
     const int p_beg = wave * np / CS_WAVES, p_end = (wave + 1) * np / CS_WAVES;
-    const float4* Wf = reinterpret_cast<const float4*>(a.Wf) + (int64_t)ct * np * 64 + lane;
-    float4 wr[CS_PR];
+    using WT = std::conditional_t<N16, float2, float4>;
+    const WT* Wf = reinterpret_cast<const WT*>(N16 ? a.Wf16 : a.Wf) + (int64_t)ct * np * 64 + lane;
+    WT wr[CS_PR];
     const int pw = wave * (CS_TAP_CIN / CS_WAVES) / 8;  // (TAP: this wave's first pair of tap 0)
     if constexpr (!TAP) {
 #pragma unroll
@@ -545,15 +553,20 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
             const int pn = (tap + 1) * (CS_TAP_CIN / 8) + pw;
 #pragma unroll
             for (int i = 0; i < CS_PR; ++i) {
-                acc0 = mfma16x16x4(xa[2 * i], wr[i].x, acc0);
-                acc1 = mfma16x16x4(xa[2 * i], wr[i].y, acc1);
-                acc0 = mfma16x16x4(xa[2 * i + 1], wr[i].z, acc0);
-                acc1 = mfma16x16x4(xa[2 * i + 1], wr[i].w, acc1);
+                if constexpr (N16) {
+                    acc0 = mfma16x16x4(xa[2 * i], wr[i].x, acc0);
+                    acc0 = mfma16x16x4(xa[2 * i + 1], wr[i].y, acc0);
+                } else {
+                    acc0 = mfma16x16x4(xa[2 * i], wr[i].x, acc0);
+                    acc1 = mfma16x16x4(xa[2 * i], wr[i].y, acc1);
+                    acc0 = mfma16x16x4(xa[2 * i + 1], wr[i].z, acc0);
+                    acc1 = mfma16x16x4(xa[2 * i + 1], wr[i].w, acc1);
+                }
                 if (tap + 1 < KW) wr[i] = Wf[(int64_t)(pn + i) * 64];
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-    } else {
+    } else if constexpr (!N16) {
     int k0 = 8 * p_beg + q;
     int ci = k0 / KW, tap = k0 - ci * KW;
     auto next4 = [&]() {  // k += 4
@@ -608,8 +621,8 @@ __global__ __launch_bounds__(CS_THREADS) void conv_small_kernel(const ConvArgs a
     __syncthreads();
     const int ld = a.out_ld ? a.out_ld : a.Cout;
     const int rtm = a.res_tmax ? a.res_tmax : a.Tmax;
-    for (int e = tid; e < CS_BM * CS_BN; e += CS_THREADS) {
-        const int tl = e / CS_BN, cl = e % CS_BN, t = t0 + tl, co = c0 + cl;
+    for (int e = tid; e < CS_BM * BN; e += CS_THREADS) {
+        const int tl = e / BN, cl = e % BN, t = t0 + tl, co = c0 + cl;
         if (t >= Tb || co >= a.Cout) continue;
         const int j = cl >> 4, src_lane = (tl >> 2) * 16 + (cl & 15), idx = src_lane * 4 + (tl & 3);
         float sum = red[j * 256 + idx];  // the waves' partial tiles in wave order
@@ -633,13 +646,18 @@ bool launch_small(const ConvArgs& a, int B, int frames_hint, hipStream_t s, hipE
         return false;
     const int Tt = a.Ttile ? a.Ttile : a.Tmax;
     const size_t smem = sizeof(float) * std::max((size_t)(CS_BM + KW - 1) * (a.Cin + 1), (size_t)2 * 256 * CS_WAVES);
-    const dim3 grid(((Tt + CS_BM - 1) / CS_BM) * (a.co_pad / CS_BN) * B);
-    if (a.wf_tap && a.Cin == CS_TAP_CIN)
-        hipLaunchKernelGGL((conv_small_kernel<KW, true>), grid, dim3(CS_THREADS), smem, s, a);
+    const int tiles = ((Tt + CS_BM - 1) / CS_BM) * B;
+    const dim3 grid(tiles * (a.co_pad / CS_BN));
+    // 16-channel tiles while the 32-channel grid leaves CUs idle (TTS_CONV_N16: that grid bound)
+    static const int n16_max = getenv("TTS_CONV_N16") ? atoi(getenv("TTS_CONV_N16")) : 128;
+    if (a.wf_tap && a.Cin == CS_TAP_CIN && a.Wf16 && (int)grid.x <= n16_max)
+        hipLaunchKernelGGL((conv_small_kernel<KW, true, true>), dim3(tiles * (a.co_pad / 16)), dim3(CS_THREADS), smem, s, a);
+    else if (a.wf_tap && a.Cin == CS_TAP_CIN)
+        hipLaunchKernelGGL((conv_small_kernel<KW, true, false>), grid, dim3(CS_THREADS), smem, s, a);
     else if (a.wf_tap)
         return false;  // (tap-major weights for another Cin: never packed so, conv_pack_frag_tap refuses)
     else
-        hipLaunchKernelGGL((conv_small_kernel<KW, false>), grid, dim3(CS_THREADS), smem, s, a);
+        hipLaunchKernelGGL((conv_small_kernel<KW, false, false>), grid, dim3(CS_THREADS), smem, s, a);
     *err = hipGetLastError();
     return true;
 }
@@ -680,6 +698,22 @@ __global__ void conv_pack_frag_tap_kernel(const float* W, int Cin, int KW, int c
     const int p = rest % np, ct = rest / np;
     const int q = lane >> 4, r = lane & 15;
     const int kt = 8 * p + 4 * (e >> 1) + q, co = 32 * ct + 16 * (e & 1) + r;
+    const int tap = kt / Cin, ci = kt - tap * Cin;
+    out[i] = W[(int64_t)(ci * KW + tap) * co_pad + co];
+}
+
+// the same tap-major order for 16-column tiles: [co_pad / 16][K / 8][64 lanes][2], lane (q, r) of
+// pair p holding W[8p + q][16ct + r], W[8p + 4 + q][16ct + r] (k' = tap Cin + ci)
+__global__ void conv_pack_frag_tap16_kernel(const float* W, int Cin, int KW, int co_pad, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int K = Cin * KW;
+    if (i >= (int64_t)K * co_pad) return;
+    const int e = i & 1, lane = (i >> 1) & 63;
+    const int64_t rest = i >> 7;
+    const int np = K >> 3;
+    const int p = rest % np, ct = rest / np;
+    const int q = lane >> 4, r = lane & 15;
+    const int kt = 8 * p + 4 * e + q, co = 16 * ct + r;
     const int tap = kt / Cin, ci = kt - tap * Cin;
     out[i] = W[(int64_t)(ci * KW + tap) * co_pad + co];
 }
@@ -816,6 +850,13 @@ hipError_t conv_pack_frag_tap(const float* W, int Cin, int KW, int co_pad, float
     const int64_t total = (int64_t)Cin * KW * co_pad;
     hipLaunchKernelGGL(conv_pack_frag_tap_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, Cin, KW, co_pad,
                        out);
+    return hipGetLastError();
+}
+hipError_t conv_pack_frag_tap16(const float* W, int Cin, int KW, int co_pad, float* out, hipStream_t s) {
+    if (Cin != CS_TAP_CIN || (co_pad % CS_BN)) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)Cin * KW * co_pad;
+    hipLaunchKernelGGL(conv_pack_frag_tap16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, Cin, KW,
+                       co_pad, out);
     return hipGetLastError();
 }
 bool conv_frag_tap_ok(int Cin) { return Cin == CS_TAP_CIN; }

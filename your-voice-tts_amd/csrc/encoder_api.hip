@@ -38,6 +38,7 @@ struct tts_encoder {
     float *Wc[3] = {}, *sc[3] = {}, *sh[3] = {};
     float *Wp = nullptr, *bp = nullptr;  // projection [512][1][2048], bias [2048]
     float *Wcf[3] = {}, *Wpf = nullptr;  // fragment-order copies (conv_pack_frag): small-batch conv kernel
+    float* Wcf16[3] = {};                // ... in its 16-channel order (conv_pack_frag_tap16), or null
     float* Whh = nullptr;                // packed [2 directions][64 tiles][16 chunks][64][4]
     int *ids = nullptr, *T = nullptr;
     float *act0 = nullptr, *act1 = nullptr, *xi = nullptr, *h = nullptr, *c = nullptr, *out = nullptr;
@@ -93,6 +94,7 @@ tts_status enqueue_encoder(tts_encoder* e, int B, int Lmax, int frames, hipStrea
         a.out = bufs[l & 1];
         a.W = e->Wc[l];
         a.Wf = e->Wcf[l];
+        a.Wf16 = e->Wcf16[l];
         a.wf_tap = conv_frag_tap_ok(EDIM) ? 1 : 0;
         a.scale = e->sc[l];
         a.shift = e->sh[l];
@@ -260,6 +262,10 @@ tts_status tts_encoder_create(const tts_tensor* tensors, int n_tensors, int max_
         CK(emalloc(e, &e->Wcf[l], (size_t)EDIM * 5 * EDIM));
         HK(conv_frag_tap_ok(EDIM) ? conv_pack_frag_tap(e->Wc[l], EDIM, 5, EDIM, e->Wcf[l], s)
                                   : conv_pack_frag(e->Wc[l], EDIM * 5, EDIM, e->Wcf[l], s));
+        if (conv_frag_tap_ok(EDIM)) {
+            CK(emalloc(e, &e->Wcf16[l], (size_t)EDIM * 5 * EDIM));
+            HK(conv_pack_frag_tap16(e->Wc[l], EDIM, 5, EDIM, e->Wcf16[l], s));
+        }
         HK(fold_bn(bias, g, be, mu, var, EDIM, 1e-5f, e->sc[l], e->sh[l], s));
     }
     CK(emalloc(e, &e->Wp, (size_t)EDIM * 2 * EG));

@@ -17,6 +17,7 @@ struct tts_postnet {
     float* W[5] = {};
     float* Wf[5] = {};  // fragment-order copies (conv_pack_frag): the small-batch conv kernel
     int wf_tap[5] = {};  // ... in the tap-major order of its Cin = 512 form (conv_pack_frag_tap)
+    float* Wf16[5] = {};  // ... and its 16-channel order (conv_pack_frag_tap16) for those layers
     float* scale[5] = {};
     float* shift[5] = {};
     float* buf[2] = {};
@@ -33,6 +34,7 @@ void tts_postnet_destroy(tts_postnet* p) {
     for (int i = 0; i < 5; ++i) {
         if (p->W[i]) (void)hipFree(p->W[i]);
         if (p->Wf[i]) (void)hipFree(p->Wf[i]);
+        if (p->Wf16[i]) (void)hipFree(p->Wf16[i]);
         if (p->scale[i]) (void)hipFree(p->scale[i]);
         if (p->shift[i]) (void)hipFree(p->shift[i]);
     }
@@ -84,6 +86,10 @@ tts_status tts_postnet_create(const tts_tensor* tensors, int n_tensors, int n_me
         if (e == hipSuccess)
             e = p->wf_tap[l] ? conv_pack_frag_tap(p->W[l], ci, 5, p->co_pad[l], p->Wf[l], s)
                              : conv_pack_frag(p->W[l], ci * 5, p->co_pad[l], p->Wf[l], s);
+        if (e == hipSuccess && p->wf_tap[l]) {
+            e = hipMalloc(&p->Wf16[l], nw * 4);
+            if (e == hipSuccess) e = conv_pack_frag_tap16(p->W[l], ci, 5, p->co_pad[l], p->Wf16[l], s);
+        }
         if (e == hipSuccess) e = fold_bn(bias, g, be, mu, var, co, 1e-5f, p->scale[l], p->shift[l], s);
         if (e != hipSuccess) { tts_postnet_destroy(p); return hip_fail(e, "postnet pack", __FILE__, __LINE__); }
     }
@@ -152,6 +158,7 @@ tts_status postnet_run_dev(tts_postnet* p, const float* mel, int mel_tmax, const
         a.W = p->W[l];
         a.Wf = p->Wf[l];
         a.wf_tap = p->wf_tap[l];
+        a.Wf16 = p->Wf16[l];
         a.scale = p->scale[l];
         a.shift = p->shift[l];
         a.resid = l == 4 ? mel : nullptr;
