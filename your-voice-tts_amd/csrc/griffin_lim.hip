@@ -1519,6 +1519,86 @@ __global__ void gl_ola_kernel(const FinArgs a) {
     a.y[(int64_t)b * a.Nmax + p] = bad ? __builtin_nanf("") : yv;
 }
 
+// gl_ola_kernel<frame_t> with OLA_R samples per thread (stride 256) and every contributor load
+// (and window sum-square load) of the thread issued before the first sum: at one sample per
+// thread a wave held ~1.3 KB of loads in flight, and the launch ran at ~2.9 TB/s (latency-bound by
+// bytes in flight; configs[4]: 442 MB per launch).  Per sample the same loads and the same
+// double-rounded sum order as gl_ola_kernel: bitwise equal.  Needs the unrolled geometry
+// (ola_multi_ok).
+constexpr int OLA_R = 4;
+__device__ __forceinline__ int div_small(int n, int d, float rd) {  // floor(n / d), 0 <= n < 2^24
+    int qt = (int)((float)n * rd);
+    const int r = n - qt * d;
+    qt += r >= d ? 1 : 0;
+    qt -= r < 0 ? 1 : 0;
+    return qt;
+}
+__global__ __launch_bounds__(256) void gl_ola_multi_kernel(const FinArgs a) {
+    const int b = blockIdx.y;
+    const int Fb = a.F[b];
+    const Geo& g = a.g;
+    const int N = g.hop * (Fb - 1);
+    const int p0 = blockIdx.x * (256 * OLA_R) + threadIdx.x;
+    if (a.host_status && p0 == 0 && b == 0) {
+        __hip_atomic_store(a.host_status, *a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.host_seq) release_word_system(a.host_seq, a.seq);
+    }
+    if (p0 >= N) return;
+    const bool bad = a.status && *a.status != 0;
+    const float* fr = static_cast<const float*>(a.frames) + (int64_t)b * a.Fmax * g.winp;
+    const float rhop = __builtin_amdgcn_rcpf((float)g.hop);
+    const int step = g.winp - g.hop;  // frame i's element for sample q: i (winp - hop) + q - fb
+    float fv[OLA_R][OLA_MAX], wv[OLA_R];
+    int ilo[OLA_R], ihi[OLA_R];
+#pragma unroll
+    for (int j = 0; j < OLA_R; ++j) {
+        const int q = p0 + 256 * j + NFFT / 2, u = q - g.woff;
+        const int ihu = div_small(u, g.hop, rhop);
+        int lo = u - g.win + 1;
+        const bool full = lo >= 1 && ihu <= Fb - 1;
+        lo = lo <= 0 ? 0 : div_small(lo + g.hop - 1, g.hop, rhop);
+        const int hi = p0 + 256 * j < N ? min(ihu, Fb - 1) : -1;
+        ilo[j] = lo;
+        ihi[j] = hi;
+        const int o = lo * step + q - g.fb;
+#pragma unroll
+        for (int k = 0; k < OLA_MAX; ++k) fv[j][k] = lo + k <= hi ? fr[o + k * step] : 0.f;
+        wv[j] = full && hi >= 0 ? a.wssp[u - ihu * g.hop] : -1.f;  // -1: sum the window here
+    }
+#pragma unroll
+    for (int j = 0; j < OLA_R; ++j) {
+        const int p = p0 + 256 * j;
+        if (p >= N) break;
+        const int q = p + NFFT / 2;
+        float y = 0.f;
+#pragma unroll
+        for (int k = 0; k < OLA_MAX; ++k) y = (float)((double)y + (double)fv[j][k]);
+        float wss = wv[j];
+        if (wss < 0.f) {
+            wss = 0.f;
+            for (int i = ilo[j]; i <= ihi[j]; ++i) wss = (float)((double)wss + a.c.win2[q - i * g.hop]);
+        }
+        const float yv = wss > 1.17549435e-38f ? y / wss : y;
+        a.y[(int64_t)b * a.Nmax + p] = bad ? __builtin_nanf("") : yv;
+    }
+}
+bool ola_multi_ok(const Geo& g, int64_t Nmax) {
+    return (g.win + g.hop - 1) / g.hop <= OLA_MAX && g.woff <= NFFT / 2 && Nmax + NFFT < (1 << 24) &&
+           (Nmax / g.hop + 2) * (int64_t)g.winp < (1ll << 31);  // (int frame offsets)
+}
+// the overlap-add of float32 frames (the fused / batched loops' slots) into the signal
+void launch_ola_frames(const FinArgs& f, hipStream_t s) {
+    static const bool single = [] {  // measurement: TTS_GL_OLA_SINGLE=1, one sample per thread
+        const char* v = getenv("TTS_GL_OLA_SINGLE");
+        return v && v[0] == '1';
+    }();
+    if (!single && ola_multi_ok(f.g, f.Nmax))
+        hipLaunchKernelGGL(gl_ola_multi_kernel, dim3((unsigned)((f.Nmax + 256 * OLA_R - 1) / (256 * OLA_R)), f.B),
+                           dim3(256), 0, s, f);
+    else
+        hipLaunchKernelGGL(gl_ola_kernel<frame_t>, dim3((unsigned)((f.Nmax + 255) / 256), f.B), dim3(256), 0, s, f);
+}
+
 // y[n] = x[n] + c*y[n-1] in float64 (scipy.signal.lfilter([1], [1, -c], x), utils/audio.py:133-136).
 // Chunk-parallel: workgroup (chunk i, sentence b) writes y[i*chunk, (i+1)*chunk) and starts its scan
 // `look` samples earlier from y = 0: the state it misses is c^look * y, below 1e-22 of |y| (the host
@@ -2256,7 +2336,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                 } else {
                     FinArgs o = fa;
                     o.frames = slot(i);
-                    hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, o);
+                    launch_ola_frames(o, s);
                     if (g->wave)
                         hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
                     else
@@ -2284,7 +2364,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         g->seq_stream = s;
     }
     if (persistent_ran) hipLaunchKernelGGL(gl_ola_kernel<gran_t>, ogrid, oblock, 0, s, fa);
-    else hipLaunchKernelGGL(gl_ola_kernel<frame_t>, ogrid, oblock, 0, s, fa);
+    else launch_ola_frames(fa, s);
     fa.status = nullptr;
     fa.host_status = nullptr;
     fa.host_seq = nullptr;
@@ -2355,7 +2435,7 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
         a.prev = f.frames;
         TTS_HIP(hipEventRecord(ev[0], s));
         if (!g->last_fused)
-            hipLaunchKernelGGL(gl_ola_kernel<frame_t>, dim3((f.Nmax + 255) / 256, f.B), dim3(256), 0, s, f);
+            launch_ola_frames(f, s);
         TTS_HIP(hipGetLastError());
         TTS_HIP(hipEventRecord(ev[1], s));
         if (g->last_fused)
