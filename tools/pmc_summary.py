@@ -43,7 +43,7 @@ LABELS = [
     (r"conv_kernel<1", "conv1"),
     (r"gl_magnitude_kernel", "gl_magnitude"),
     (r"preemph_scan_kernel", "preemph"),
-    (r"gl_ola_kernel", "gl_ola"),
+    (r"gl_ola_kernel|gl_ola_multi_kernel", "gl_ola"),
     (r"project_inputs_kernel", "project_inputs"),
     (r"resident_decoder_kernel<(?:false|true), true>", "resident_decoder_general"),
     (r"resident_decoder_kernel", "resident_decoder"),
