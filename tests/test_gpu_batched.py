@@ -13,7 +13,7 @@ from oracle.tacotron2_oracle import Tacotron2Oracle
 
 pytestmark = pytest.mark.gpu
 WAV_RTOL = 1e-4
-MEL_RTOL = 4e-6  # model half: 10x the measured worst case (profiles/r05_parity_report.jsonl)
+MEL_RTOL = 4e-6  # model half: 10x the measured worst case (profiles/r05f_parity_report.jsonl)
 
 
 def _t2(max_batch=64, **over):

@@ -21,7 +21,7 @@ from conftest import GOLDEN, golden, golden_flags, load_pkg, rel_rms
 
 pytestmark = pytest.mark.gpu
 
-MEL_RTOL = 4e-6  # 10x the worst measured over every fixture and path (profiles/r05_parity_report.jsonl)
+MEL_RTOL = 4e-6  # 10x the worst measured over every fixture and path (profiles/r05f_parity_report.jsonl)
 ALIGN_ATOL = 4e-6
 SAME_RTOL = 1e-5  # resident vs multi-launch: the same fp32 step, different reduction orders
 SAME_ATOL = 1e-5

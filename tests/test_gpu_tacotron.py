@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 TACO_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "gst_*.npz")) +
                     glob.glob(os.path.join(GOLDEN, "taco_*.npz")))
-RTOL = 4e-6  # 10x the worst measured (profiles/r05_parity_report.jsonl: mel / linear <= 3e-7)
+RTOL = 4e-6  # 10x the worst measured (profiles/r05f_parity_report.jsonl: mel / linear <= 3e-7)
 ATOL = 4e-6
 
 
