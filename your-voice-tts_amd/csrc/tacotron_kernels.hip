@@ -46,36 +46,26 @@ __global__ __launch_bounds__(GRU_THREADS) void bigru_kernel(const GruSeqArgs a) 
     for (int s = 0; s < Tb; ++s) {
         const int cur = s & 1;
         const float4* h4 = reinterpret_cast<const float4*>(&hs[cur][half * 64]);
-        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        f2v p0 = f2v{0.f, 0.f}, p1 = p0, p2 = p0, p3 = p0;
 #pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-            const float4 h0 = h4[i], h1 = h4[i + 1], h2 = h4[i + 2], h3 = h4[i + 3];
-            c0 = fmaf(w[i].x, h0.x, c0);
-            c0 = fmaf(w[i].y, h0.y, c0);
-            c0 = fmaf(w[i].z, h0.z, c0);
-            c0 = fmaf(w[i].w, h0.w, c0);
-            c1 = fmaf(w[i + 1].x, h1.x, c1);
-            c1 = fmaf(w[i + 1].y, h1.y, c1);
-            c1 = fmaf(w[i + 1].z, h1.z, c1);
-            c1 = fmaf(w[i + 1].w, h1.w, c1);
-            c2 = fmaf(w[i + 2].x, h2.x, c2);
-            c2 = fmaf(w[i + 2].y, h2.y, c2);
-            c2 = fmaf(w[i + 2].z, h2.z, c2);
-            c2 = fmaf(w[i + 2].w, h2.w, c2);
-            c3 = fmaf(w[i + 3].x, h3.x, c3);
-            c3 = fmaf(w[i + 3].y, h3.y, c3);
-            c3 = fmaf(w[i + 3].z, h3.z, c3);
-            c3 = fmaf(w[i + 3].w, h3.w, c3);
+        for (int i = 0; i < 16; i += 2) {
+            const float4 h0 = h4[i], h1 = h4[i + 1];
+            p0 = __builtin_elementwise_fma(f2v{w[i].x, w[i].y}, f2v{h0.x, h0.y}, p0);
+            p1 = __builtin_elementwise_fma(f2v{w[i].z, w[i].w}, f2v{h0.z, h0.w}, p1);
+            p2 = __builtin_elementwise_fma(f2v{w[i + 1].x, w[i + 1].y}, f2v{h1.x, h1.y}, p2);
+            p3 = __builtin_elementwise_fma(f2v{w[i + 1].z, w[i + 1].w}, f2v{h1.z, h1.w}, p3);
         }
+        const float c0 = p0.x + p0.y, c1 = p1.x + p1.y, c2 = p2.x + p2.y, c3 = p3.x + p3.y;
         float g = (c0 + c1) + (c2 + c3);
-        g += __shfl_xor(g, 1, 64);
+        g += dpp_move<0xB1, 0xf>(g, 0.f);  // quad_perm [1,0,3,2]: the row's other half
         if (half == 0) gs[row] = g + bh;
         __syncthreads();
         if (tid < GRU_H) {
             const int pos = dir ? Tb - 1 - s : s;
-            const float r = sigmoidf_(xr + gs[tid]);
-            const float z = sigmoidf_(xz + gs[GRU_H + tid]);
-            const float n = tanhf(xn + r * gs[2 * GRU_H + tid]);
+            const float r = sigmoid_cell(xr + gs[tid]);
+            const float z = sigmoid_cell(xz + gs[GRU_H + tid]);
+            const float n = tanh_cell(xn + r * gs[2 * GRU_H + tid]);
             const float h = (hs[cur][tid] - n) * z + n;
             hs[cur ^ 1][tid] = h;
             if (a.out) a.out[((int64_t)b * a.Tmax + pos) * a.out_ld + dir * GRU_H + tid] = (h + ad1) + ad2;
