@@ -290,3 +290,33 @@ def test_overlap_add_launch_bitwise_vs_in_kernel_gather(audio_cfg, monkeypatch):
     wav_f = ap_f.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
     assert ap_f.last_gl_path() == "fused"
     assert np.array_equal(wav, wav_f)
+
+
+def test_griffin_lim_wave_kernel_initial_istft_vs_oracle(audio_cfg, monkeypatch):
+    """The batched loops' initial iSTFT on the one-wave-per-frame layout (gl_iter_wave_kernel<true>):
+    with zero iterations the waveform is that launch's output alone (plus the overlap-add), so it is
+    held much tighter than after 60 iterations (no Griffin-Lim amplification): vs the oracle's
+    istft(|S| exp(2 pi i U)) and vs the 256-thread block kernels (TTS_GL_WAVE=0)."""
+    audio = load_pkg("audio")
+    cfg = {**audio_cfg, "griffin_lim_iters": 0}
+    o = AudioOracle(**cfg)
+    rng = np.random.Generator(np.random.PCG64(13))
+    Fs = [3, 150, 33, 220, 64, 7]
+    Fmax = max(Fs)
+    assert len(Fs) * Fmax > 1024  # the unfused (batched) loop
+    mel = np.zeros((len(Fs), Fmax, 80), np.float32)
+    pu = np.zeros((len(Fs), 1025, Fmax))
+    for b, F in enumerate(Fs):
+        mel[b, :F] = rng.uniform(0, 1, size=(F, 80))
+        pu[b, :, :F] = rng.uniform(0, 1, size=(1025, F))
+    mel_d = torch.from_numpy(mel).cuda()
+    ap = audio.AudioProcessor(**cfg)
+    wav = ap.griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    assert ap.last_gl_path() == "unfused"
+    monkeypatch.setenv("TTS_GL_WAVE", "0")
+    wav_block = audio.AudioProcessor(**cfg).griffin_lim_batch(mel_d, Fs, phase_u=pu).cpu().numpy()
+    for b, F in enumerate(Fs):
+        n = ap.hop_length * (F - 1)
+        ref = o.inv_mel_spectrogram(mel[b, :F].T, pu[b, :, :F])
+        assert rel_rms(wav[b, :n], ref) < 1e-6, (b, F)
+        assert rel_rms(wav[b, :n], wav_block[b, :n]) < 1e-6, (b, F)

@@ -919,6 +919,10 @@ __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, i
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, 0, 0);
 }
 
+// INIT: the initial iSTFT of exp(2 pi i U) |S| (utils/audio.py:183) on the same wave layout: no
+// STFT, the bin pairs' X formed from the phases, then the inverse half as below (the batched
+// loops' first launch; the 256-thread gl_iter_kernel<true> took ~1.5x a wave iteration).
+template <bool INIT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void gl_iter_wave_kernel(const IterArgs a) {
     const int b = blockIdx.y;
     const int f = xcd_remap(blockIdx.x, gridDim.x);
@@ -938,84 +942,110 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // c_{r+1} = 2 cos(theta) c_r - c_{r-1} (one fma per sample from two seeds per parity, a few
     // ulp over 16 steps, instead of 16 window-table loads).  Outside the support the sample is
     // exactly 0: the support-sized y range reads 0 there, or (reflected frames) a select.
-    const int N = g.hop * (Fb - 1);
-    const int base = f * g.hop - NFFT / 2;
     const double K = a.wrot;
     double2 v[16];
-    float y0[16], y1[16];
-    const bool interior = base + g.woff >= 0 && base + g.woff + g.win <= N;
-    if (interior) {  // the support needs no reflection
-        const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax + base + g.woff, (unsigned)g.win * 4);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int s = 2 * (L + 64 * r) - g.woff;
-            y0[r] = buf_f32(rY, s * 4);
-            y1[r] = buf_f32(rY, (s + 1) * 4);
-        }
-    } else {
-        const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax, (unsigned)N * 4);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int s = 2 * (L + 64 * r);
-            const bool i0 = s >= g.woff && s < g.woff + g.win, i1 = s + 1 >= g.woff && s + 1 < g.woff + g.win;
-            y0[r] = i0 ? buf_f32(rY, reflect_idx(base + s, N) * 4) : 0.f;
-            y1[r] = i1 ? buf_f32(rY, reflect_idx(base + s + 1, N) * 4) : 0.f;
-        }
-    }
-    {
-        const double2 s0 = buf_c64(rC, 16 * L, 0), s1 = buf_c64(rC, 16 * L, 1024);  // (c_0, c_1) per parity
-        double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            v[r] = double2{fma(-0.5, a0, 0.5) * (double)y0[r], fma(-0.5, b0, 0.5) * (double)y1[r]};
-            const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
-            a0 = a1;
-            a1 = a2;
-            b0 = b1;
-            b1 = b2;
-        }
-    }
-    t2[L] = buf_c64(rP, 16 * L, 0);  // first LDS use: ordered before the reads by the FFT's barriers
-    wave_fft1024<false>(v, lds, t2, rT, L);
-    // ---- Z to LDS in natural (swizzled) order, real parts then imaginary parts; bin pairs
-    // (k, 1024 - k), k = L + 64 m, m < 8, plus k = 512.  sig() only permutes bits 2-3 by bits 4-5,
-    // so every address below is one per-lane base plus a multiple of 64 slots: Z[k] at zb + 64 m,
-    // Z[1024 - k] at mb + 64 (15 - m) (for lane 0, m = 0 that is the spare slot 1024: Z[0] is taken
-    // from its own Z[k] read, and the partner store that pair does not have lands there).  Every
-    // LDS store is unconditional: a divergent store makes the compiler branch around the partner's
-    // computation and spill.
     const int r3 = L & 3, K2 = L >> 2;
-    const int wb = wv_sig(16 * r3 + K2);              // this lane's output Z[256 q1 + 64 j + wb']
     const int zb = wv_sig(L);                         // Z[L + 64 m]
     const int mb = wv_sig((64 - L) & 63) + (L == 0 ? 64 : 0);
-    double zkr[8], zmr[8];
+    double zkr[8], zmr[8], z512r = 0.0, z512i = 0.0;
+    t2[L] = buf_c64(rP, 16 * L, 0);  // first LDS use: ordered before the reads by the FFT's barriers
+    if constexpr (!INIT) {
+        const int N = g.hop * (Fb - 1);
+        const int base = f * g.hop - NFFT / 2;
+        float y0[16], y1[16];
+        const bool interior = base + g.woff >= 0 && base + g.woff + g.win <= N;
+        if (interior) {  // the support needs no reflection
+            const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax + base + g.woff, (unsigned)g.win * 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+            for (int r = 0; r < 16; ++r) {
+                const int s = 2 * (L + 64 * r) - g.woff;
+                y0[r] = buf_f32(rY, s * 4);
+                y1[r] = buf_f32(rY, (s + 1) * 4);
+            }
+        } else {
+            const auto rY = buf_rsrc(a.y + (int64_t)b * a.Nmax, (unsigned)N * 4);
 #pragma unroll
-        for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].x;
-    __syncthreads();
+            for (int r = 0; r < 16; ++r) {
+                const int s = 2 * (L + 64 * r);
+                const bool i0 = s >= g.woff && s < g.woff + g.win, i1 = s + 1 >= g.woff && s + 1 < g.woff + g.win;
+                y0[r] = i0 ? buf_f32(rY, reflect_idx(base + s, N) * 4) : 0.f;
+                y1[r] = i1 ? buf_f32(rY, reflect_idx(base + s + 1, N) * 4) : 0.f;
+            }
+        }
+        {
+            const double2 s0 = buf_c64(rC, 16 * L, 0), s1 = buf_c64(rC, 16 * L, 1024);  // (c_0, c_1) per parity
+            double a0 = s0.x, a1 = s0.y, b0 = s1.x, b1 = s1.y;
 #pragma unroll
-    for (int m = 0; m < 8; ++m) {
-        zkr[m] = lds[zb + 64 * m];
-        zmr[m] = lds[mb + 64 * (15 - m)];
+            for (int r = 0; r < 16; ++r) {
+                v[r] = double2{fma(-0.5, a0, 0.5) * (double)y0[r], fma(-0.5, b0, 0.5) * (double)y1[r]};
+                const double a2 = fma(K, a1, -a0), b2 = fma(K, b1, -b0);
+                a0 = a1;
+                a1 = a2;
+                b0 = b1;
+                b1 = b2;
+            }
+        }
+        wave_fft1024<false>(v, lds, t2, rT, L);
+        // ---- Z to LDS in natural (swizzled) order, real parts then imaginary parts; bin pairs
+        // (k, 1024 - k), k = L + 64 m, m < 8, plus k = 512.  sig() only permutes bits 2-3 by bits 4-5,
+        // so every address below is one per-lane base plus a multiple of 64 slots: Z[k] at zb + 64 m,
+        // Z[1024 - k] at mb + 64 (15 - m) (for lane 0, m = 0 that is the spare slot 1024: Z[0] is taken
+        // from its own Z[k] read, and the partner store that pair does not have lands there).  Every
+        // LDS store is unconditional: a divergent store makes the compiler branch around the partner's
+        // computation and spill.
+        const int wb = wv_sig(16 * r3 + K2);              // this lane's output Z[256 q1 + 64 j + wb']
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].x;
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            zkr[m] = lds[zb + 64 * m];
+            zmr[m] = lds[mb + 64 * (15 - m)];
+        }
+        if (L == 0) zmr[0] = zkr[0];
+        z512r = lds[512];  // sig(512) = 512
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].y;
+        __syncthreads();
+        z512i = lds[512];
     }
-    if (L == 0) zmr[0] = zkr[0];
-    const double z512r = lds[512];  // sig(512) = 512
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q1 = 0; q1 < 4; ++q1) lds[wb + 256 * q1 + 64 * j] = v[4 * j + q1].y;
-    __syncthreads();
-    const double z512i = lds[512];
     // One pair at a time (its imaginary parts, |S| and split twiddle read one pair ahead).  The
     // partner bin's pre-split value goes to lane (64 - L) & 63, register 15 - m (16 - m on lane 0),
     // i.e. to the slot of Z[1024 - k]: a slot only this lane reads (512 is read by one instruction
     // of all lanes and rewritten by lane 0 only), so it is stored in place with no barrier; its
-    // real part at once, its imaginary part after the next barrier.
+    // real part at once, its imaginary part after the next barrier.  INIT: X from the phases.
     double vmy[8];
-    double zki = lds[zb], zmi = lds[mb + 64 * 15];
-    if (L == 0) zmi = zki;
+    double zki = 0.0, zmi = 0.0;
+    if constexpr (!INIT) {
+        zki = lds[zb];
+        zmi = lds[mb + 64 * 15];
+        if (L == 0) zmi = zki;
+    }
+    // INIT: the phases U of the lane's bins (k, 1024 - k per pair, then 512), all issued up front
+    double uk[8], um[8], u512 = 0.0;
+    auto phase_of = [&](int k) -> double {
+        return a.phase_u ? a.phase_u[((int64_t)b * NB + k) * a.Fmax + f]
+                         : hash_uniform(a.seed, ((unsigned long long)b * NB + k) * 1048576ull + f);
+    };
+    // exp(2 pi i U) |S| with .real at DC and Nyquist (gl_iter_kernel's init_bin)
+    auto phase_bin = [&](int k, double sv, double u) -> double2 {
+        double sn, cs;
+        sincospi(2.0 * u, &sn, &cs);
+        return double2{sv * cs, (k == 0 || k == NB - 1) ? 0.0 : sv * sn};
+    };
+    if constexpr (INIT) {
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+            uk[m] = phase_of(L + 64 * m);
+            um[m] = phase_of(NH - L - 64 * m);
+        }
+        u512 = phase_of(512);
+    }
     double sa = buf_f32(rS, 4 * L), sb = buf_f32(rS, 4 * (NH - L));
     // split twiddles t[k] = W2048^(L + 64 m) = W2048^L x W32^m (compile-time W32^m)
     const double2 tL = buf_c64(rT, 16 * L, 0);
@@ -1027,8 +1057,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
         double zki_n = 0.0, zmi_n = 0.0, sa_n, sb_n = 0.0;
         double2 tk_n = double2{0.0, 0.0};
         if (m < 7) {
-            zki_n = lds[zb + 64 * (m + 1)];
-            zmi_n = lds[mb + 64 * (14 - m)];
+            if constexpr (!INIT) {
+                zki_n = lds[zb + 64 * (m + 1)];
+                zmi_n = lds[mb + 64 * (14 - m)];
+            }
             sa_n = buf_f32s(rS, 4 * L, 256 * (m + 1));
             sb_n = buf_f32(rS, 4 * (NH - k - 64));
             tk_n = cmulf(tL, double2{kW32[m + 1][0], kW32[m + 1][1]});
@@ -1036,12 +1068,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
             sa_n = buf_f32s(rS, 0, 2048);  // k = 512
             tk_n = buf_c64(rT, 0, 8192);  // k = 512
         }
-        // 2E = Z[k] + conj Z[N-k], 2O = -i (Z[k] - conj Z[N-k]): X[k] = E + t O up to the factor 2
-        const double2 E = double2{zkr[m] + zmr[m], zki - zmi};
-        const double2 O = double2{zki + zmi, zmr[m] - zkr[m]};
-        const double2 tO = cmulf(O, tk);
-        double2 xk = unit_phase(cadd(E, tO), sa);         // X[k]
-        double2 xm = unit_phase(cconj(csub(E, tO)), sb);  // X[1024 - k]
+        double2 xk, xm;
+        if constexpr (INIT) {
+            xk = phase_bin(k, sa, uk[m]);
+            xm = phase_bin(NH - k, sb, um[m]);
+        } else {
+            // 2E = Z[k] + conj Z[N-k], 2O = -i (Z[k] - conj Z[N-k]): X[k] = E + t O up to the factor 2
+            const double2 E = double2{zkr[m] + zmr[m], zki - zmi};
+            const double2 O = double2{zki + zmi, zmr[m] - zkr[m]};
+            const double2 tO = cmulf(O, tk);
+            xk = unit_phase(cadd(E, tO), sa);         // X[k]
+            xm = unit_phase(cconj(csub(E, tO)), sb);  // X[1024 - k]
+        }
         if ((L | m) == 0) {  // istft: .real of the Hermitian extension at DC and Nyquist
             xk.y = 0.0;
             xm.y = 0.0;
@@ -1063,7 +1101,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     __builtin_amdgcn_sched_barrier(0);
     double2 v512;
     {  // k = 512 pairs with itself: 2E = (2 Re Z, 0), 2O = (2 Im Z, 0)
-        const double2 x = unit_phase(double2{2.0 * z512r + 2.0 * z512i * tk.x, 2.0 * z512i * tk.y}, sa);
+        const double2 x = INIT ? phase_bin(512, sa, u512)
+                               : unit_phase(double2{2.0 * z512r + 2.0 * z512i * tk.x, 2.0 * z512i * tk.y}, sa);
         v512 = inv_presplit2(x, x, tk);
     }
     lds[512] = v512.x;  // the same value from every lane
@@ -2220,7 +2259,13 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
         ia.zero_status = g->pstatus;
     }
     const dim3 grid(Fmax, B), block(GL_THREADS);
+    static const bool wave_init = [] {  // measurement: TTS_GL_WAVE_INIT=0 keeps the block-kernel init
+        const char* v = getenv("TTS_GL_WAVE_INIT");
+        return !(v && v[0] == '0');
+    }();
     if (persistent) hipLaunchKernelGGL((gl_iter_kernel<true, false, gran_t>), grid, block, 0, s, ia);
+    else if (!fused && g->wave && wave_init)  // the batched loop's own layout for its first launch
+        hipLaunchKernelGGL(gl_iter_wave_kernel<true>, grid, dim3(64), 0, s, ia);
     else hipLaunchKernelGGL((gl_iter_kernel<true, false, frame_t>), grid, block, 0, s, ia);
     ia.zero_flags = nullptr;
     ia.zero_status = nullptr;
@@ -2338,7 +2383,7 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
                     o.frames = slot(i);
                     launch_ola_frames(o, s);
                     if (g->wave)
-                        hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
+                        hipLaunchKernelGGL(gl_iter_wave_kernel<false>, grid, dim3(64), 0, s, a);
                     else
                         hipLaunchKernelGGL((gl_iter_kernel<false, false, frame_t>), grid, block, 0, s, a);
                 }
@@ -2441,7 +2486,7 @@ tts_status tts_gl_profile(tts_gl* g, int reps, float* kernel_ms, int n_kernels) 
         if (g->last_fused)
             hipLaunchKernelGGL((gl_iter_kernel<false, true, frame_t>), grid, block, 0, s, a);
         else if (g->wave)
-            hipLaunchKernelGGL(gl_iter_wave_kernel, grid, dim3(64), 0, s, a);
+            hipLaunchKernelGGL(gl_iter_wave_kernel<false>, grid, dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL((gl_iter_kernel<false, false, frame_t>), grid, block, 0, s, a);
         TTS_HIP(hipGetLastError());
