@@ -1465,13 +1465,17 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
         // the line stays in the XCD's L2) when every consumer shares this XCD, else written through
         const unsigned nt = tag0 | (unsigned)(it + 1);
         const auto rD = buf_rsrc(dst, (unsigned)g.winp * 8);
+        // one 16-byte store per sample pair (2n, 2n + 1): two whole granules; a pair straddling an
+        // end of the support also writes the slot's sample outside it (never read)
 #pragma unroll
-        for (int i = 0; i < PN; ++i) {
-            const double zv = (i & 1) ? v[i >> 1].y : v[i >> 1].x;
-            const u32x2 gv = u32x2{__float_as_uint((float)(wi[i] * (zv * (1.0 / NH)))), nt};
+        for (int r = 0; r < PN / 2; ++r) {
+            const u32x4 gv = u32x4{__float_as_uint((float)(wi[2 * r] * (v[r].x * (1.0 / NH)))), nt,
+                                   __float_as_uint((float)(wi[2 * r + 1] * (v[r].y * (1.0 / NH)))), nt};
+            const int e = edge_sample(TWO ? tid_opaque() : tid, 2 * r);
+            const int off = e + 1 >= g.woff && e < g.woff + g.win ? (e - g.fb) * 8 : GL_OOB_OFF;
             // plain (workgroup-scope) store: the line stays in this XCD's L2; sc1: written through
-            if (local) __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff(i), 0, 0);
-            else __builtin_amdgcn_raw_buffer_store_b64(gv, rD, soff(i), 0, 0x10);
+            if (local) __builtin_amdgcn_raw_buffer_store_b128(gv, rD, off, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(gv, rD, off, 0, 0x10);
         }
         GL_PHASE(5)
     }
