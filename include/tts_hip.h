@@ -145,6 +145,10 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
  * attention + mask, sigmoid norm) on a GPU with >= 256 compute units; TTS_RESIDENT=0 in the
  * environment at tts_decoder_create disables it. */
 tts_status tts_decoder_last_path(tts_decoder* d, int* resident);
+/* The requests the resident decoder serves on this handle now: batches of at most *max_batch
+ * sentences of encoder length <= *max_len (both 0: the handle runs multi-launch only, e.g. after
+ * repeated placement failures).  Callers that split a request (Synthesizer.tts's dispatch) gate on it. */
+tts_status tts_decoder_resident_limits(tts_decoder* d, int* max_batch, int* max_len);
 
 /* Measurement only: re-runs the last resident batch-1 sentence with phase timers and returns the
  * mean microseconds per decoder step of each phase, us[0..15] on compute unit 0 and us[16..31] on
@@ -210,6 +214,29 @@ void tts_gl_destroy(tts_gl* g);
  *   wav     [dev]  fp64 [B][hop*(Fmax-1)]: sentence b fills its first hop*(F_b-1) samples */
 tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
                       const double* phase_u, uint64_t seed, int iters, double* wav, void* stream);
+
+/* numpy-stream initial phases.  The reference draws each sentence's initial Griffin-Lim phases
+ * with np.random.rand(*S.shape) from numpy's global legacy generator (utils/audio.py:183), sentence
+ * after sentence (server/synthesizer.py:145-158).  tts_gl_set_phase_state takes that generator's
+ * state (np.random.get_state(): MT19937 key[624] and position 0..624) and arms the handle: every
+ * following tts_gl_run with phase_u == NULL (and the runs of a tts_synth on this handle) draws its
+ * phases from it ON THE DEVICE, one [n_fft/2+1][F_b] draw per sentence in batch order, bitwise the
+ * values np.random.rand returns, and advances the state; key == NULL disarms (device-seeded phases
+ * again).  tts_gl_get_phase_state waits for the last draw and returns the state numpy would hold
+ * after the same draws (np.random.set_state it back).  tts_gl_draw_phases draws into phase_u [dev]
+ * fp64 [B][n_fft/2+1][Fmax] directly (F [host] int32 [B], 0 <= F[b] <= Fmax, B <= 1024). */
+tts_status tts_gl_set_phase_state(tts_gl* g, const uint32_t* key, int pos);
+tts_status tts_gl_get_phase_state(tts_gl* g, uint32_t* key, int* pos);
+tts_status tts_gl_draw_phases(tts_gl* g, const int32_t* F, int B, int Fmax, double* phase_u, void* stream);
+
+/* Synthesizer.tts's join + AudioProcessor.save_wav's int16 conversion (server/synthesizer.py:157-161,
+ * utils/audio.py:56-58), on the device: sentence b's first n[b] samples, each sentence followed by
+ * `gap` zeros (10000 in the reference), scaled by 32767 / max(0.01, peak) and truncated to int16, with
+ * numpy's float64 arithmetic (the bytes of the reference's wav).  peak < 0: max |y| over the request;
+ * peak >= 0: that value (a sharded request's all-ranks maximum).
+ *   wav [dev] fp64 [B][pitch]; n [host] int64 [B]; out [dev] int16 [sum(n[b] + gap)] */
+tts_status tts_gl_save_pcm16(tts_gl* g, const double* wav, int64_t pitch, const int64_t* n, int B, int gap,
+                             double peak, int16_t* out, void* stream);
 
 /* Mel analysis for GST style wavs: AudioProcessor.melspectrogram (utils/audio.py:146-152) as used by
  * compute_style_mel (utils/synthesis.py:28-35): pre-emphasis FIR, librosa 0.6.2 stft (float64 FFT,

@@ -14,7 +14,7 @@ HEADER = os.path.join(REPO, "include", "tts_hip.h")
 
 def header_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"\b(tts_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(tts_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_matches_binding_table():

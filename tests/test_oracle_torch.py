@@ -10,6 +10,9 @@ from conftest import GOLDEN, golden, golden_flags, rel_rms, weights_mod
 from oracle.tacotron2_torch import Tacotron2TorchCPU
 
 T2_CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "t2_*.npz")))
+# the 3000-step fixture (Synthesizer.tts()'s cap) pins the GPU path directly; the CPU restatements
+# take ~2 min on it (checked when it was made): TTS_SLOW_ORACLE=1 includes it here
+T2_CASES = [c for c in T2_CASES if not c.endswith("_cap3000") or os.environ.get("TTS_SLOW_ORACLE") == "1"]
 
 
 @pytest.mark.parametrize("case", T2_CASES)

@@ -25,11 +25,12 @@ EXPORTS = (
     "tts_encoder_create", "tts_encoder_destroy", "tts_encoder_run", "tts_encoder_run_state", "tts_encoder_last_path",
     "tts_encoder_add_speakers", "tts_synth_run_speakers",
     "tts_decoder_create", "tts_decoder_destroy", "tts_decoder_run", "tts_decoder_run_continue", "tts_decoder_run_teacher",
-    "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_phases", "tts_decoder_resident_trace",
+    "tts_decoder_last_timing", "tts_decoder_last_path", "tts_decoder_resident_limits", "tts_decoder_resident_phases", "tts_decoder_resident_trace",
     "tts_decoder_profile",
     "tts_postnet_create", "tts_postnet_destroy", "tts_postnet_run",
     "tts_gl_create", "tts_gl_destroy", "tts_gl_run", "tts_gl_last_timing", "tts_gl_last_path", "tts_gl_profile",
-    "tts_gl_set_mel_basis", "tts_gl_melspectrogram",
+    "tts_gl_set_mel_basis", "tts_gl_melspectrogram", "tts_gl_set_phase_state", "tts_gl_get_phase_state",
+    "tts_gl_draw_phases", "tts_gl_save_pcm16",
     "tts_synth_create", "tts_synth_destroy", "tts_synth_run", "tts_synth_sync",
     "tts_tacotron_create", "tts_tacotron_destroy", "tts_tacotron_encode", "tts_tacotron_decode",
     "tts_tacotron_postnet", "tts_tacotron_last_timing", "tts_tacotron_last_path", "tts_tacotron_resident_phases",
@@ -88,6 +89,7 @@ def _declare(lib):
                                             vp, vp, vp, vp]
     lib.tts_decoder_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     lib.tts_decoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_decoder_resident_limits.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     lib.tts_encoder_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     lib.tts_gl_last_path.argtypes = [vp, ctypes.POINTER(ctypes.c_int)]
     lib.tts_synth_sync.argtypes = [vp]
@@ -105,6 +107,12 @@ def _declare(lib):
     lib.tts_gl_set_mel_basis.argtypes = [vp, vp]
     lib.tts_gl_melspectrogram.argtypes = [vp, vp, I32P, ctypes.c_int, ctypes.c_int64, vp, ctypes.c_int, vp]
     lib.tts_gl_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    U32P = ctypes.POINTER(ctypes.c_uint32)
+    lib.tts_gl_set_phase_state.argtypes = [vp, U32P, ctypes.c_int]
+    lib.tts_gl_get_phase_state.argtypes = [vp, U32P, ctypes.POINTER(ctypes.c_int)]
+    lib.tts_gl_draw_phases.argtypes = [vp, I32P, ctypes.c_int, ctypes.c_int, vp, vp]
+    lib.tts_gl_save_pcm16.argtypes = [vp, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_double, vp, vp]
     lib.tts_synth_create.argtypes = [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
     lib.tts_synth_destroy.argtypes = [vp]
     lib.tts_synth_destroy.restype = None
@@ -132,7 +140,8 @@ def _declare(lib):
     for name in EXPORTS:
         fn = getattr(lib, name)
         if name.endswith(("_create", "_run", "_timing", "_profile", "_encode", "_decode", "_postnet", "_state",
-                          "_continue", "_basis", "_melspectrogram", "_path", "_sync", "_phases", "_teacher")):
+                          "_continue", "_basis", "_melspectrogram", "_path", "_sync", "_phases", "_teacher",
+                          "_phase_state", "_pcm16", "_limits")):
             fn.restype = ctypes.c_int
 
 

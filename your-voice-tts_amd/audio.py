@@ -14,6 +14,7 @@ host (utils/audio.py:64-66 recomputes it on every call).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import io as _io
 
@@ -167,6 +168,60 @@ class AudioProcessor:
                                      ctypes.c_void_p(wav.data_ptr()), _native.stream_handle()), "tts_gl_run")
         return wav
 
+    # ---------------------------------------------------------------- numpy-stream phases (device)
+    @contextlib.contextmanager
+    def numpy_phases(self):
+        """Within the block, every Griffin-Lim run on this processor's handle with no explicit
+        phase_u (griffin_lim_batch, and the one-call tts_synth_run of a model using it) draws its
+        initial phases from numpy's global generator ON THE DEVICE: bitwise np.random.rand(1025, F_b)
+        per sentence in batch order (utils/audio.py:183), without the host draw or its upload
+        (tts_gl_set_phase_state, phase_mt.hip).  On exit numpy's global state is where the same
+        draws would have left it."""
+        lib, h = self._handle()
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise RuntimeError("numpy's global generator is not the legacy MT19937")
+        key = np.ascontiguousarray(st[1], dtype=np.uint32)
+        _native.check(lib.tts_gl_set_phase_state(h, key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), int(st[2])),
+                      "tts_gl_set_phase_state")
+        try:
+            yield self
+            out = np.empty(624, np.uint32)
+            pos = ctypes.c_int()
+            _native.check(lib.tts_gl_get_phase_state(h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                                     ctypes.byref(pos)), "tts_gl_get_phase_state")
+            np.random.set_state(("MT19937", out, pos.value, st[3], st[4]))
+        finally:
+            lib.tts_gl_set_phase_state(h, None, 0)
+
+    def draw_phases(self, frames, Fmax=None):
+        """The initial phases numpy_phases() gives a batch of these frame counts, as a CUDA fp64
+        [B, 1025, Fmax] tensor (advances the armed state; zero past each sentence's frames)."""
+        lib, h = self._handle()
+        Fmax = max(frames) if Fmax is None else Fmax
+        out = torch.zeros(len(frames), self.n_fft // 2 + 1, Fmax, dtype=torch.float64, device="cuda")
+        _native.check(lib.tts_gl_draw_phases(h, _native.i32_array(frames), len(frames), Fmax,
+                                             ctypes.c_void_p(out.data_ptr()), _native.stream_handle()),
+                      "tts_gl_draw_phases")
+        return out
+
+    def pcm16_join(self, wav, lens, gap=0, peak=None):
+        """Synthesizer.tts's join + save_wav's conversion on the device (tts_gl_save_pcm16): the
+        first lens[b] samples of each row of the CUDA fp64 [B, pitch] ``wav``, each followed by
+        ``gap`` zeros, times 32767 / max(0.01, peak) truncated to int16 (peak None: max |y| of the
+        request).  Returns the int16 samples as a numpy array, bytes equal to numpy's."""
+        lib, h = self._handle()
+        wav = wav if wav.dim() == 2 else wav.view(1, -1)
+        assert wav.dtype == torch.float64 and wav.is_cuda and wav.stride(1) == 1
+        n = np.ascontiguousarray([int(x) for x in lens], dtype=np.int64)
+        total = int(n.sum()) + gap * len(n)
+        out = torch.empty(max(total, 1), dtype=torch.int16, device=wav.device)
+        _native.check(lib.tts_gl_save_pcm16(h, ctypes.c_void_p(wav.data_ptr()), wav.stride(0),
+                                            n.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(n), int(gap),
+                                            -1.0 if peak is None else float(peak), ctypes.c_void_p(out.data_ptr()),
+                                            _native.stream_handle()), "tts_gl_save_pcm16")
+        return out[:total].cpu().numpy()
+
     def inv_mel_spectrogram_batch(self, mel, frames, seed=0, phase_u=None):
         return self.griffin_lim_batch(mel, frames, _native.TTS_GL_FROM_MEL, phase_u, seed)
 
@@ -252,9 +307,11 @@ class AudioProcessor:
         self._handle()  # raises without a GPU / library: no CPU fallback
         spec_nT = np.asarray(spec_nT, dtype=np.float32)
         T = spec_nT.shape[1]
-        phase_u = np.random.rand(self.n_fft // 2 + 1, T)  # utils/audio.py:183 (unseeded, numpy global RNG)
         spec = torch.from_numpy(np.ascontiguousarray(spec_nT.T)).cuda()[None]
-        wav = self.griffin_lim_batch(spec, [T], mode, phase_u[None])
+        # utils/audio.py:183: np.random.rand(1025, T) from numpy's global generator (unseeded unless
+        # the caller seeds it), continued on the device
+        with self.numpy_phases():
+            wav = self.griffin_lim_batch(spec, [T], mode)
         return wav[0].cpu().numpy()
 
     def inv_mel_spectrogram(self, mel_spectrogram):  # utils/audio.py:164-172

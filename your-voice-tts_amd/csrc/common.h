@@ -75,6 +75,14 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
 tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, checks its status
 // whether gl_run_dev takes the persistent loop for this shape (host values only)
 bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters);  // (caches per-F checks in g)
+// phase_mt.hip: numpy's legacy np.random.rand(1025, F[b]) draws for b = 0..B-1 in order, continued
+// on the device from the MT19937 state `state` ([dev] 624 key words + position, updated in place)
+// into out [dev] fp64 [B][1025][Fmax] (one workgroup; F_dev on the device, read on stream s)
+constexpr int MT_MAX_BATCH = 1024;
+hipError_t mt_draw_phases(unsigned* state, const int* F_dev, int B, int Fmax, double* out, hipStream_t s);
+// wav_io.hip: Synthesizer.tts's join + save_wav's int16 conversion (tts_gl_save_pcm16's body)
+hipError_t pcm16_join(const double* wav, int64_t pitch, const int64_t* start_dev, int64_t total, int B, int gap,
+                      double peak, unsigned long long* peak_bits, int16_t* out, hipStream_t s);
 
 // Persistent kernels (in-launch hand-offs between workgroups: resident decoder / encoder, persistent
 // Griffin-Lim) are only correct if every workgroup of the grid is resident at once.  This checks

@@ -106,6 +106,7 @@ struct tts_decoder {
     int last_steps_done = 0;  // steps of the last batch-1 run (continuous mode), 0 otherwise
     int last_resident = 0;    // the last run used the resident decoder
     int res_timeouts = 0;     // resident runs that timed out a hand-off and re-ran multi-launch
+    int res_place_fails = 0;  // consecutive resident runs that stopped on a placement failure
     ResArgs last_ra{};
     InitArgs last_init{};
 };
@@ -860,9 +861,15 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         n_steps[0] = d->host_flags[4];
         if (verbose) fprintf(stderr, "[tts] resident status=%d steps=%d\n", d->host_flags[0], n_steps[0]);
         if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
-            // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD: the kernel
-            // stopped before touching any state; use the multi-launch path from now on
-            d->resident = false;
+            // the runtime placed fewer than RES_MIN_CUS_PER_XCD workgroups on some XCD (or, for the
+            // general form, more than that on one): the kernel stopped before touching any state.
+            // This sentence runs multi-launch; the handle gives the resident path up only after
+            // RES_PLACEMENT_RETRIES such sentences in a row (one uneven dispatch is not a device that
+            // cannot place the grid: ADVICE r5)
+            if (++d->res_place_fails >= RES_PLACEMENT_RETRIES) d->resident = false;
+            if (verbose)
+                fprintf(stderr, "[tts] resident decoder: placement failed (%d in a row)%s\n", d->res_place_fails,
+                        d->resident ? "" : ", multi-launch from now on");
             if (tts_status st = stage_fallback()) return st;
             TTS_HIP(launch_decoder_init(ia, s));
             if (!keep) { tts_status st = enqueue_prenet_go(d, B, s); if (st) return st; }
@@ -891,6 +898,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             run = n_steps[0];
             res_done = true;
             d->last_resident = 1;
+            d->res_place_fails = 0;
         }
         }
     }
@@ -1015,6 +1023,13 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
     TTS_CHECK(d && loop_ms && steps_run, TTS_ERR_INVALID, "null argument");
     *loop_ms = d->last_ms;
     *steps_run = d->last_steps;
+    return TTS_OK;
+}
+
+tts_status tts_decoder_resident_limits(tts_decoder* d, int* max_batch, int* max_len) {
+    TTS_CHECK(d && max_batch && max_len, TTS_ERR_INVALID, "null argument");
+    *max_batch = d->resident ? 1 : 0;
+    *max_len = d->resident ? RES_LMAX : 0;
     return TTS_OK;
 }
 

@@ -1853,6 +1853,21 @@ struct tts_gl {
     bool last_timed = true;       // the last run recorded its events (not in pipeline mode)
     FinArgs last_fin{};
     size_t last_fstride = 0;
+    // numpy-stream initial phases (tts_gl_set_phase_state, phase_mt.hip): the MT19937 state on the
+    // device, the phases it drew for the current run, the stream and event of its last draw
+    bool mt_armed = false;
+    unsigned* mt_state = nullptr;  // [625] key + position
+    double* mt_phase = nullptr;    // [B][1025][Fmax]
+    size_t mt_phase_n = 0;
+    int* mt_F = nullptr;           // tts_gl_draw_phases: the frame counts on the device
+    int mt_F_n = 0;
+    hipStream_t mt_stream = nullptr;
+    hipEvent_t ev_mt = nullptr;
+    // tts_gl_save_pcm16: the peak word and the output offsets ([dev], host copy kept for the upload)
+    unsigned long long* pcm_peak = nullptr;
+    int64_t* pcm_start = nullptr;
+    int pcm_start_n = 0;
+    std::vector<int64_t> pcm_start_h;
 };
 
 extern "C" {
@@ -1861,13 +1876,15 @@ void tts_gl_destroy(tts_gl* g) {
     if (!g) return;
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
+    if (g->mt_stream) (void)hipEventSynchronize(g->ev_mt);  // the last numpy-stream phase draw
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
                     (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pgr, (void*)g->wt, (void*)g->winc,
-                    (void*)g->wssp})
+                    (void*)g->wssp, (void*)g->mt_state, (void*)g->mt_phase, (void*)g->mt_F, (void*)g->pcm_peak,
+                    (void*)g->pcm_start})
         if (p) (void)hipFree(p);
     if (g->host_status) (void)hipHostFree(g->host_status);
-    for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done})
+    for (hipEvent_t e : {g->ev_in, g->ev_out, g->ev_t0, g->ev_t1, g->ev_done, g->ev_mt})
         if (e) (void)hipEventDestroy(e);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -1906,6 +1923,7 @@ tts_status tts_gl_create(const tts_audio_config* cfg, const double* inv_mel_basi
     if ((e = hipEventCreateWithFlags(&g->ev_in, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_out, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
+    if ((e = hipEventCreateWithFlags(&g->ev_mt, hipEventDisableTiming)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_t0, hipEventReleaseToDevice)) != hipSuccess) return fail(e, "event");
     if ((e = hipEventCreateWithFlags(&g->ev_t1, hipEventReleaseToDevice)) != hipSuccess) return fail(e, "event");
     if ((e = hipMalloc(&g->win, NFFT * 8)) != hipSuccess) return fail(e, "hipMalloc");
@@ -2092,6 +2110,18 @@ bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters)
     return true;
 }
 
+// numpy-stream phases for a run of B sentences (F_dev on the device, read on s) into `out`
+// ([B][1025][Fmax]), continuing the handle's MT19937 state; draws on another stream than the last
+// one wait for it (the stream's order is the draws' order)
+static tts_status mt_draw(tts_gl* g, const int* F_dev, int B, int Fmax, double* out, hipStream_t s) {
+    TTS_CHECK(B <= MT_MAX_BATCH, TTS_ERR_UNSUPPORTED, "numpy-stream phases: at most 1024 sentences per run");
+    if (g->mt_stream && g->mt_stream != s) TTS_HIP(hipStreamWaitEvent(s, g->ev_mt, 0));
+    TTS_HIP(mt_draw_phases(g->mt_state, F_dev, B, Fmax, out, s));
+    TTS_HIP(hipEventRecord(g->ev_mt, s));
+    g->mt_stream = s;
+    return TTS_OK;
+}
+
 tts_status gl_collect(tts_gl* g) {
     if (!g->pending) return TTS_OK;
     g->pending = false;
@@ -2113,6 +2143,72 @@ extern "C" {
 tts_status tts_gl_run(tts_gl* g, int mode, const float* spec, const int32_t* F, int B, int Fmax,
                       const double* phase_u, uint64_t seed, int iters, double* wav, void* stream) {
     return tts::gl_run_dev(g, mode, spec, F, nullptr, B, Fmax, phase_u, seed, iters, wav, static_cast<hipStream_t>(stream));
+}
+
+tts_status tts_gl_set_phase_state(tts_gl* g, const uint32_t* key, int pos) {
+    TTS_CHECK(g, TTS_ERR_INVALID, "null handle");
+    if (!key) {
+        g->mt_armed = false;
+        return TTS_OK;
+    }
+    TTS_CHECK(pos >= 0 && pos <= 624, TTS_ERR_INVALID, "MT19937 position must be in [0, 624]");
+    if (!g->mt_state) TTS_HIP(hipMalloc(&g->mt_state, 625 * sizeof(unsigned)));
+    if (g->mt_stream) TTS_HIP(hipEventSynchronize(g->ev_mt));  // a draw may still read the old state
+    unsigned h[625];
+    std::copy(key, key + 624, h);
+    h[624] = (unsigned)pos;
+    TTS_HIP(hipMemcpy(g->mt_state, h, sizeof(h), hipMemcpyHostToDevice));
+    g->mt_armed = true;
+    return TTS_OK;
+}
+
+tts_status tts_gl_get_phase_state(tts_gl* g, uint32_t* key, int* pos) {
+    TTS_CHECK(g && key && pos, TTS_ERR_INVALID, "null argument");
+    TTS_CHECK(g->mt_state, TTS_ERR_INVALID, "no phase state set (tts_gl_set_phase_state)");
+    if (g->mt_stream) TTS_HIP(hipEventSynchronize(g->ev_mt));
+    unsigned h[625];
+    TTS_HIP(hipMemcpy(h, g->mt_state, sizeof(h), hipMemcpyDeviceToHost));
+    std::copy(h, h + 624, key);
+    *pos = (int)h[624];
+    return TTS_OK;
+}
+
+tts_status tts_gl_draw_phases(tts_gl* g, const int32_t* F, int B, int Fmax, double* phase_u, void* stream) {
+    TTS_CHECK(g && F && phase_u && B >= 1 && Fmax >= 1, TTS_ERR_INVALID, "bad draw_phases arguments");
+    TTS_CHECK(g->mt_armed, TTS_ERR_INVALID, "no phase state set (tts_gl_set_phase_state)");
+    for (int b = 0; b < B; ++b) TTS_CHECK(F[b] >= 0 && F[b] <= Fmax, TTS_ERR_INVALID, "F[b] out of range [0, Fmax]");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // (mt_F is rewritten below: a draw on another stream may still read it)
+    if (g->mt_stream && g->mt_stream != s) TTS_HIP(hipStreamWaitEvent(s, g->ev_mt, 0));
+    if (B > g->mt_F_n) {
+        if (g->mt_stream) TTS_HIP(hipEventSynchronize(g->ev_mt));
+        if (g->mt_F) TTS_HIP(hipFree(g->mt_F));
+        g->mt_F = nullptr;
+        TTS_HIP(hipMalloc(&g->mt_F, B * sizeof(int)));
+        g->mt_F_n = B;
+    }
+    TTS_HIP(hipMemcpyAsync(g->mt_F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+    return tts::mt_draw(g, g->mt_F, B, Fmax, phase_u, s);
+}
+
+tts_status tts_gl_save_pcm16(tts_gl* g, const double* wav, int64_t pitch, const int64_t* n, int B, int gap,
+                             double peak, int16_t* out, void* stream) {
+    TTS_CHECK(g && wav && n && out && B >= 1 && gap >= 0, TTS_ERR_INVALID, "bad save_pcm16 arguments");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    for (int b = 0; b < B; ++b) TTS_CHECK(n[b] >= 0 && n[b] <= pitch, TTS_ERR_INVALID, "n[b] out of range [0, pitch]");
+    if (!g->pcm_peak) TTS_HIP(hipMalloc(&g->pcm_peak, sizeof(unsigned long long)));
+    if (B + 1 > g->pcm_start_n) {
+        TTS_HIP(hipStreamSynchronize(s));  // (the previous join on this stream may still read it)
+        if (g->pcm_start) TTS_HIP(hipFree(g->pcm_start));
+        g->pcm_start = nullptr;
+        TTS_HIP(hipMalloc(&g->pcm_start, (B + 1) * sizeof(int64_t)));
+        g->pcm_start_n = B + 1;
+    }
+    g->pcm_start_h.assign(B + 1, 0);
+    for (int b = 0; b < B; ++b) g->pcm_start_h[b + 1] = g->pcm_start_h[b] + n[b] + gap;
+    TTS_HIP(hipMemcpyAsync(g->pcm_start, g->pcm_start_h.data(), (B + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    TTS_HIP(tts::pcm16_join(wav, pitch, g->pcm_start, g->pcm_start_h[B], B, gap, peak, g->pcm_peak, out, s));
+    return TTS_OK;
 }
 }  // extern "C"
 
@@ -2186,6 +2282,20 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
     if (Fd == g->F) {
         if (F_bound) TTS_HIP(hipMemcpyAsync(g->F, F_dev, B * sizeof(int), hipMemcpyDeviceToDevice, s));
         else TTS_HIP(hipMemcpyAsync(g->F, F, B * sizeof(int), hipMemcpyHostToDevice, s));
+    }
+    if (!phase_u && g->mt_armed) {
+        // the reference's np.random.rand draws, continued on the device from numpy's state
+        // (tts_gl_set_phase_state): one [1025][F_b] draw per sentence in batch order
+        const size_t needP = (size_t)B * NB * Fmax;
+        if (needP > g->mt_phase_n) {
+            if (g->mt_stream) TTS_HIP(hipStreamSynchronize(g->mt_stream));  // an earlier run may still read it
+            if (g->mt_phase) TTS_HIP(hipFree(g->mt_phase));
+            g->mt_phase = nullptr;
+            TTS_HIP(hipMalloc(&g->mt_phase, needP * sizeof(double)));
+            g->mt_phase_n = needP;
+        }
+        if ((st = mt_draw(g, Fd, B, Fmax, g->mt_phase, s))) return st;
+        phase_u = g->mt_phase;
     }
     MagArgs ma{};
     ma.mode = mode;

@@ -52,6 +52,7 @@ constexpr int GR_HATT = 576, GR_HDEC = 2304, GR_PRE2X = 3328, GR_SETUP = 5376, G
 constexpr int RES_MIN_CUS_PER_XCD = 32;  // 8 XCDs x 32: query rows 4 per CU, prenet-1/2 rows 8 per CU
 static_assert(RES_MIN_CUS_PER_XCD * 8 >= PRE, "at most one prenet row per wave");
 constexpr int RES_STATUS_PLACEMENT = 50;  // status: an XCD holds fewer than RES_MIN_CUS_PER_XCD workgroups
+constexpr int RES_PLACEMENT_RETRIES = 3;  // placement failures in a row before a handle stops trying
 // the failure code of launch `salt` from its status word (salt << 8 | code; anything else: none)
 inline int res_status_code(int word, unsigned salt) {
     return ((unsigned)word >> 8) == salt ? (word & 0xFF) : 0;

@@ -45,6 +45,9 @@ struct tts_synth {
     size_t pin_n[2] = {0, 0};
     unsigned calls = 0;
     int* fspec = nullptr;  // [dev] frame count of a speculative batch-1 Griffin-Lim (synth_stages)
+    // the caller's stream the last batch-1 run worked on (synth_stages), or null: tts_synth_sync waits
+    // for it (that run's stages, down to the de-emphasis writing the waveform, are on it only)
+    hipStream_t last_cs = nullptr;
 };
 
 namespace {
@@ -119,6 +122,8 @@ void tts_synth_destroy(tts_synth* s) {
     if (!s) return;
     for (hipStream_t q : {s->stream, s->gl_stream})
         if (q) (void)hipStreamSynchronize(q);
+    // a batch-1 run worked on the caller's stream, which may be gone by now: wait for the device
+    if (s->last_cs) (void)hipDeviceSynchronize();
     if (tts::gl_collect(s->g) != TTS_OK)  // the last pipelined run's status was never collected
         std::fprintf(stderr, "tts_synth_destroy: the last run failed: %s\n", tts_last_error());
     for (void* q : {(void*)s->ids, (void*)s->enc, (void*)s->mel, (void*)s->stop, (void*)s->post[0],
@@ -216,6 +221,8 @@ tts_status tts_synth_sync(tts_synth* s) {
     TTS_CHECK(s, TTS_ERR_INVALID, "null handle");
     TTS_HIP(hipStreamSynchronize(s->stream));
     TTS_HIP(hipStreamSynchronize(s->gl_stream));
+    // a batch-1 run's stages ran on the caller's stream (no event marks their end: ADVICE r5)
+    if (s->last_cs) TTS_HIP(hipStreamSynchronize(s->last_cs));
     return tts::gl_collect(s->g);
 }
 
@@ -236,6 +243,7 @@ tts_status synth_stages(tts_synth* s, int32_t* h_ids, int32_t* h_lens, const int
         return v && v[0] == '1';
     }();
     hipStream_t ss = B == 1 && !own_stream ? cs : s->stream;
+    s->last_cs = ss == cs ? cs : nullptr;
     const int cap = max_steps + 21;
     const size_t T = (size_t)cap * s->r;
     tts_status st;

@@ -14,6 +14,7 @@ import re
 import time
 
 import numpy as np
+import scipy.io.wavfile
 import torch
 
 from . import _native
@@ -70,43 +71,84 @@ def wav_to_int16(wav):
 SERIAL_RESIDENT_MAX = int(os.environ.get("TTS_SERIAL_MAX", "3"))
 
 
-def _decode(model, ids_list, speaker_ids=None):
-    """Tacotron2 decode of a request: serial resident calls below the crossover, else one batch."""
+def _serial_eligible(model, ids_list):
+    """Whether a request decodes serially on the resident batch-1 decoder: 2..SERIAL_RESIDENT_MAX
+    sentences, each within the length the handle's resident decoder serves now
+    (tts_decoder_resident_limits: no hard-coded limit here)."""
     B = len(ids_list)
-    if B == 1 or B > SERIAL_RESIDENT_MAX or max(len(x) for x in ids_list) > 256:
-        out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
-        out["dispatch"] = "batch"
-        return out
-    from .tacotron2 import _speaker_array
-    spk = None if speaker_ids is None else _speaker_array(speaker_ids, B)
-    outs = []
-    for b, x in enumerate(ids_list):
-        outs.append(model.inference_batch([x], speaker_ids=None if spk is None else spk[b:b + 1]))
-        if b == 0 and not model.last_timing.get("resident"):
-            # no resident decoder on this handle: the rest as one batch is cheaper
-            outs.append(model.inference_batch(ids_list[1:], speaker_ids=None if spk is None else spk[1:]))
-            break
+    if B < 2 or B > SERIAL_RESIDENT_MAX:
+        return False
+    Lmax = max(len(x) for x in ids_list)
+    mb, ml = model.resident_limits(Lmax)
+    return mb >= 1 and Lmax <= ml
+
+
+def _stack(outs, B):
+    """Per-call inference_batch dicts (in sentence order) -> the batch dict inference_batch returns
+    for the whole request: mel / mel_post [B, T, 80], align [B, S, Lmax], stop [B, S], zero-padded."""
     frames = [f for o in outs for f in o["frames"]]
     steps = [n for o in outs for n in o["steps"]]
-    T = max(frames)
-    mel_post = torch.zeros(B, T, outs[0]["mel_post"].shape[2], device=outs[0]["mel_post"].device)
+    lens = [n for o in outs for n in o["lens"]]
+    T, S, Lmax = max(frames), max(steps), max(lens)
+    dev = outs[0]["mel_post"].device
+    res = dict(mel=torch.zeros(B, T, outs[0]["mel"].shape[2], device=dev),
+               mel_post=torch.zeros(B, T, outs[0]["mel_post"].shape[2], device=dev),
+               align=torch.zeros(B, S, Lmax, device=dev), stop=torch.zeros(B, S, device=dev))
     b = 0
     for o in outs:
         for k in range(len(o["frames"])):
-            mel_post[b, :o["frames"][k]] = o["mel_post"][k, :o["frames"][k]]
+            t, n, L = o["frames"][k], o["steps"][k], o["lens"][k]
+            res["mel"][b, :t] = o["mel"][k, :t]
+            res["mel_post"][b, :t] = o["mel_post"][k, :t]
+            res["align"][b, :n, :L] = o["align"][k, :n, :L]
+            res["stop"][b, :n] = o["stop"][k, :n]
             b += 1
-    return dict(mel_post=mel_post, frames=frames, steps=steps, dispatch="serial-resident")
+    res.update(frames=frames, steps=steps, lens=lens)
+    return res
+
+
+def _decode(model, ids_list, speaker_ids=None):
+    """Tacotron2 decode of a request: serial resident calls below the crossover, else one batch.
+    Both dispatches return inference_batch's dict; ``decoder_timings`` lists each call's timing."""
+    B = len(ids_list)
+    if not _serial_eligible(model, ids_list):
+        out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
+        out["dispatch"] = "batch"
+        out["decoder_timings"] = [dict(model.last_timing)]
+        return out
+    from .tacotron2 import _speaker_array
+    spk = None if speaker_ids is None else _speaker_array(speaker_ids, B)
+    outs, timings = [], []
+    for b, x in enumerate(ids_list):
+        outs.append(model.inference_batch([x], speaker_ids=None if spk is None else spk[b:b + 1]))
+        timings.append(dict(model.last_timing))
+        if not model.last_timing.get("resident") and b + 1 < B:
+            # this call fell off the resident path (placement, a long sentence): the rest as one
+            # batch is cheaper than more multi-launch batch-1 calls (ADVICE r5)
+            outs.append(model.inference_batch(ids_list[b + 1:], speaker_ids=None if spk is None else spk[b + 1:]))
+            timings.append(dict(model.last_timing))
+            break
+    out = _stack(outs, B)
+    out["dispatch"] = "serial-resident"
+    out["decoder_timings"] = timings
+    # the request's decoder loop time is the sum of its calls'
+    model.last_timing = dict(timings[-1], decoder_loop_ms=sum(t.get("decoder_loop_ms", 0.0) for t in timings),
+                             decoder_steps_run=sum(t.get("decoder_steps_run", 0) for t in timings),
+                             resident=all(t.get("resident") for t in timings))
+    return out
 
 
 @torch.no_grad()
 def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed=0, phase="device",
-                     iters=None, keep_outputs=False, style_mel=None):
+                     iters=None, keep_outputs=False, style_mel=None, to_host=True):
     """ids -> encoder -> HIP decoder -> HIP postnet -> HIP Griffin-Lim for a ragged batch.
 
-    phase: "device" draws the initial GL phases on the GPU from ``seed``; "numpy" draws them
-    sentence by sentence with np.random.rand(1025, T_b) in batch order, as the reference does
-    when it synthesises the sentences one after another.  Returns (wavs: list of float64 numpy
-    arrays, info dict)."""
+    phase: "device" draws the initial GL phases on the GPU from ``seed``; "numpy" gives every
+    sentence numpy's np.random.rand(1025, T_b) draw in batch order, as the reference does when it
+    synthesises the sentences one after another (utils/audio.py:183) -- continued on the device from
+    numpy's global state (ap.numpy_phases, phase_mt.hip), which is left where those draws would
+    leave it.  Returns (wavs: list of float64 numpy arrays, or None with to_host=False, info dict;
+    info["wav_dev"] is the CUDA fp64 [B, N] waveform batch with keep_outputs or to_host=False)."""
     linear = hasattr(model, "linear_dim")  # Tacotron / TacotronGST: linear-spectrogram GL
     if linear:
         out = model.inference_batch(ids_list, speaker_ids=speaker_ids, style_mel=style_mel)
@@ -114,20 +156,23 @@ def synthesize_batch(model, ap: AudioProcessor, ids_list, speaker_ids=None, seed
         out = _decode(model, ids_list, speaker_ids)
     frames = out["frames"]
     mel_post = out["linear"] if linear else out["mel_post"]
-    phase_u = None
-    if phase == "numpy":
-        Fmax = mel_post.shape[1]
-        phase_u = np.zeros((len(frames), ap.n_fft // 2 + 1, Fmax))
-        for b, T in enumerate(frames):
-            phase_u[b, :, :T] = np.random.rand(ap.n_fft // 2 + 1, T)
     mode = _native.TTS_GL_FROM_LINEAR if linear else _native.TTS_GL_FROM_MEL
-    wav = ap.griffin_lim_batch(mel_post, frames, mode=mode, phase_u=phase_u, seed=seed, iters=iters)
+    if phase == "numpy":
+        with ap.numpy_phases():
+            wav = ap.griffin_lim_batch(mel_post, frames, mode=mode, iters=iters)
+    elif phase == "device":
+        wav = ap.griffin_lim_batch(mel_post, frames, mode=mode, seed=seed, iters=iters)
+    else:
+        raise ValueError(f"phase must be 'device' or 'numpy', not {phase!r}")
     lens = [ap.hop_length * (T - 1) for T in frames]
     info = dict(frames=frames, steps=out["steps"], samples=lens, decoder_dispatch=out.get("dispatch", "batch"),
                 **model.last_timing, **ap.last_gl_timing())
     if keep_outputs:
         info.update(out)
+    if keep_outputs or not to_host:
         info["wav_dev"] = wav
+    if not to_host:
+        return None, info
     wav_h = wav.cpu().numpy()
     return [wav_h[b, :n] for b, n in enumerate(lens)], info
 
@@ -277,16 +322,41 @@ class Synthesizer:
             sens = [text + "."]
         return [s.strip() for s in sens if len(s) >= 3]
 
+    def synthesize(self, ids):
+        """The waveforms of a request's sentences, on the device: (CUDA fp64 [B, pitch], samples per
+        sentence).  Initial phases from numpy's global stream (the caller is inside
+        ap.numpy_phases()).  Tacotron2 requests of up to SERIAL_RESIDENT_MAX sentences run one
+        tts_synth_run per sentence (encoder -> resident decoder -> postnet -> Griffin-Lim in one
+        native call each); larger ones, and the Tacotron family, as one batch (synthesize_batch)."""
+        model, ap = self.tts_model, self.ap
+        if not hasattr(model, "linear_dim") and (len(ids) == 1 or _serial_eligible(model, ids)):
+            cap = model.native_wav_capacity(ap, 1)
+            buf = torch.empty(len(ids), cap, dtype=torch.float64, device="cuda")
+            lens = []
+            for b, x in enumerate(ids):
+                # sync: the next sentence's resident launch must not share the device with this one's
+                # Griffin-Lim (and the numpy stream stays in sentence order)
+                _, frames = model.synthesize_native([x], ap, sync=True, out=buf[b])
+                lens.append(ap.hop_length * (frames[0] - 1))
+            return buf, lens
+        _, info = synthesize_batch(model, ap, ids, seed=self.seed, phase="numpy", to_host=False)
+        return info["wav_dev"], info["samples"]
+
     def tts(self, text):
+        """server/synthesizer.py:128-162: split, synthesise every sentence, join them with 10 000
+        zeros after each, peak-normalise to int16 and return the wav in a BytesIO.  The waveforms stay
+        on the device until the int16 join (tts_gl_save_pcm16: the reference's Python-list join and
+        save_wav conversion, bytes equal); the phases are numpy's global stream continued on the
+        device (the reference's per-sentence np.random.rand draws, utils/audio.py:183)."""
         sens = self.sentences(text)
         adapter = self.input_adapter or (lambda sen: text_to_seqvec(sen, self.tts_config))
         ids = [np.asarray(adapter(s)) for s in sens]
-        wavs = []
-        if ids:
-            outs, _ = synthesize_batch(self.tts_model, self.ap, ids, seed=self.seed, phase="numpy")
-            for w in outs:
-                wavs += list(w)
-                wavs += [0] * 10000  # server/synthesizer.py:158
         out = io.BytesIO()
-        self.save_wav(wavs, out)
+        if not ids:  # the reference's save_wav([]) raises on the empty maximum, so does this
+            self.save_wav([], out)
+            return out
+        with self.ap.numpy_phases():
+            wav, lens = self.synthesize(ids)
+        pcm = self.ap.pcm16_join(wav, lens, gap=10000)  # server/synthesizer.py:158
+        scipy.io.wavfile.write(out, self.ap.sample_rate, pcm)
         return out

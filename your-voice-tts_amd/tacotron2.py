@@ -340,7 +340,7 @@ class Tacotron2:
         return out["mel"], out["mel_post"], out["align"], out["stop"].unsqueeze(-1)
 
     @torch.no_grad()
-    def synthesize_native(self, ids_list, ap, seed=0, iters=None, sync=True, speaker_ids=None):
+    def synthesize_native(self, ids_list, ap, seed=0, iters=None, sync=True, speaker_ids=None, out=None):
         """utils/synthesis.py:synthesis (model.inference, :50-57 -> ap.inv_mel_spectrogram, :69-77)
         for a ragged batch in ONE native call (tts_synth_run): encoder -> decoder -> postnet ->
         Griffin-Lim with device phases from ``seed``, bitwise what inference_batch followed by
@@ -349,7 +349,10 @@ class Tacotron2:
 
         sync=True waits for the run and raises on its completion status; sync=False returns once
         Griffin-Lim is enqueued (the next call overlaps it and raises a failure of this one; a
-        failed run's waveform is NaN, never a plausible signal)."""
+        failed run's waveform is NaN, never a plausible signal).  ``out``: a CUDA fp64 buffer of at
+        least ``native_wav_capacity(ap, B)`` elements to write into instead of the model's own (which
+        the next call reuses).  Inside ``ap.numpy_phases()`` the phases are numpy's stream, not
+        ``seed``'s."""
         if speaker_ids is not None and "speaker_embedding.weight" not in self._params:
             speaker_ids = None  # (the reference adds no embedding without the table either)
         lens = [len(x) for x in ids_list]
@@ -375,20 +378,26 @@ class Tacotron2:
             ids[b, :lens[b]] = np.asarray(x, dtype=np.int32)
         # the decoder may legally run max_steps + 20 steps (the elif cap of layers/tacotron2.py:271-277
         # is skipped once every stop flag is set): size for the decoder's own steps_cap
-        cap = B * ap.hop_length * ((max_steps + 21) * self.n_frames_per_step - 1)
-        if self._wav_buf is None or self._wav_buf.numel() < cap:
-            self._wav_buf = torch.empty(cap, dtype=torch.float64, device=self.device)
+        cap = self.native_wav_capacity(ap, B)
+        if out is not None:
+            if out.dtype != torch.float64 or not out.is_cuda or not out.is_contiguous() or out.numel() < cap:
+                raise ValueError(f"out must be a contiguous CUDA float64 buffer of >= {cap} elements")
+            wav_buf = out
+        else:
+            if self._wav_buf is None or self._wav_buf.numel() < cap:
+                self._wav_buf = torch.empty(cap, dtype=torch.float64, device=self.device)
+            wav_buf = self._wav_buf
         frames = (ctypes.c_int32 * B)()
         iters = ap.griffin_lim_iters if iters is None else iters
         if speaker_ids is None:
             _native.check(lib.tts_synth_run(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens), B, Lmax,
-                                            max_steps, int(iters), int(seed), ctypes.c_void_p(self._wav_buf.data_ptr()),
+                                            max_steps, int(iters), int(seed), ctypes.c_void_p(wav_buf.data_ptr()),
                                             cap, frames, _native.stream_handle()), "tts_synth_run")
         else:
             spk = _speaker_array(speaker_ids, B)
             _native.check(lib.tts_synth_run_speakers(hs, ids.ctypes.data_as(_native.I32P), _native.i32_array(lens),
                                                      _native.i32_array(spk), B, Lmax, max_steps, int(iters), int(seed),
-                                                     ctypes.c_void_p(self._wav_buf.data_ptr()), cap, frames,
+                                                     ctypes.c_void_p(wav_buf.data_ptr()), cap, frames,
                                                      _native.stream_handle()), "tts_synth_run_speakers")
         frames = [int(f) for f in frames]
         if sync:
@@ -396,7 +405,22 @@ class Tacotron2:
         self.last_timing = self._path_timing(lib, hdec)
         self.last_lengths = frames
         n = ap.hop_length * (max(frames) - 1)
-        return self._wav_buf[:B * n].view(B, n), frames
+        return wav_buf.view(-1)[:B * n].view(B, n), frames
+
+    def native_wav_capacity(self, ap, B=1):
+        """Waveform elements one synthesize_native call of B sentences may write: the decoder may
+        legally run max_steps + 20 steps (the elif cap of layers/tacotron2.py:271-277 is skipped once
+        every stop flag is set), so the buffer is sized for the decoder's own steps_cap."""
+        return B * ap.hop_length * ((int(self.decoder.max_decoder_steps) + 21) * self.n_frames_per_step - 1)
+
+    def resident_limits(self, Lmax=1):
+        """(max sentences, max encoder length) the resident decoder serves on this handle now
+        (tts_decoder_resident_limits; (0, 0): multi-launch only)."""
+        lib, hdec, _ = self._handles(max(int(Lmax), 1), 1)
+        mb, ml = ctypes.c_int(), ctypes.c_int()
+        _native.check(lib.tts_decoder_resident_limits(hdec, ctypes.byref(mb), ctypes.byref(ml)),
+                      "tts_decoder_resident_limits")
+        return mb.value, ml.value
 
     def synth_sync(self):
         """Wait for the last synthesize_native call and raise if its Griffin-Lim failed
