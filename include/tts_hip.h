@@ -140,10 +140,12 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
 
 /* Which implementation ran the last tts_decoder_run / _continue (no reference counterpart):
  * *resident = 1 for the resident single-launch batch-1 decoder (every step weight held on chip
- * by 256 workgroups, hand-offs in device memory), 0 for the per-step multi-launch hipGraph path.
- * The resident path serves B = 1, L <= 256 under the synthesis attention configuration (forward
- * attention + mask, sigmoid norm) on a GPU with >= 256 compute units; TTS_RESIDENT=0 in the
- * environment at tts_decoder_create disables it. */
+ * by 256 workgroups, hand-offs in device memory), 2 for the resident batch decoder (the same for
+ * up to 4 sentences per launch, both LSTMs' rows in registers; consecutive launches for larger
+ * batches), 0 for the per-step multi-launch hipGraph path.  The batch-1 path serves L <= 256 under
+ * every Tacotron2 attention configuration, the batch path 2 <= B with every L_b <= 256 under those
+ * without location features, windowing or transition agent; both need >= 256 compute units.
+ * TTS_RESIDENT=0 / TTS_RESIDENT_BATCH=0 in the environment at tts_decoder_create disable them. */
 tts_status tts_decoder_last_path(tts_decoder* d, int* resident);
 /* The requests the resident decoder serves on this handle now: batches of at most *max_batch
  * sentences of encoder length <= *max_len (both 0: the handle runs multi-launch only, e.g. after

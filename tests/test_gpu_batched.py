@@ -171,17 +171,18 @@ def test_config4_gst_batch32_full_cap_linear_griffin_lim_vs_oracle():
     assert rel_rms(wav[b, :nb], ref) < WAV_RTOL, (b, T)
 
 
-@pytest.mark.parametrize("txt,sens_ref,dispatch", [
+@pytest.mark.parametrize("txt,sens_ref,kind", [
     ("It took me quite a long time. Dr. Smith spoke! Ok? Then we left.",
-     ["It took me quite a long time.", "Dr. Smith spoke!", "Ok?", "Then we left."], "batch"),
+     ["It took me quite a long time.", "Dr. Smith spoke!", "Ok?", "Then we left."], 2),
     ("It took me quite a long time. Dr. Smith spoke! Then we left.",
-     ["It took me quite a long time.", "Dr. Smith spoke!", "Then we left."], "serial-resident")])
-def test_synthesizer_tts_vs_oracle_chain(audio_cfg, txt, sens_ref, dispatch):
+     ["It took me quite a long time.", "Dr. Smith spoke!", "Then we left."], 2),
+    ("It took me quite a long time.", ["It took me quite a long time."], 1)])
+def test_synthesizer_tts_vs_oracle_chain(audio_cfg, txt, sens_ref, kind):
     """Synthesizer.tts (server/synthesizer.py:128-162) on a multi-sentence text with the reference's
     numpy phases: split, drop len < 3, per-sentence Tacotron2 (cap 3000) + GL in order, 10 000-zero
     gaps, one global peak -> int16, vs the oracle chain doing exactly that one sentence at a time.
-    Four sentences decode as one batch, three as serial resident batch-1 calls (synthesis.py:
-    SERIAL_RESIDENT_MAX); Griffin-Lim is one batch either way."""
+    Requests of several sentences decode on the resident batch decoder in one tts_synth_run (kind 2),
+    one sentence on the batch-1 resident decoder (kind 1)."""
     import scipy.io.wavfile
     text = load_pkg("text")
     synth = load_pkg("synthesis")
@@ -194,7 +195,7 @@ def test_synthesizer_tts_vs_oracle_chain(audio_cfg, txt, sens_ref, dispatch):
     assert sens == sens_ref
     np.random.seed(77)
     buf = s.tts(txt)
-    assert bool(m.last_timing["resident"]) == (dispatch == "serial-resident")
+    assert m.last_timing["resident_kind"] == kind
     buf.seek(0)
     sr, pcm = scipy.io.wavfile.read(buf)
     assert sr == 22050 and pcm.dtype == np.int16

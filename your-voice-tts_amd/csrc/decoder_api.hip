@@ -107,11 +107,27 @@ struct tts_decoder {
     int last_resident = 0;    // the last run used the resident decoder
     int res_timeouts = 0;     // resident runs that timed out a hand-off and re-ran multi-launch
     int res_place_fails = 0;  // consecutive resident runs that stopped on a placement failure
+    // resident decoder for batches of 2..RB_MAXB sentences per launch (resident_batch.hip)
+    bool rbatch = false;
+    int rb_gen = 0;
+    float4 *rb_wa = nullptr, *rb_wd = nullptr;
+    unsigned long long* rb_gran = nullptr;  // resident_batch_granules() slots, then int status[4]
+    unsigned rb_salt = 0;
+    int rb_place_fails = 0;
     ResArgs last_ra{};
     InitArgs last_init{};
 };
 
 namespace {
+
+// the largest batch the resident batch decoder takes (consecutive launches of <= RB_MAXB)
+int rb_max_batch() {
+    static const int v = [] {
+        const char* e = getenv("TTS_RB_MAX");
+        return e && e[0] ? std::max(0, atoi(e)) : 12;
+    }();
+    return v;
+}
 
 template <typename T>
 tts_status dmalloc(tts_decoder* d, T** p, size_t n) {
@@ -519,6 +535,32 @@ tts_status tts_decoder_create(const tts_decoder_config* cfg, const tts_tensor* t
                 d->rw.wdc = reinterpret_cast<float4*>(pdc);
                 ResSrc src{a_wih, a_whh, a_bih, a_bhh, d_wih, d_whh, d_bih, d_bhh, w_p1, d->b_pre2, wq, wf, bf, nfused};
                 e = resident_pack(src, d->rw, s);
+                // small batches: the batched resident decoder (both LSTMs' rows in registers) for the
+                // attention configurations it covers; TTS_RESIDENT_BATCH=0 keeps them multi-launch
+                const int gen = GEN_ON | (cfg->attn_norm == 0 ? GEN_SOFTMAX : 0) | (cfg->forward_attn ? GEN_FORWARD : 0) |
+                                (cfg->forward_attn && cfg->forward_attn_mask ? GEN_MASK : 0) |
+                                (cfg->forward_attn && cfg->trans_agent ? GEN_TA : 0) | (cfg->location_attn ? GEN_LOCATION : 0) |
+                                (cfg->windowing ? GEN_WINDOW : 0);
+                const char* rbe = getenv("TTS_RESIDENT_BATCH");
+                if (e == hipSuccess && cfg->max_batch >= 2 && resident_batch_supports(gen) && !(rbe && rbe[0] == '0') &&
+                    resident_batch_prepare() == hipSuccess) {
+                    size_t nra, nrd;
+                    resident_batch_weight_floats(&nra, &nrd);
+                    float *qa = nullptr, *qd = nullptr;
+                    if (dmalloc(d, &qa, nra) || dmalloc(d, &qd, nrd) || dmalloc(d, &d->rb_gran, resident_batch_granules() + 2))
+                        e = hipErrorOutOfMemory;
+                    if (e == hipSuccess) {
+                        d->rb_wa = reinterpret_cast<float4*>(qa);
+                        d->rb_wd = reinterpret_cast<float4*>(qd);
+                        e = resident_batch_pack(src, d->rb_wa, d->rb_wd, s);
+                        if (e == hipSuccess)
+                            e = hipMemsetAsync(d->rb_gran, 0, sizeof(unsigned long long) * (resident_batch_granules() + 2), s);
+                    }
+                    if (e == hipSuccess) {
+                        d->rbatch = true;
+                        d->rb_gen = gen;
+                    }
+                }
             }
         }
         if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -796,7 +838,88 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     if (verbose)
         fprintf(stderr, "[tts] decoder_run B=%d L=%d resident=%d gen=%d keep=%d direct=%d\n", B, lens[0],
                 (int)d->resident, d->res_gen, (int)keep, (int)direct);
-    if (d->resident && B == 1 && lens[0] <= RES_LMAX) {
+    // consecutive launches of <= RB_MAXB sentences beat the multi-launch step (~45 us at any batch up
+    // to 64) only for a few groups: TTS_RB_MAX (default rb_max_batch()) bounds the batch
+    bool rb_ok = d->rbatch && B >= 2 && B <= rb_max_batch() && !keep;
+    for (int b = 0; rb_ok && b < B; ++b) rb_ok = lens[b] <= RES_LMAX;
+    if (rb_ok) {
+        // batches: one persistent launch per group of <= RB_MAXB sentences (resident_batch.hip),
+        // each sentence's state, histories and step count in the multi-launch path's slots
+        if (timed) TTS_HIP(hipEventRecord(d->ev_t0, s));
+        bool all = true;
+        for (int g0 = 0; g0 < B && all; g0 += RB_MAXB) {
+            const int nb = std::min(RB_MAXB, B - g0);
+            ResBatchArgs rb{};
+            rb.B = nb;
+            rb.gen = d->rb_gen;
+            for (int b = 0; b < nb; ++b) rb.L[b] = lens[g0 + b];
+            rb.Lcap = d->Lcap; rb.nmel = d->nmel; rb.nrows = d->nmel + PRE + 1; rb.max_steps = max_steps;
+            rb.hist_cap = d->hist_cap; rb.Lalign = Lmax; rb.timeout_ticks = d->res_ticks;
+            rb.wa = d->rb_wa; rb.wd = d->rb_wd;
+            rb.w2 = d->rw.w2; rb.b2 = d->rw.b2; rb.wq = d->rw.wq; rb.wf = d->rw.wf; rb.bf = d->rw.bf; rb.ba = d->rw.ba;
+            rb.bd = d->rw.bd;
+            rb.v = d->v; rb.v_b = d->v_b;
+            rb.Pt = d->Pt + (size_t)g0 * ADIM * d->Lcap;
+            rb.enc = d->enc + (size_t)g0 * d->Lcap * ENC;
+            rb.h_att = d->h_att + (size_t)g0 * HATT; rb.c_att = d->c_att + (size_t)g0 * HATT;
+            rb.h_dec = d->h_dec + (size_t)g0 * HDEC; rb.c_dec = d->c_dec + (size_t)g0 * HDEC;
+            rb.xa = d->xa + (size_t)g0 * XA;
+            rb.hps = (int64_t)d->Bcap * HATT; rb.xps = (int64_t)d->Bcap * XA;
+            rb.pre1 = d->pre1 + (size_t)g0 * PRE;
+            rb.alpha = d->alpha + (size_t)g0 * d->Lcap;
+            rb.nidx = d->nidx + g0; rb.u = d->u + g0; rb.flag1 = d->flag1 + g0; rb.count = d->count + g0;
+            rb.done = d->done + g0; rb.n_steps = d->n_steps + g0;
+            rb.mel_hist = d->mel_hist + (size_t)g0 * d->hist_cap * d->nmel;
+            rb.stop_hist = d->stop_hist + (size_t)g0 * d->hist_cap;
+            rb.align_hist = d->align_hist + (size_t)g0 * d->hist_cap * Lmax;
+            rb.gran = d->rb_gran;
+            rb.status = reinterpret_cast<int*>(d->rb_gran + resident_batch_granules());
+            bool wrapped = false;
+            d->rb_salt = res_next_salt(d->rb_salt, &wrapped);
+            rb.salt = d->rb_salt;
+            if (wrapped)
+                TTS_HIP(hipMemsetAsync(d->rb_gran, 0, sizeof(unsigned long long) * (resident_batch_granules() + 2), s));
+            TTS_HIP(hipMemsetAsync(rb.status, 0, 4 * sizeof(int), s));
+            bool launched = false;
+            TTS_HIP(launch_resident_batch(rb, s, &launched));
+            if (verbose) fprintf(stderr, "[tts] resident batch launch g0=%d nb=%d launched=%d\n", g0, nb, (int)launched);
+            if (!launched) {
+                d->rbatch = false;  // the grid cannot be co-resident on this device
+                all = false;
+                break;
+            }
+            TTS_HIP(hipMemcpyAsync(d->host_flags, rb.status, sizeof(int), hipMemcpyDeviceToHost, s));
+            TTS_HIP(hipMemcpyAsync(d->host_flags + 4 + g0, d->n_steps + g0, sizeof(int) * nb, hipMemcpyDeviceToHost, s));
+            TTS_HIP(spin_sync(s, d->ev_sync));
+            if (verbose) fprintf(stderr, "[tts] resident batch status=%d\n", d->host_flags[0]);
+            if (d->host_flags[0] != 0) {
+                TTS_CHECK(d->host_flags[0] != 100, TTS_ERR_HIP, "decoder did not stop within max_steps + 20 (internal error)");
+                if (d->host_flags[0] == RES_STATUS_PLACEMENT) {
+                    if (++d->rb_place_fails >= RES_PLACEMENT_RETRIES) d->rbatch = false;
+                } else {
+                    ++d->res_timeouts;
+                }
+                all = false;
+                break;
+            }
+            d->rb_place_fails = 0;
+        }
+        if (all) {
+            if (timed) TTS_HIP(hipEventRecord(d->ev_t1, s));
+            std::copy(d->host_flags + 4, d->host_flags + 4 + B, n_steps);
+            run = 0;
+            for (int b = 0; b < B; ++b) run = std::max(run, (int)n_steps[b]);
+            res_done = true;
+            d->last_resident = 2;
+        } else {
+            // re-run the whole batch on the multi-launch path from its initial state
+            TTS_HIP(launch_decoder_init(ia, s));
+            if (frag_on(d, B)) { tts_status fs = enqueue_frag_sync(d, B, s); if (fs) return fs; }
+            tts_status st = enqueue_prenet_go(d, B, s);
+            if (st) return st;
+        }
+    }
+    if (!res_done && d->resident && B == 1 && lens[0] <= RES_LMAX) {
         // one persistent launch runs every step (resident.h); same state / history buffers
         ResArgs ra{};
         ra.w = d->rw;
@@ -982,7 +1105,7 @@ namespace {
 // Measurement only: re-run the last batch-1 resident sentence with timers (marks: per-phase tick
 // sums of CU 0 and the logging attention CU; always: the per-CU event trace, kept in d->res_trace).
 tts_status res_rerun(tts_decoder* d, bool marks, long long* h) {
-    TTS_CHECK(d->last_resident && d->last_steps > 0, TTS_ERR_INVALID,
+    TTS_CHECK(d->last_resident == 1 && d->last_steps > 0, TTS_ERR_INVALID,
               "the resident decoder profile needs a previous resident tts_decoder_run");
     TTS_HIP(hipDeviceSynchronize());  // measurement only: nothing else (a pipeline GL) on the device
     hipStream_t s = d->stream;
@@ -1028,7 +1151,7 @@ tts_status tts_decoder_last_timing(tts_decoder* d, float* loop_ms, int* steps_ru
 
 tts_status tts_decoder_resident_limits(tts_decoder* d, int* max_batch, int* max_len) {
     TTS_CHECK(d && max_batch && max_len, TTS_ERR_INVALID, "null argument");
-    *max_batch = d->resident ? 1 : 0;
+    *max_batch = d->resident ? (d->rbatch ? std::max(1, std::min(d->Bcap, rb_max_batch())) : 1) : 0;
     *max_len = d->resident ? RES_LMAX : 0;
     return TTS_OK;
 }
@@ -1125,7 +1248,7 @@ void decoder_set_post_hook(tts_decoder* d, void (*fn)(void*, hipStream_t), void*
     d->post_ctx = ctx;
     d->hook_ran = false;
 }
-bool decoder_hook_ran(tts_decoder* d) { return d->hook_ran && d->last_resident; }
+bool decoder_hook_ran(tts_decoder* d) { return d->hook_ran && d->last_resident == 1; }
 void decoder_histories(tts_decoder* d, const float** mel, int64_t* sentence_floats, const int** n_steps) {
     *mel = d->mel_hist;
     *sentence_floats = (int64_t)d->hist_cap * d->nmel;

@@ -152,4 +152,43 @@ hipError_t resident_prepare();
 // co-residency guaranteed or nothing launched (*launched = false): common.h launch_persistent
 hipError_t launch_resident(const ResArgs& a, hipStream_t s, bool* launched);
 
+// ---- resident decoder for batches of 2..RB_MAXB sentences (resident_batch.hip): the same
+// weight-stationary design with both LSTMs' rows in registers and the batch's activations in LDS
+constexpr int RB_MAXB = 4;  // per launch (larger requests: consecutive launches of <= RB_MAXB)
+struct ResBatchArgs {
+    int B, gen;                // sentences, GEN_* bits (resident_batch_supports)
+    int L[RB_MAXB];            // encoder lengths (2..RES_LMAX)
+    int Lcap, nmel, nrows, max_steps, hist_cap, Lalign;
+    long long timeout_ticks;
+    unsigned salt;
+    const float4* wa;          // [256 CU][14][512] 4 gates per k, attention LSTM (resident_batch_pack)
+    const float4* wd;          // [256 CU][20][512] decoder LSTM
+    const float *w2, *b2, *wq, *wf, *bf, *ba, *bd;  // ResWeights' reference-layout rows and biases
+    const float* v;
+    const float* v_b;
+    const float* Pt;           // [B][ADIM][Lcap]
+    const float* enc;          // [B][Lcap][ENC]
+    float *h_att, *c_att, *h_dec, *c_dec, *xa;  // multi-launch state layout ([2][Bcap][.] by parity)
+    int64_t hps, xps;
+    const float* pre1;         // [B][PRE] step-0 prenet layer 1
+    const float* alpha;        // [B][Lcap]
+    const int* nidx;
+    const float* u;
+    const int* flag1;
+    const int* count;
+    int* done;
+    int* n_steps;
+    float* mel_hist;           // [B][hist_cap][nmel]
+    float* stop_hist;          // [B][hist_cap]
+    float* align_hist;         // [B][hist_cap][Lalign]
+    unsigned long long* gran;  // resident_batch_granules() slots
+    int* status;
+};
+void resident_batch_weight_floats(size_t* wa, size_t* wd);
+size_t resident_batch_granules();
+hipError_t resident_batch_pack(const ResSrc& src, float4* wa, float4* wd, hipStream_t s);
+hipError_t resident_batch_prepare();
+bool resident_batch_supports(int gen);
+hipError_t launch_resident_batch(const ResBatchArgs& a, hipStream_t s, bool* launched);
+
 }  // namespace tts

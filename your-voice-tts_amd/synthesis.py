@@ -71,16 +71,24 @@ def wav_to_int16(wav):
 SERIAL_RESIDENT_MAX = int(os.environ.get("TTS_SERIAL_MAX", "3"))
 
 
+def _resident_batch(model, ids_list):
+    """Whether the whole request decodes in one call on a resident decoder (the batch-1 one, or the
+    batch one for 2..max sentences, tts_decoder_resident_limits)."""
+    Lmax = max(len(x) for x in ids_list)
+    mb, ml = model.resident_limits(Lmax)
+    return len(ids_list) <= mb and Lmax <= ml
+
+
 def _serial_eligible(model, ids_list):
     """Whether a request decodes serially on the resident batch-1 decoder: 2..SERIAL_RESIDENT_MAX
-    sentences, each within the length the handle's resident decoder serves now
-    (tts_decoder_resident_limits: no hard-coded limit here)."""
+    sentences the batch decoder does not take, each within the length the handle's resident
+    decoder serves now (tts_decoder_resident_limits: no hard-coded limit here)."""
     B = len(ids_list)
     if B < 2 or B > SERIAL_RESIDENT_MAX:
         return False
     Lmax = max(len(x) for x in ids_list)
     mb, ml = model.resident_limits(Lmax)
-    return mb >= 1 and Lmax <= ml
+    return mb == 1 and Lmax <= ml
 
 
 def _stack(outs, B):
@@ -113,7 +121,7 @@ def _decode(model, ids_list, speaker_ids=None):
     B = len(ids_list)
     if not _serial_eligible(model, ids_list):
         out = model.inference_batch(ids_list, speaker_ids=speaker_ids)
-        out["dispatch"] = "batch"
+        out["dispatch"] = {2: "batch-resident", 1: "batch-resident"}.get(model.last_timing.get("resident_kind", 0), "batch")
         out["decoder_timings"] = [dict(model.last_timing)]
         return out
     from .tacotron2 import _speaker_array
@@ -329,6 +337,11 @@ class Synthesizer:
         tts_synth_run per sentence (encoder -> resident decoder -> postnet -> Griffin-Lim in one
         native call each); larger ones, and the Tacotron family, as one batch (synthesize_batch)."""
         model, ap = self.tts_model, self.ap
+        if not hasattr(model, "linear_dim") and len(ids) > 1 and _resident_batch(model, ids):
+            # the resident batch decoder: the whole request in one tts_synth_run
+            buf = torch.empty(model.native_wav_capacity(ap, len(ids)), dtype=torch.float64, device="cuda")
+            wav, frames = model.synthesize_native(ids, ap, sync=True, out=buf)
+            return wav, [ap.hop_length * (T - 1) for T in frames]
         if not hasattr(model, "linear_dim") and (len(ids) == 1 or _serial_eligible(model, ids)):
             cap = model.native_wav_capacity(ap, 1)
             buf = torch.empty(len(ids), cap, dtype=torch.float64, device="cuda")

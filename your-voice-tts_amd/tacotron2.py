@@ -435,7 +435,7 @@ class Tacotron2:
         lib.tts_decoder_last_path(hdec, ctypes.byref(res))
         lib.tts_encoder_last_path(self._native[3], ctypes.byref(enc))
         return dict(decoder_loop_ms=ms.value, decoder_steps_run=ns.value, resident=bool(res.value),
-                    encoder_resident=bool(enc.value), encoder_path=int(enc.value))
+                    resident_kind=int(res.value), encoder_resident=bool(enc.value), encoder_path=int(enc.value))
 
     RESIDENT_PHASES = ("att_early_wait_pre1", "prenet2_row", "wait_prenet2", "att_lstm_prenet", "att_cell_gather",
                        "query_dec_early", "wait_query", "energies_max", "weights_ctx_publish", "next_prefetch",
