@@ -77,9 +77,19 @@ tts_status gl_collect(tts_gl* g);  // waits for a pending run, sets its timing, 
 bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters);  // (caches per-F checks in g)
 // phase_mt.hip: numpy's legacy np.random.rand(1025, F[b]) draws for b = 0..B-1 in order, continued
 // on the device from the MT19937 state `state` ([dev] 624 key words + position, updated in place)
-// into out [dev] fp64 [B][1025][Fmax] (one workgroup; F_dev on the device, read on stream s)
+// into out [dev] fp64 [B][1025][Fmax] (F_dev on the device, read on stream s).  The stream is cut into
+// chunks of MT_CHUNK_BLOCKS key blocks, each started by a GF(2) jump-ahead and generated by its own
+// workgroup; `w` holds the caller's device workspace (grown on demand; the caller orders reuse).
 constexpr int MT_MAX_BATCH = 1024;
-hipError_t mt_draw_phases(unsigned* state, const int* F_dev, int B, int Fmax, double* out, hipStream_t s);
+struct MtWork {
+    unsigned* xs = nullptr;             // the raw word stream, [blocks][624]
+    size_t xs_words = 0;
+    unsigned long long* polys = nullptr;  // jump polynomials of chunks 1.., [n][312]
+    int npolys = 0;
+    long long* meta = nullptr;          // position, draws, last block, sentence offsets
+};
+hipError_t mt_draw_phases(unsigned* state, const int* F_dev, int B, int Fmax, double* out, MtWork* w, hipStream_t s);
+void mt_work_free(MtWork* w);
 // wav_io.hip: Synthesizer.tts's join + save_wav's int16 conversion (tts_gl_save_pcm16's body)
 hipError_t pcm16_join(const double* wav, int64_t pitch, const int64_t* start_dev, int64_t total, int B, int gap,
                       double peak, unsigned long long* peak_bits, int16_t* out, hipStream_t s);

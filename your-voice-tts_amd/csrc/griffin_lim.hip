@@ -1863,6 +1863,7 @@ struct tts_gl {
     int mt_F_n = 0;
     hipStream_t mt_stream = nullptr;
     hipEvent_t ev_mt = nullptr;
+    MtWork mt_work;                // the draws' device workspace (phase_mt.hip)
     // tts_gl_save_pcm16: the peak word and the output offsets ([dev], host copy kept for the upload)
     unsigned long long* pcm_peak = nullptr;
     int64_t* pcm_start = nullptr;
@@ -1877,6 +1878,7 @@ void tts_gl_destroy(tts_gl* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     if (g->ev_done) (void)hipEventSynchronize(g->ev_done);  // a pipeline run on another stream
     if (g->mt_stream) (void)hipEventSynchronize(g->ev_mt);  // the last numpy-stream phase draw
+    mt_work_free(&g->mt_work);
     for (auto& kv : g->graphs) (void)hipGraphExecDestroy(kv.second);
     for (void* p : {(void*)g->win, (void*)g->win2, (void*)g->pinv, (void*)g->tw, (void*)g->S, (void*)g->frames,
                     (void*)g->y, (void*)g->F, (void*)g->basis, (void*)g->NS, (void*)g->flags, (void*)g->pstatus, (void*)g->pgr, (void*)g->wt, (void*)g->winc,
@@ -2116,7 +2118,7 @@ bool gl_persistent_path(tts_gl* g, int B, int Fmax, int frames_total, int iters)
 static tts_status mt_draw(tts_gl* g, const int* F_dev, int B, int Fmax, double* out, hipStream_t s) {
     TTS_CHECK(B <= MT_MAX_BATCH, TTS_ERR_UNSUPPORTED, "numpy-stream phases: at most 1024 sentences per run");
     if (g->mt_stream && g->mt_stream != s) TTS_HIP(hipStreamWaitEvent(s, g->ev_mt, 0));
-    TTS_HIP(mt_draw_phases(g->mt_state, F_dev, B, Fmax, out, s));
+    TTS_HIP(mt_draw_phases(g->mt_state, F_dev, B, Fmax, out, &g->mt_work, s));
     TTS_HIP(hipEventRecord(g->ev_mt, s));
     g->mt_stream = s;
     return TTS_OK;

@@ -15,22 +15,39 @@
 // in place when exhausted (mt19937_gen); each output word is the key word tempered; a double is
 // ((w0 >> 5) * 2^26 + (w1 >> 6)) / 2^53 from two consecutive words (mt19937_next_double).  Viewed
 // as one sequence x[0..] (x[0..623] = the current key), the twist is x[n] = x[n-227] ^
-// mix(x[n-624], x[n-623]): a whole block depends only on the previous block, except through the
-// x[n-227] chain inside it.  One workgroup therefore produces a block per step: thread t < 227
-// computes the chain t, t + 227, t + 454 from the previous block (LDS), thread 169 also recomputes
-// the block's first word for its last one (x[n+623] needs x[n]); blocks rotate through three LDS
-// buffers so that the pairs straddling a block boundary (odd start position) can be converted
-// while the next block is generated, with ONE barrier per 624 words.  The chain is sequential by
-// construction (~10k block steps per 3000-frame sentence); the conversion to doubles and the
-// scatter into [b][bin][frame] ride along in the same steps.
+// mix(x[n-624], x[n-623]): a block depends only on the previous block (and on the x[n-227] chain
+// inside it), so one workgroup produces a block per barrier, ~0.75 us each: 7.4 ms for one
+// 3000-frame sentence (6.15 M words) when the whole draw ran in one workgroup (round-6 profile).
+//
+// The draw is cut instead into chunks of MT_CHUNK key blocks that run on their own workgroups:
+//   mt_prefix_kernel  one workgroup: sentence offsets, the last block K, key blocks 1..32;
+//   mt_chunk_kernel   chunk k >= 1 jumps to key block k * MT_CHUNK: with r_k = x^(624 MT_CHUNK k)
+//                     mod phi (mt_jump.cpp, host, once per process), that block is the XOR of the
+//                     624-word windows x[i..i+623] of the prefix at the set bits i of r_k (Cayley-
+//                     Hamilton on the stream's linear step), then twists its MT_CHUNK blocks; chunk 0
+//                     continues the prefix;
+//   mt_emit_kernel    every double from two tempered words, scattered to [b][bin][frame], and the
+//                     state numpy holds afterwards (the key block holding the last word, position).
+#include <algorithm>
+#include <vector>
+
 #include "common.h"
 
 namespace tts {
 namespace {
 
 constexpr int MT_N = 624, MT_M = 397, MT_K = MT_N - MT_M;  // 227
-constexpr int MT_THREADS = 256;
-constexpr int MT_NB = 1025;  // rows of one draw: np.random.rand(n_fft / 2 + 1, T)
+constexpr int MT_NB = 1025;   // rows of one draw: np.random.rand(n_fft / 2 + 1, T)
+constexpr int MT_DEG = 19937;
+constexpr int MT_PW = (MT_DEG + 63) / 64;  // 312 words per jump polynomial
+constexpr int MT_PFX = 33;     // prefix key blocks 0..32: words 0 .. 20591 >= 19936 + 623
+constexpr int MT_CHUNK = 48;   // key blocks per chunk
+constexpr int PFX_THREADS = 256, CHUNK_THREADS = 1024, EMIT_THREADS = 256;
+constexpr int CHUNK_WAVES = CHUNK_THREADS / 64;
+constexpr size_t CHUNK_SMEM = (size_t)(MT_PFX * MT_N + CHUNK_WAVES * MT_N) * sizeof(unsigned);
+// meta: [0] position, [1] doubles drawn, [2] the block K holding the last word, [3 + b] offset of
+// sentence b's draws (b <= B)
+constexpr int META_OFF = 3;
 
 __device__ __forceinline__ unsigned mt_mix(unsigned a, unsigned b) {
     const unsigned y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -43,93 +60,187 @@ __device__ __forceinline__ unsigned mt_temper(unsigned y) {
     y ^= y >> 18;
     return y;
 }
+// the block after o into n: thread t < 227 computes words t, t + 227, t + 454 (the x[n-227] chain);
+// word 623 needs the new word 0, which thread 169 recomputes
+__device__ __forceinline__ void mt_twist(const unsigned* o, unsigned* n, int t) {
+    if (t >= MT_K) return;
+    const unsigned x0 = o[t + MT_M] ^ mt_mix(o[t], o[t + 1]);
+    const unsigned x1 = x0 ^ mt_mix(o[t + MT_K], o[t + MT_K + 1]);
+    n[t] = x0;
+    n[t + MT_K] = x1;
+    if (t + 2 * MT_K < MT_N) {
+        const int i2 = t + 2 * MT_K;
+        const unsigned nxt = i2 < MT_N - 1 ? o[i2 + 1] : o[MT_M] ^ mt_mix(o[0], o[1]);
+        n[i2] = x1 ^ mt_mix(o[i2], nxt);
+    }
+}
 
-struct MtArgs {
-    unsigned* state;  // [625] key[624], pos: read, then overwritten with the state after the draws
-    const int* F;     // [dev] frames per sentence (0 allowed: no draw)
-    int B, Fmax;
-    double* out;      // [B][1025][Fmax]: sentence b's draw at [b][k][f] for f < F[b]
-};
-
-__global__ __launch_bounds__(MT_THREADS) void mt_phase_kernel(const MtArgs a) {
-    __shared__ unsigned R[3][MT_N];
-    __shared__ long long off[MT_MAX_BATCH + 1];
-    __shared__ int Fs[MT_MAX_BATCH];
+__global__ __launch_bounds__(PFX_THREADS) void mt_prefix_kernel(const unsigned* state, const int* F, int B,
+                                                                 long long* meta, unsigned* xs) {
+    __shared__ unsigned R[2][MT_N];
+    __shared__ long long sK;
     const int tid = threadIdx.x;
-    for (int i = tid; i < MT_N; i += MT_THREADS) R[0][i] = a.state[i];
-    const long long pos = (long long)a.state[MT_N];
     if (tid == 0) {
         long long acc = 0;
-        for (int b = 0; b < a.B; ++b) {
-            off[b] = acc;
-            Fs[b] = a.F[b];
-            acc += (long long)MT_NB * a.F[b];
+        for (int b = 0; b < B; ++b) {
+            meta[META_OFF + b] = acc;
+            acc += (long long)MT_NB * F[b];
         }
-        off[a.B] = acc;
+        meta[META_OFF + B] = acc;
+        const long long pos = (long long)state[MT_N];
+        const long long K = acc > 0 ? (pos + 2 * acc - 1) / MT_N : 0;
+        meta[0] = pos;
+        meta[1] = acc;
+        meta[2] = K;
+        sK = K;
+    }
+    for (int i = tid; i < MT_N; i += PFX_THREADS) {
+        R[0][i] = state[i];
+        xs[i] = state[i];
     }
     __syncthreads();
-    const long long D = off[a.B];  // doubles drawn
-    if (D == 0) return;            // the state stays as it is
-    const long long e = pos + 2 * D;         // the first word not consumed
-    const long long K = (e - 1) / MT_N;      // the block holding the last consumed word
-    // doubles j whose second word p + 2j + 1 lies in block kb (its first word may be the previous
-    // block's last, whose buffer is intact: blocks rotate through three buffers)
-    auto emit = [&](long long kb) {
-        const long long base = kb * MT_N;
-        long long jlo = base - pos - 1;
-        jlo = jlo <= 0 ? 0 : (jlo + 1) >> 1;
-        const long long hi = base + MT_N - 2 - pos;
-        if (hi < 0) return;
-        const long long jhi = min(hi >> 1, D - 1);
-        const unsigned* cur = R[kb % 3];
-        const unsigned* prv = R[(kb + 2) % 3];
-        for (long long j = jlo + tid; j <= jhi; j += MT_THREADS) {
-            const int r0 = (int)(pos + 2 * j - base);  // in [-1, 622]
-            const unsigned w0 = r0 < 0 ? prv[MT_N - 1] : cur[r0];
-            const unsigned w1 = cur[r0 + 1];
-            const double u = ((double)(mt_temper(w0) >> 5) * 67108864.0 + (double)(mt_temper(w1) >> 6)) *
-                             (1.0 / 9007199254740992.0);
-            int lo = 0, up = a.B - 1;  // the sentence: off[b] <= j < off[b + 1]
-            while (lo < up) {
-                const int mid = (lo + up + 1) >> 1;
-                if (off[mid] <= j) lo = mid;
-                else up = mid - 1;
-            }
-            const int local = (int)(j - off[lo]);
-            const int fb = Fs[lo];
-            const int k = local / fb, f = local - k * fb;
-            a.out[((long long)lo * MT_NB + k) * a.Fmax + f] = u;
-        }
-    };
-    emit(0);
-    for (long long kb = 0; kb < K; ++kb) {
-        const unsigned* o = R[kb % 3];
-        unsigned* n = R[(kb + 1) % 3];
-        if (tid < MT_K) {
-            const int t = tid;
-            const unsigned x0 = o[t + MT_M] ^ mt_mix(o[t], o[t + 1]);  // word t (< 227): old t + 397
-            const unsigned x1 = x0 ^ mt_mix(o[t + MT_K], o[t + MT_K + 1]);  // word t + 227: new t
-            n[t] = x0;
-            n[t + MT_K] = x1;
-            if (t + 2 * MT_K < MT_N) {  // word t + 454 (t <= 169): new t + 227
-                const int i2 = t + 2 * MT_K;
-                const unsigned nxt = i2 < MT_N - 1 ? o[i2 + 1] : o[MT_M] ^ mt_mix(o[0], o[1]);  // word 623: new 0
-                n[i2] = x1 ^ mt_mix(o[i2], nxt);
-            }
-        }
+    const long long np = min(sK, (long long)(MT_PFX - 1));
+    for (long long kb = 0; kb < np; ++kb) {
+        const unsigned* o = R[kb & 1];
+        unsigned* n = R[(kb + 1) & 1];
+        mt_twist(o, n, tid);
         __syncthreads();
-        emit(kb + 1);
+        for (int i = tid; i < MT_N; i += PFX_THREADS) xs[(kb + 1) * MT_N + i] = n[i];
     }
-    for (int i = tid; i < MT_N; i += MT_THREADS) a.state[i] = R[K % 3][i];
-    if (tid == 0) a.state[MT_N] = (unsigned)(e - K * MT_N);
+}
+
+__global__ __launch_bounds__(CHUNK_THREADS) void mt_chunk_kernel(const long long* meta, unsigned* xs,
+                                                                 const unsigned long long* polys) {
+    extern __shared__ unsigned smt[];
+    const long long K = meta[2];
+    const int k = blockIdx.x;
+    const long long s = k == 0 ? min(K, (long long)(MT_PFX - 1)) : (long long)k * MT_CHUNK;
+    const long long e = min(K, (long long)(k + 1) * MT_CHUNK);
+    if (s >= e) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned* R0 = smt;  // two block buffers (over the prefix copy once the jump is done)
+    if (k == 0) {
+        for (int i = tid; i < MT_N; i += CHUNK_THREADS) R0[i] = xs[s * MT_N + i];
+    } else {
+        unsigned* X = smt;
+        unsigned* part = smt + MT_PFX * MT_N;
+        for (int i = tid; i < MT_PFX * MT_N; i += CHUNK_THREADS) X[i] = xs[i];
+        __syncthreads();
+        // key block k * MT_CHUNK = XOR over the set bits i of r_k of x[i .. i + 623]; wave wv takes
+        // the polynomial's words [w0, w1), lane l the window words l + 64 g
+        const unsigned long long* c = polys + (size_t)(k - 1) * MT_PW;
+        const int w0 = wv * MT_PW / CHUNK_WAVES, w1 = (wv + 1) * MT_PW / CHUNK_WAVES;
+        unsigned acc[10];
+#pragma unroll
+        for (int g = 0; g < 10; ++g) acc[g] = 0u;
+        for (int wi = w0; wi < w1; ++wi) {
+            unsigned long long bits = c[wi];
+            while (bits) {
+                const int i = wi * 64 + __builtin_ctzll(bits);
+                bits &= bits - 1;
+#pragma unroll
+                for (int g = 0; g < 9; ++g) acc[g] ^= X[i + lane + 64 * g];
+                if (lane < MT_N - 576) acc[9] ^= X[i + lane + 576];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 9; ++g) part[wv * MT_N + lane + 64 * g] = acc[g];
+        if (lane < MT_N - 576) part[wv * MT_N + lane + 576] = acc[9];
+        __syncthreads();
+        for (int w = tid; w < MT_N; w += CHUNK_THREADS) {
+            unsigned v = 0u;
+            for (int q = 0; q < CHUNK_WAVES; ++q) v ^= part[q * MT_N + w];
+            R0[w] = v;  // (the prefix copy is no longer read)
+        }
+    }
+    __syncthreads();
+    for (long long kb = s; kb < e; ++kb) {
+        const unsigned* o = R0 + ((kb - s) & 1) * MT_N;
+        unsigned* n = R0 + (((kb - s) + 1) & 1) * MT_N;
+        mt_twist(o, n, tid);
+        __syncthreads();
+        for (int i = tid; i < MT_N; i += CHUNK_THREADS) xs[(kb + 1) * MT_N + i] = n[i];
+    }
+}
+
+__global__ __launch_bounds__(EMIT_THREADS) void mt_emit_kernel(const long long* meta, const int* F, const unsigned* xs,
+                                                               double* out, int Fmax, unsigned* state) {
+    const int b = blockIdx.y;
+    const int fb = F[b];
+    const long long pos = meta[0];
+    const int local = blockIdx.x * EMIT_THREADS + threadIdx.x;
+    if (local < MT_NB * fb) {
+        const long long p = pos + 2 * (meta[META_OFF + b] + local);
+        const double u = ((double)(mt_temper(xs[p]) >> 5) * 67108864.0 + (double)(mt_temper(xs[p + 1]) >> 6)) *
+                         (1.0 / 9007199254740992.0);
+        const int kk = local / fb, f = local - kk * fb;
+        out[((long long)b * MT_NB + kk) * Fmax + f] = u;
+    }
+    if (blockIdx.x == 0 && b == 0) {
+        const long long D = meta[1];
+        if (D > 0) {  // numpy's state after the draw: the key block holding the last word, its position
+            const long long K = meta[2];
+            for (int i = threadIdx.x; i < MT_N; i += EMIT_THREADS) state[i] = xs[K * MT_N + i];
+            if (threadIdx.x == 0) state[MT_N] = (unsigned)(pos + 2 * D - K * MT_N);
+        }
+    }
 }
 
 }  // namespace
 
-hipError_t mt_draw_phases(unsigned* state, const int* F_dev, int B, int Fmax, double* out, hipStream_t s) {
-    if (B < 1 || B > MT_MAX_BATCH) return hipErrorInvalidValue;
-    MtArgs a{state, F_dev, B, Fmax, out};
-    hipLaunchKernelGGL(mt_phase_kernel, dim3(1), dim3(MT_THREADS), 0, s, a);
+bool mt_jump_polys(int chunk_blocks, int n, std::vector<unsigned long long>* out);  // mt_jump.cpp
+
+void mt_work_free(MtWork* w) {
+    for (void* p : {(void*)w->xs, (void*)w->polys, (void*)w->meta})
+        if (p) (void)hipFree(p);
+    *w = MtWork{};
+}
+
+hipError_t mt_draw_phases(unsigned* state, const int* F_dev, int B, int Fmax, double* out, MtWork* w, hipStream_t s) {
+    if (B < 1 || B > MT_MAX_BATCH || Fmax < 0) return hipErrorInvalidValue;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mt_chunk_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHUNK_SMEM);
+    if (attr != hipSuccess) return attr;
+    // bounds from Fmax (the frame counts are on the device): position <= 624
+    const long long Dmax = (long long)B * MT_NB * Fmax;
+    const long long Kmax = (MT_N + 2 * Dmax - 1) / MT_N;
+    const int nchunks = Kmax > MT_PFX - 1 ? (int)((Kmax - 1) / MT_CHUNK) + 1 : 0;
+    const size_t words = (size_t)std::max<long long>(Kmax + 1, MT_PFX) * MT_N;
+    const bool grow_xs = words > w->xs_words, grow_meta = !w->meta, grow_polys = nchunks - 1 > w->npolys;
+    if (grow_xs || grow_meta || grow_polys) {
+        hipError_t e = hipStreamSynchronize(s);  // earlier draws on s may still read the workspace
+        if (e != hipSuccess) return e;
+    }
+    if (grow_meta) {
+        hipError_t e = hipMalloc(&w->meta, sizeof(long long) * (META_OFF + MT_MAX_BATCH + 1));
+        if (e != hipSuccess) return e;
+    }
+    if (grow_xs) {
+        if (w->xs) (void)hipFree(w->xs);
+        w->xs = nullptr;
+        w->xs_words = 0;
+        hipError_t e = hipMalloc(&w->xs, words * sizeof(unsigned));
+        if (e != hipSuccess) return e;
+        w->xs_words = words;
+    }
+    if (grow_polys) {
+        std::vector<unsigned long long> h;
+        if (!mt_jump_polys(MT_CHUNK, nchunks - 1, &h)) return hipErrorNotSupported;
+        if (w->polys) (void)hipFree(w->polys);
+        w->polys = nullptr;
+        w->npolys = 0;
+        hipError_t e = hipMalloc(&w->polys, h.size() * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemcpy(w->polys, h.data(), h.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return e;
+        w->npolys = nchunks - 1;
+    }
+    hipLaunchKernelGGL(mt_prefix_kernel, dim3(1), dim3(PFX_THREADS), 0, s, state, F_dev, B, w->meta, w->xs);
+    if (nchunks > 0)
+        hipLaunchKernelGGL(mt_chunk_kernel, dim3(nchunks), dim3(CHUNK_THREADS), CHUNK_SMEM, s, w->meta, w->xs,
+                           w->polys);
+    const int gx = (int)std::max<long long>(1, (MT_NB * (long long)Fmax + EMIT_THREADS - 1) / EMIT_THREADS);
+    hipLaunchKernelGGL(mt_emit_kernel, dim3(gx, B), dim3(EMIT_THREADS), 0, s, w->meta, F_dev, w->xs, out, Fmax, state);
     return hipGetLastError();
 }
 
