@@ -111,6 +111,7 @@ struct tts_decoder {
     bool rbatch = false;
     int rb_gen = 0;
     float4 *rb_wa = nullptr, *rb_wd = nullptr;
+    long long* rb_prof = nullptr;           // TTS_RB_PROF=1 phase clocks
     unsigned long long* rb_gran = nullptr;  // resident_batch_granules() slots, then int status[4]
     unsigned rb_salt = 0;
     int rb_place_fails = 0;
@@ -841,6 +842,10 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
     // consecutive launches of <= RB_MAXB sentences beat the multi-launch step (~45 us at any batch up
     // to 64) only for a few groups: TTS_RB_MAX (default rb_max_batch()) bounds the batch
     bool rb_ok = d->rbatch && B >= 2 && B <= rb_max_batch() && !keep;
+    static const bool rb_prof = [] {
+        const char* v = getenv("TTS_RB_PROF");
+        return v && v[0] == '1';
+    }();
     for (int b = 0; rb_ok && b < B; ++b) rb_ok = lens[b] <= RES_LMAX;
     if (rb_ok) {
         // batches: one persistent launch per group of <= RB_MAXB sentences (resident_batch.hip),
@@ -874,6 +879,11 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             rb.align_hist = d->align_hist + (size_t)g0 * d->hist_cap * Lmax;
             rb.gran = d->rb_gran;
             rb.status = reinterpret_cast<int*>(d->rb_gran + resident_batch_granules());
+            if (rb_prof && !d->rb_prof) {
+                tts_status ps = dmalloc(d, &d->rb_prof, (size_t)RES_CUS * 4 * RB_PROF_SLOTS);
+                if (ps) return ps;
+            }
+            rb.prof = rb_prof ? d->rb_prof : nullptr;
             bool wrapped = false;
             d->rb_salt = res_next_salt(d->rb_salt, &wrapped);
             rb.salt = d->rb_salt;
@@ -903,6 +913,29 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                 break;
             }
             d->rb_place_fails = 0;
+            if (rb_prof) {
+                // TTS_RB_PROF=1: microseconds per step of each phase (wall clock 100 MHz) for every wave
+                // index: min / mean / max over the 256 CUs, and CU 0
+                std::vector<long long> pk((size_t)RES_CUS * 4 * RB_PROF_SLOTS);
+                TTS_HIP(hipMemcpy(pk.data(), rb.prof, pk.size() * sizeof(long long), hipMemcpyDeviceToHost));
+                const double steps = pk[RB_PROF_SLOTS - 1] > 0 ? (double)pk[RB_PROF_SLOTS - 1] : 1.0;
+                fprintf(stderr, "[tts] resident batch nb=%d steps=%lld (us/step per phase: min/mean/max over CUs)\n", nb,
+                        pk[RB_PROF_SLOTS - 1]);
+                for (int w = 0; w < 4; ++w) {
+                    fprintf(stderr, "[tts]  wave %d:", w);
+                    for (int k = 0; k < 13; ++k) {
+                        double mn = 1e30, mx = 0, sum = 0;
+                        for (int cu = 0; cu < RES_CUS; ++cu) {
+                            const double v = pk[((size_t)cu * 4 + w) * RB_PROF_SLOTS + k] * 0.01 / steps;
+                            mn = std::min(mn, v);
+                            mx = std::max(mx, v);
+                            sum += v;
+                        }
+                        fprintf(stderr, " %d:%.2f/%.2f/%.2f", k, mn, sum / RES_CUS, mx);
+                    }
+                    fprintf(stderr, "\n");
+                }
+            }
         }
         if (all) {
             if (timed) TTS_HIP(hipEventRecord(d->ev_t1, s));

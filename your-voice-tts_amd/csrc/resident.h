@@ -161,8 +161,8 @@ struct ResBatchArgs {
     int Lcap, nmel, nrows, max_steps, hist_cap, Lalign;
     long long timeout_ticks;
     unsigned salt;
-    const float4* wa;          // [256 CU][14][512] 4 gates per k, attention LSTM (resident_batch_pack)
-    const float4* wd;          // [256 CU][20][512] decoder LSTM
+    const float4* wa;          // [256 CU][28][256 threads] 4 gates per k, attention LSTM (resident_batch_pack)
+    const float4* wd;          // [256 CU][40][256 threads] decoder LSTM
     const float *w2, *b2, *wq, *wf, *bf, *ba, *bd;  // ResWeights' reference-layout rows and biases
     const float* v;
     const float* v_b;
@@ -183,7 +183,9 @@ struct ResBatchArgs {
     float* align_hist;         // [B][hist_cap][Lalign]
     unsigned long long* gran;  // resident_batch_granules() slots
     int* status;
+    long long* prof;           // [256 CU][4 waves][RB_PROF_SLOTS] phase clocks (TTS_RB_PROF=1), else null
 };
+constexpr int RB_PROF_SLOTS = 16;
 void resident_batch_weight_floats(size_t* wa, size_t* wd);
 size_t resident_batch_granules();
 hipError_t resident_batch_pack(const ResSrc& src, float4* wa, float4* wd, hipStream_t s);

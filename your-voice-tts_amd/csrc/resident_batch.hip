@@ -69,33 +69,64 @@ struct Lds {
     static constexpr int GSUM = GW + NB * 2 * GW_PAD;      // [4 units][4 NB]
     static constexpr int RM = GSUM + 4 * 4 * NB;           // mel row c [6][64] float4 + stop row [6][64] float4
     static constexpr int INTS = RM + 2 * 6 * 64 * 4;       // [0, 8) flags, [8, 16) active, [16, 24) flag1, [24, 32) count
-    static constexpr int TOTAL = INTS + 32;
+    static constexpr int ENC_L = NB == 2 ? RES_LMAX : 128;  // positions of the context channels held in LDS
+    static constexpr int ENCS = INTS + 32;                 // [NB][ENC_L][16] the CU's context channels
+    static constexpr int WDC = ENCS + NB * ENC_L * 16;     // [8][256 threads] float4: decoder LSTM ctx part
+    static constexpr int WQ = WDC + 8 * RB_THREADS * 4;    // [4 waves][1024] the waves' query rows
+    static constexpr int TOTAL = WQ + 4 * HATT;
 };
 
 // The transpose reduction: V values per lane summed over the 64 lanes of the wave; lane l ends with
-// the total of value index l >> (6 - log2 V).  Each xor level halves the values a lane keeps: it
-// keeps one half and adds its partner's copy of the same half.  (Lane selects by bit masks, not
-// `up ? v[i] : v[h + i]`: the compiler turns a select of two array elements into a select of their
-// addresses, which sends the array to scratch memory.)
+// the total of value index l >> (6 - log2 V).  Each level halves the values a lane keeps: it keeps
+// one half and adds its partner's copy of the same half.  No LDS crossbar: the 32- and 16-lane
+// levels are gfx950's v_permlane32_swap / v_permlane16_swap (one instruction exchanges a value pair
+// between the two halves), the lower ones DPP (row_ror:8, row_half_mirror, quad_perm xor 2 / xor 1;
+// the half mirror pairs lane i with 7 - i, opposite in bit 2 and equal above it, which is all the
+// reduction needs).  (Lane selects by bit masks, not `up ? v[i] : v[h + i]`: the compiler turns a
+// select of two array elements into a select of their addresses, which sends the array to scratch.)
+template <int M>
+__device__ __forceinline__ float xpartner(float x) {
+    static_assert(M == 8 || M == 4 || M == 2 || M == 1, "DPP levels");
+    return M == 8 ? dpp_move<0x128, 0xf>(x, 0.f)    // row_ror:8
+         : M == 4 ? dpp_move<0x141, 0xf>(x, 0.f)    // row_half_mirror
+         : M == 2 ? dpp_move<0x4E, 0xf>(x, 0.f)     // quad_perm [2,3,0,1]
+                  : dpp_move<0xB1, 0xf>(x, 0.f);    // quad_perm [1,0,3,2]
+}
+// lanes with bit M clear keep lo, the others hi; returns keep + the partner's copy of it
+template <int M>
+__device__ __forceinline__ float xlevel(float lo, float hi) {
+    if constexpr (M == 32 || M == 16) {
+        const auto r = M == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false)
+                               : __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+        return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    } else {
+        const unsigned msk = (threadIdx.x & M) ? 0xffffffffu : 0u;
+        const unsigned l = __float_as_uint(lo), h = __float_as_uint(hi);
+        const float send = __uint_as_float((l & msk) | (h & ~msk));
+        const float keep = __uint_as_float((h & msk) | (l & ~msk));
+        return keep + xpartner<M>(send);
+    }
+}
+template <int LEV, int V>
+__device__ __forceinline__ void xstep(float (&v)[V]) {
+    constexpr int M = 32 >> LEV;
+    constexpr int H = (V >> LEV) >> 1;
+    if constexpr (H >= 1) {
+#pragma unroll
+        for (int i = 0; i < H; ++i) v[i] = xlevel<M>(v[i], v[H + i]);
+    } else {
+        v[0] = xlevel<M>(v[0], v[0]);  // one value left: a plain butterfly sum
+    }
+}
 template <int V>
 __device__ __forceinline__ float xreduce(float (&v)[V]) {
-    const int lane = threadIdx.x & 63;
-    constexpr int LV = V == 32 ? 5 : V == 16 ? 4 : V == 8 ? 3 : V == 4 ? 2 : V == 2 ? 1 : 0;
-#pragma unroll
-    for (int lev = 0; lev < LV; ++lev) {
-        const int m = 32 >> lev;
-        const int h = (V >> lev) >> 1;
-        const unsigned msk = (lane & m) ? 0xffffffffu : 0u;
-#pragma unroll
-        for (int i = 0; i < h; ++i) {
-            const unsigned lo = __float_as_uint(v[i]), hi = __float_as_uint(v[h + i]);
-            const float send = __uint_as_float((lo & msk) | (hi & ~msk));
-            const float keep = __uint_as_float((hi & msk) | (lo & ~msk));
-            v[i] = keep + __shfl_xor(send, m, 64);
-        }
-    }
-#pragma unroll
-    for (int lev = LV; lev < 6; ++lev) v[0] += __shfl_xor(v[0], 32 >> lev, 64);
+    static_assert(V == 1 || V == 2 || V == 4 || V == 8 || V == 16 || V == 32, "power of two");
+    xstep<0>(v);
+    xstep<1>(v);
+    xstep<2>(v);
+    xstep<3>(v);
+    xstep<4>(v);
+    xstep<5>(v);
     return v[0];
 }
 
@@ -120,27 +151,30 @@ __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
 }
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// Poll npairs consecutive granule pairs from even slot `base`, thread i taking pairs i, i + 256, ...,
-// writing the values to dst[2p], dst[2p + 1] on every poll (the last, successful one leaves them).
-// Every wave spins until its pairs carry `tag`; false after the timeout.
-template <int MAXP>
-__device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base, int npairs, unsigned tag, float* dst,
-                                             long long tmo) {
+// Poll NP consecutive granule pairs from even slot `base` (thread i: pairs i, i + 256, ...): every
+// poll issues all of the thread's loads before one wait; the values go to dst[2p], dst[2p + 1]
+// once every pair of the wave carries `tag`.  false after the timeout.
+template <int NP>
+__device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base, unsigned tag, float* dst, long long tmo) {
+    static_assert(NP % RB_THREADS == 0, "whole pairs per thread");
+    constexpr int MAXP = NP / RB_THREADS;
     const int tid = threadIdx.x;
     long long t_end = 0;
     for (int spin = 0;; ++spin) {
+        u32x4 x[MAXP];
+#pragma unroll
+        for (int i = 0; i < MAXP; ++i)
+            x[i] = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (base + 2 * (tid + i * RB_THREADS)) * 8, 0, SC1_VOLATILE));
         bool ok = true;
 #pragma unroll
-        for (int i = 0; i < MAXP; ++i) {
-            const int p = tid + i * RB_THREADS;
-            if (p < npairs) {
-                const u32x4 x =
-                    __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (base + 2 * p) * 8, 0, SC1_VOLATILE));
-                *reinterpret_cast<float2*>(dst + 2 * p) = float2{__uint_as_float(x.x), __uint_as_float(x.z)};
-                ok = ok && x.y == tag && x.w == tag;
-            }
+        for (int i = 0; i < MAXP; ++i) ok = ok && x[i].y == tag && x[i].w == tag;
+        if (__all(ok)) {
+#pragma unroll
+            for (int i = 0; i < MAXP; ++i)
+                *reinterpret_cast<float2*>(dst + 2 * (tid + i * RB_THREADS)) = float2{__uint_as_float(x[i].x), __uint_as_float(x[i].z)};
+            return true;
         }
-        if (__all(ok)) return true;
         if (spin == 0) {
             t_end = (long long)wall_clock64() + tmo;
         } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
@@ -149,7 +183,7 @@ __device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base,
     }
 }
 
-template <int NB>
+template <int NB, bool PROF>
 __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const ResBatchArgs a) {
     using S = Lds<NB>;
     constexpr int V = 4 * NB;  // partial sums per lane (sentence x gate)
@@ -171,6 +205,17 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     int* act = ints + 8;      // sentence b decodes this step
     int* sflag1 = ints + 16;  // stop rule state (the stop CU)
     int* scount = ints + 24;
+    // phase clocks (PROF builds): lane 0 of every wave
+    long long ptk[RB_PROF_SLOTS] = {}, tprev = 0;
+    auto mark = [&](int k) {
+        if constexpr (PROF) {
+            if (lane == 0) {
+                const long long now = (long long)wall_clock64();
+                ptk[k] += now - tprev;
+                tprev = now;
+            }
+        }
+    };
 
     // ---- weights (once per launch): the 4 gates at each k of this lane's slice
     float4 wa[KA], wd[KD];
@@ -180,7 +225,10 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         for (int j = 0; j < KA; ++j) wa[j] = p[(size_t)j * RB_THREADS];
         const float4* q = a.wd + (size_t)c * KD * RB_THREADS + tid;
 #pragma unroll
-        for (int j = 0; j < KD; ++j) wd[j] = q[(size_t)j * RB_THREADS];
+        for (int j = 0; j < KD; ++j)
+            if (j < 16 || j >= 24) wd[j] = q[(size_t)j * RB_THREADS];
+        // the context part (j = 16..23) lives in LDS: read once per step, in phase 10
+        for (int j = 0; j < 8; ++j) reinterpret_cast<float4*>(sm + S::WDC)[j * RB_THREADS + tid] = q[(size_t)(16 + j) * RB_THREADS];
     }
     constexpr int KF = HDEC + ENC;
     if (wave == 1 && c < a.nmel)
@@ -253,10 +301,15 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     const bool xlog = xcc == flags[4];  // the XCD whose copies write the outputs
     const bool stop_cu = rank == 0;
     // this wave's prenet-2 / prenet-1 rows of the XCD's copies (8 per CU, 2 per wave) and query row
+    // (the query row's weights stay in registers; the prenet-1 rows' are fetched from the XCD's L2
+    // each step while the h_dec hand-off is in flight)
     const int r0 = 8 * rank + 2 * wave;
     const float4 wp0 = ld4(a.w2 + r0 * PRE + lane * 4), wp1 = ld4(a.w2 + (r0 + 1) * PRE + lane * 4);
     const float bp1a = a.bf[a.nmel + r0], bp1b = a.bf[a.nmel + r0 + 1], bp2a = a.b2[r0], bp2b = a.b2[r0 + 1];
     const int qrow = 4 * rank + wave;
+    const float* wql = sm + S::WQ + wave * HATT + lane * 4;
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(sm + S::WQ + wave * HATT + i * 256 + lane * 4) = ld4(a.wq + qrow * HATT + i * 256 + lane * 4);
+    const float* w1a = a.wf + (size_t)(a.nmel + r0) * KF + lane * 4;
     if (stop_cu && wave == 3)
         for (int i = 0; i < 6; ++i)
             reinterpret_cast<float4*>(rm)[(6 + i) * 64 + lane] = ld4(a.wf + (size_t)(a.nmel + PRE) * KF + i * 256 + lane * 4);
@@ -279,6 +332,10 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             gw[(ab * 2) * GW_PAD + k] = j >= 0 && j < Lb ? a.alpha[(size_t)ab * a.Lcap + j] : 0.f;
             gw[(ab * 2 + 1) * GW_PAD + k] = 0.f;
         }
+        // the CU's 16 context channels of sentence ab at every position, [j][16] (read each step)
+        float* es = sm + S::ENCS + ab * S::ENC_L * 16;
+        const float* src = a.enc + (size_t)ab * a.Lcap * ENC + 16 * rank;
+        for (int k = lane; k < min(Lb, S::ENC_L) * 16; k += 64) es[k] = src[(size_t)(k >> 4) * ENC + (k & 15)];
     } else if (att_w) {
         for (int k = lane; k < 2 * GW_PAD; k += 64) gw[ab * 2 * GW_PAD + k] = 0.f;
     }
@@ -288,6 +345,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     const auto rg = __builtin_amdgcn_make_buffer_rsrc(a.gran, (short)0, 2 * RBG_TOTAL * 8, 0x00020000);
     const int xb = RBG_X + xcc * RBX_SIZE;  // this XCD's block (the parity offset is added per step)
     __syncthreads();
+    if constexpr (PROF) tprev = (long long)wall_clock64();
 
     int t = 0;
     for (;; ++t) {
@@ -295,7 +353,8 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         u64* G = a.gran + P;
         const unsigned E = (a.salt << 14) | (((unsigned)t & 2047u) << 3);
         const unsigned EP6 = ((a.salt << 14) | (((unsigned)(t - 1) & 2047u) << 3)) + 6u;
-        // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}] for every sentence (acc[4 b + gate])
+        // 1) attention LSTM over [ctx_{t-1} | h_att_{t-1}] for every sentence (acc[4 b + gate]); lane l
+        //    reads k = 256 q + 4 l .. + 3 of each part (consecutive lanes, consecutive LDS banks)
         float acc[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[i] = 0.f;
@@ -303,16 +362,17 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         for (int b = 0; b < NB; ++b) {
             float* ac = acc + 4 * b;
 #pragma unroll
-            for (int q = 0; q < 2; ++q) fma44(wa + 4 + 4 * q, ld4(xctx + b * ENC + 8 * lane + 4 * q), ac);
+            for (int q = 0; q < 2; ++q) fma44(wa + 4 + 4 * q, ld4(xctx + b * ENC + 256 * q + 4 * lane), ac);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) fma44(wa + 12 + 4 * q, ld4(xh_att + b * HATT + 16 * lane + 4 * q), ac);
+            for (int q = 0; q < 4; ++q) fma44(wa + 12 + 4 * q, ld4(xh_att + b * HATT + 256 * q + 4 * lane), ac);
             asm volatile("" ::: "memory");  // one sentence's LDS operands in flight at a time
         }
+        mark(0);
         // 2) pre1_t (+ continue flags) of this XCD's copy, gathered from the previous step's parity
         if (t == 0) {
             for (int k = tid; k < NB * PRE; k += RB_THREADS) xp1[k] = k < a.B * PRE ? a.pre1[k] : 0.f;
         } else {
-            const bool ok = gather_pairs<NB * PRE / 2 / RB_THREADS>(rg, Pp + xb + RBX_P1, NB * PRE / 2, EP6, xp1, tmo);
+            const bool ok = gather_pairs<NB * PRE / 2>(rg, Pp + xb + RBX_P1, EP6, xp1, tmo);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 1, t); }
             if (wave == 0) {
                 float f0 = 0.f, f1 = 0.f;
@@ -332,20 +392,32 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
 #pragma unroll
         for (int b = 0; b < NB; ++b) actm |= act[b] ? 1u << b : 0u;
         if (!actm) break;
-        // 3) prenet layer 2: this wave's two rows of the XCD copy for every sentence, XCD-local
-#pragma unroll 1
-        for (int b = 0; b < NB; ++b) {
-            const float4 x = ld4(xp1 + b * PRE + lane * 4);
-            const float s0 = wave_sum_dpp(dot4(wp0, x, 0.f)), s1 = wave_sum_dpp(dot4(wp1, x, 0.f));
-            if (lane == 0) publish_xcd(G + xb + RBX_PRE2 + b * PRE + r0, E + 1, fmaxf(s0 + bp2a, 0.f));
-            if (lane == 1) publish_xcd(G + xb + RBX_PRE2 + b * PRE + r0 + 1, E + 1, fmaxf(s1 + bp2b, 0.f));
-        }
+        mark(1);
+        // 3) prenet layer 2: this wave's two rows of the XCD copy for every sentence (2 NB sums
+        //    reduced together), XCD-local
         {
-            const bool ok = gather_pairs<NB * PRE / 2 / RB_THREADS>(rg, P + xb + RBX_PRE2, NB * PRE / 2, E + 1, xpre, tmo);
+            float pv[2 * NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const float4 x = ld4(xp1 + b * PRE + lane * 4);
+                pv[2 * b] = dot4(wp0, x, 0.f);
+                pv[2 * b + 1] = dot4(wp1, x, 0.f);
+            }
+            const float r = xreduce<2 * NB>(pv);
+            constexpr int SP = 64 / (2 * NB);
+            if ((lane & (SP - 1)) == 0) {
+                const int idx = lane / SP, b = idx >> 1, rr = idx & 1;
+                publish_xcd(G + xb + RBX_PRE2 + b * PRE + r0 + rr, E + 1, fmaxf(r + (rr ? bp2b : bp2a), 0.f));
+            }
+        }
+        mark(2);
+        {
+            const bool ok = gather_pairs<NB * PRE / 2>(rg, P + xb + RBX_PRE2, E + 1, xpre, tmo);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7, t); }
         }
         __syncthreads();  // P2
         if (flags[1]) break;
+        mark(3);
         // 4) prenet part of the attention LSTM, reduction and cell of unit 4c + wave (this wave):
         //    publish h_att (device-wide)
 #pragma unroll
@@ -363,23 +435,29 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 publish(G + RBG_HATT + lane * HATT + 4 * c + wave, E + 2, h_att_l);
             }
         }
+        mark(4);
         // 5) gather h_att_t
         {
-            const bool ok = gather_pairs<NB * HATT / 2 / RB_THREADS>(rg, P + RBG_HATT, NB * HATT / 2, E + 2, xh_att, tmo);
+            const bool ok = gather_pairs<NB * HATT / 2>(rg, P + RBG_HATT, E + 2, xh_att, tmo);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2, t); }
         }
         __syncthreads();  // P3
         if (flags[1]) break;
+        mark(5);
         // 6) query row 4 rank + wave of the XCD copy for every sentence (common_layers.py:179), XCD-local
-#pragma unroll 1
-        for (int b = 0; b < NB; ++b) {
-            const float* wqr = a.wq + qrow * HATT + lane * 4;
-            float q = 0.f;
+        {
+            float qv[NB];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) q = dot4(ld4(wqr + i * 256), ld4(xh_att + b * HATT + i * 256 + lane * 4), q);
-            q = wave_sum_dpp(q);
-            if (lane == 0) publish_xcd(G + xb + RBX_Q + b * ADIM + qrow, E + 3, q);
+            for (int b = 0; b < NB; ++b) {
+                qv[b] = 0.f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qv[b] = dot4(ld4(wql + i * 256), ld4(xh_att + b * HATT + i * 256 + lane * 4), qv[b]);
+            }
+            const float r = xreduce<NB>(qv);
+            constexpr int SQ = 64 / NB;
+            if ((lane & (SQ - 1)) == 0) publish_xcd(G + xb + RBX_Q + (lane / SQ) * ADIM + qrow, E + 3, r);
         }
+        mark(6);
         // 7) attention of sentence ab in wave ab (common_layers.py:166-256 without location / windowing /
         //    transition agent), the context of this CU's 16 channels, XCD-local publish
         if (att_w && Lb == 0) {  // a padding sentence: zero context (every CU's gather waits for it)
@@ -401,13 +479,13 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3, t); }
             }
             // the energy of positions rank + 32 i: v . tanh(q + P) + b_v (common_layers.py:178-182)
+            {
+                float ev[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int pe = rank + 32 * i;
-                if (pe < Lb) {
-                    const float e = wave_sum_dpp(gv.x * tanh_fast(q.x + gp[i].x) + gv.y * tanh_fast(q.y + gp[i].y));
-                    if (lane == 0) publish_xcd(G + xb + RBX_E + ab * RES_LMAX + pe, E + 7, e + vb);
-                }
+                for (int i = 0; i < 8; ++i) ev[i] = gv.x * tanh_fast(q.x + gp[i].x) + gv.y * tanh_fast(q.y + gp[i].y);
+                const float r = xreduce<8>(ev);  // lane 8 i: position rank + 32 i
+                const int pe = rank + 32 * (lane >> 3);
+                if ((lane & 7) == 0 && pe < Lb) publish_xcd(G + xb + RBX_E + ab * RES_LMAX + pe, E + 7, r + vb);
             }
             // sentence ab's energies from every CU of the XCD: positions 2 lane (+1), 128 + 2 lane (+1)
             int ps[4];
@@ -487,13 +565,18 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             *reinterpret_cast<float2*>(wnew + 2 * lane) = float2{w[0], w[1]};
             *reinterpret_cast<float2*>(wnew + 128 + 2 * lane) = float2{w[2], w[3]};
             // the context of channels 16 rank + (lane & 15) over positions (lane >> 4) + 4 m (bmm, :217 /
-            // :253); the weights were just written by this wave (its LDS operations complete in order)
-            const float* encb = a.enc + (size_t)ab * a.Lcap * ENC + 16 * rank + (lane & 15);
+            // :253) from the LDS copy; the weights were just written by this wave (in order)
+            const float* es = sm + S::ENCS + ab * S::ENC_L * 16 + (lane & 15);
             float cacc = 0.f;
+            int j = lane >> 4;
 #pragma unroll 4
-            for (int j = lane >> 4; j < Lb; j += 4) cacc = fmaf(wnew[j], encb[(size_t)j * ENC], cacc);
-            cacc += __shfl_xor(cacc, 16, 64);
-            cacc += __shfl_xor(cacc, 32, 64);
+            for (; j < min(Lb, S::ENC_L); j += 4) cacc = fmaf(wnew[j], es[j * 16], cacc);
+            if (Lb > S::ENC_L) {  // positions past the LDS copy (NB = 4, L > 128): from L2
+                const float* encb = a.enc + (size_t)ab * a.Lcap * ENC + 16 * rank + (lane & 15);
+                for (; j < Lb; j += 4) cacc = fmaf(wnew[j], encb[(size_t)j * ENC], cacc);
+            }
+            cacc = xlevel<16>(cacc, cacc);
+            cacc = xlevel<32>(cacc, cacc);
             if (lane < 16) publish_xcd(G + xb + RBX_CTX + ab * ENC + 16 * rank + lane, E + 4, cacc);
             if (rank == 0 && lane == 16) publish_xcd(G + xb + RBX_TAIL + ab, E + 4, tail);
             if (xlog && rank == 0 && (actm >> ab & 1u) && t < a.hist_cap) {
@@ -503,6 +586,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                     if (ps[i] < a.Lalign) arow[ps[i]] = w[i];
             }
         }
+        mark(7);
         // 8) decoder LSTM over [h_att_t | h_dec_{t-1}] (its partial sums are not held across the
         //    attention), while the other CUs' contexts arrive
 #pragma unroll
@@ -511,15 +595,16 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         for (int b = 0; b < NB; ++b) {
             float* ac = acc + 4 * b;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) fma44(wd + 4 * q, ld4(xh_att + b * HATT + 16 * lane + 4 * q), ac);
+            for (int q = 0; q < 4; ++q) fma44(wd + 4 * q, ld4(xh_att + b * HATT + 256 * q + 4 * lane), ac);
             asm volatile("" ::: "memory");
 #pragma unroll
-            for (int q = 0; q < 4; ++q) fma44(wd + 24 + 4 * q, ld4(xh_dec + b * HDEC + 16 * lane + 4 * q), ac);
+            for (int q = 0; q < 4; ++q) fma44(wd + 24 + 4 * q, ld4(xh_dec + b * HDEC + 256 * q + 4 * lane), ac);
             asm volatile("" ::: "memory");
         }
+        mark(8);
         // 9) gather the NB contexts and tails
         {
-            const bool ok = gather_pairs<NB * ENC / 2 / RB_THREADS>(rg, P + xb + RBX_CTX, NB * ENC / 2, E + 4, xctx, tmo);
+            const bool ok = gather_pairs<NB * ENC / 2>(rg, P + xb + RBX_CTX, E + 4, xctx, tmo);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4, t); }
             if (wave == 1) {
                 float t0 = 0.f, t1 = 0.f;
@@ -533,11 +618,16 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         }
         __syncthreads();  // P4
         if (flags[1]) break;
-        // 10) decoder LSTM context part, reduction, cell -> publish h_dec (device-wide)
+        mark(9);
+        // 10) decoder LSTM context part, reduction, cell -> publish h_dec (device-wide); this wave's
+        //     prenet-1 row weights of step 12 are fetched meanwhile
+        float4 wdc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wdc[j] = reinterpret_cast<const float4*>(sm + S::WDC)[j * RB_THREADS + tid];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
 #pragma unroll
-            for (int q = 0; q < 2; ++q) fma44(wd + 16 + 4 * q, ld4(xctx + b * ENC + 8 * lane + 4 * q), acc + 4 * b);
+            for (int q = 0; q < 2; ++q) fma44(wdc + 4 * q, ld4(xctx + b * ENC + 256 * q + 4 * lane), acc + 4 * b);
         }
         {
             const float r = xreduce<V>(acc);
@@ -551,84 +641,103 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 publish(G + RBG_HDEC + lane * HDEC + 4 * c + wave, E + 5, h_dec_l);
             }
         }
-        // 11) gather h_dec_t
+        mark(10);
+        // 11) gather h_dec_t (this wave's prenet-1 row weights of step 12 in flight meanwhile)
+        float4 w1p[12];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            w1p[i] = ld4(w1a + i * 256);
+            w1p[6 + i] = ld4(w1a + KF + i * 256);
+        }
         {
-            const bool ok = gather_pairs<NB * HDEC / 2 / RB_THREADS>(rg, P + RBG_HDEC, NB * HDEC / 2, E + 5, xh_dec, tmo);
+            const bool ok = gather_pairs<NB * HDEC / 2>(rg, P + RBG_HDEC, E + 5, xh_dec, tmo);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5, t); }
         }
         __syncthreads();  // P5
         if (flags[1]) break;
+        mark(11);
         // 12) prenet-1 rows of step t+1 (XCD copy) over [h_dec_t | ctx_t], XCD-local; the stop CU's
         //     wave 3: stopnet + stop rule per sentence -> continue flags; CU c < nmel: mel row c
         {
-            const float* w1a = a.wf + (size_t)(a.nmel + r0) * KF + lane * 4;
-#pragma unroll 1
+            float pv[2 * NB];
+#pragma unroll
             for (int b = 0; b < NB; ++b) {
                 float s0 = 0.f, s1 = 0.f;
 #pragma unroll
                 for (int i = 0; i < 6; ++i) {
                     const float4 x = i < 4 ? ld4(xh_dec + b * HDEC + i * 256 + lane * 4) : ld4(xctx + b * ENC + (i - 4) * 256 + lane * 4);
-                    s0 = dot4(ld4(w1a + i * 256), x, s0);
-                    s1 = dot4(ld4(w1a + KF + i * 256), x, s1);
+                    s0 = dot4(w1p[i], x, s0);
+                    s1 = dot4(w1p[6 + i], x, s1);
                 }
-                s0 = wave_sum_dpp(s0);
-                s1 = wave_sum_dpp(s1);
-                if (lane == 0) publish_xcd(G + xb + RBX_P1 + b * PRE + r0, E + 6, fmaxf(s0 + bp1a, 0.f));
-                if (lane == 1) publish_xcd(G + xb + RBX_P1 + b * PRE + r0 + 1, E + 6, fmaxf(s1 + bp1b, 0.f));
+                pv[2 * b] = s0;
+                pv[2 * b + 1] = s1;
+            }
+            const float r = xreduce<2 * NB>(pv);
+            constexpr int SP = 64 / (2 * NB);
+            if ((lane & (SP - 1)) == 0) {
+                const int idx = lane / SP, b = idx >> 1, rr = idx & 1;
+                publish_xcd(G + xb + RBX_P1 + b * PRE + r0 + rr, E + 6, fmaxf(r + (rr ? bp1b : bp1a), 0.f));
             }
         }
-        if (stop_cu && wave == 3) {
-            const float4* wsr = reinterpret_cast<const float4*>(rm) + 6 * 64 + lane;
-#pragma unroll 1
+        if ((stop_cu && wave == 3) || (wave == 1 && c < a.nmel)) {
+            // stop CU wave 3: the stopnet row; wave 1 of CU c < nmel: mel row c (LDS copies)
+            const float4* wr = reinterpret_cast<const float4*>(rm) + (wave == 3 ? 6 * 64 : 0) + lane;
+            float sv[NB];
+#pragma unroll
             for (int b = 0; b < NB; ++b) {
-                float ss = 0.f;
+                float s = 0.f;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ss = dot4(wsr[i * 64], ld4(xh_dec + b * HDEC + i * 256 + lane * 4), ss);
+                for (int i = 0; i < 4; ++i) s = dot4(wr[i * 64], ld4(xh_dec + b * HDEC + i * 256 + lane * 4), s);
 #pragma unroll
-                for (int i = 4; i < 6; ++i) ss = dot4(wsr[i * 64], ld4(xctx + b * ENC + (i - 4) * 256 + lane * 4), ss);
-                ss = wave_sum_dpp(ss);
-                if (lane == 0) {
-                    // stopnet + stop rule (tacotron2.py:219-224, 257-277) of sentence b, as a batch-1 run
-                    int cont = 0;
-                    if (actm >> b & 1u) {
-                        const float stv = sigmoidf_(ss + stop_b);
-                        if (xlog && t < a.hist_cap) a.stop_hist[(size_t)b * a.hist_cap + t] = stv;
-                        const int Lsb = a.L[b];
-                        const int f1 = sflag1[b] | ((xtail[b] > 0.8f && t > Lsb) ? 1 : 0);
-                        sflag1[b] = f1;
-                        int nd = 0;
-                        if (f1 && t > 2 * Lsb) {
-                            scount[b] += 1;
-                            if (scount[b] > 20) nd = 1;
-                        } else if (t + 1 == a.max_steps) {
-                            nd = 1;
-                        }
-                        if (!nd && t + 1 >= a.hist_cap) {  // cannot happen: the rule stops by max_steps + 20
-                            nd = 1;
-                            fail(a.status, 100);
-                        }
-                        if (nd && xlog) {
-                            a.done[b] = 1;
-                            a.n_steps[b] = t + 1;
-                        }
-                        cont = !nd;
+                for (int i = 4; i < 6; ++i) s = dot4(wr[i * 64], ld4(xctx + b * ENC + (i - 4) * 256 + lane * 4), s);
+                sv[b] = s;
+            }
+            const float ss = xreduce<NB>(sv);
+            constexpr int SQ = 64 / NB;
+            const int b = lane / SQ;  // lanes SQ b: sentence b
+            const bool actb = (actm >> b & 1u) != 0;
+            if ((lane & (SQ - 1)) == 0 && wave == 1) {
+                if (actb && t < a.hist_cap) a.mel_hist[((size_t)b * a.hist_cap + t) * a.nmel + c] = ss + mel_b;
+            } else if ((lane & (SQ - 1)) == 0) {
+                // stopnet + stop rule (tacotron2.py:219-224, 257-277) of sentence b, as a batch-1 run
+                int cont = 0;
+                if (actb) {
+                    const float stv = sigmoidf_(ss + stop_b);
+                    if (xlog && t < a.hist_cap) a.stop_hist[(size_t)b * a.hist_cap + t] = stv;
+                    int Lsb = a.L[0];
+#pragma unroll
+                    for (int k = 1; k < NB; ++k)
+                        if (b == k) Lsb = a.L[k];
+                    const int f1 = sflag1[b] | ((xtail[b] > 0.8f && t > Lsb) ? 1 : 0);
+                    sflag1[b] = f1;
+                    int nd = 0;
+                    if (f1 && t > 2 * Lsb) {
+                        scount[b] += 1;
+                        if (scount[b] > 20) nd = 1;
+                    } else if (t + 1 == a.max_steps) {
+                        nd = 1;
                     }
-                    publish_xcd(G + xb + RBX_FLAG + b, E + 6, cont ? 1.f : 0.f);
+                    if (!nd && t + 1 >= a.hist_cap) {  // cannot happen: the rule stops by max_steps + 20
+                        nd = 1;
+                        fail(a.status, 100);
+                    }
+                    if (nd && xlog) {
+                        a.done[b] = 1;
+                        a.n_steps[b] = t + 1;
+                    }
+                    cont = !nd;
                 }
+                publish_xcd(G + xb + RBX_FLAG + b, E + 6, cont ? 1.f : 0.f);
             }
         }
-        if (wave == 1 && c < a.nmel) {  // mel row c of step t for the sentences decoding it
-            const float4* wm = reinterpret_cast<const float4*>(rm) + lane;
-#pragma unroll 1
-            for (int b = 0; b < NB; ++b) {
-                float mv = 0.f;
+        mark(12);
+    }
+    if constexpr (PROF) {
+        if (lane == 0) {
+            long long* pr = a.prof + (size_t)(c * 4 + wave) * RB_PROF_SLOTS;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) mv = dot4(wm[i * 64], ld4(xh_dec + b * HDEC + i * 256 + lane * 4), mv);
-#pragma unroll
-                for (int i = 4; i < 6; ++i) mv = dot4(wm[i * 64], ld4(xctx + b * ENC + (i - 4) * 256 + lane * 4), mv);
-                mv = wave_sum_dpp(mv);
-                if (lane == 0 && (actm >> b & 1u) && t < a.hist_cap) a.mel_hist[((size_t)b * a.hist_cap + t) * a.nmel + c] = mv + mel_b;
-            }
+            for (int k = 0; k < RB_PROF_SLOTS - 1; ++k) pr[k] = ptk[k];
+            pr[RB_PROF_SLOTS - 1] = t;
         }
     }
     if (flags[1]) return;
@@ -649,8 +758,9 @@ __global__ void rb_pack_wa(const float* wih, const float* whh, float4* out) {
     if (idx >= (int64_t)RES_CUS * KA * RB_THREADS) return;
     const int tid = idx % RB_THREADS, j = (idx / RB_THREADS) % KA, c = idx / (KA * RB_THREADS);
     const int uu = tid >> 6, l = tid & 63;
-    // k over [prenet 256 | ctx 512 | h_att 1024]: 4 + 8 + 16 per lane
-    const int k = j < 4 ? 4 * l + j : j < 12 ? PRE + 8 * l + (j - 4) : XA + 16 * l + (j - 12);
+    // k over [prenet 256 | ctx 512 | h_att 1024]: 4 + 8 + 16 per lane, k = 256 q + 4 l + e in each part
+    const int jj = j < 4 ? j : j < 12 ? j - 4 : j - 12;
+    const int k = (j < 4 ? 0 : j < 12 ? PRE : XA) + 256 * (jj >> 2) + 4 * l + (jj & 3);
     float v[4];
     for (int g = 0; g < 4; ++g) {
         const int row = g * HATT + 4 * c + uu;
@@ -663,8 +773,9 @@ __global__ void rb_pack_wd(const float* wih, const float* whh, float4* out) {
     if (idx >= (int64_t)RES_CUS * KD * RB_THREADS) return;
     const int tid = idx % RB_THREADS, j = (idx / RB_THREADS) % KD, c = idx / (KD * RB_THREADS);
     const int uu = tid >> 6, l = tid & 63;
-    // k over [h_att 1024 | ctx 512 | h_dec 1024]: 16 + 8 + 16 per lane
-    const int k = j < 16 ? 16 * l + j : j < 24 ? HATT + 8 * l + (j - 16) : HATT + ENC + 16 * l + (j - 24);
+    // k over [h_att 1024 | ctx 512 | h_dec 1024]: 16 + 8 + 16 per lane, k = 256 q + 4 l + e in each part
+    const int jj = j < 16 ? j : j < 24 ? j - 16 : j - 24;
+    const int k = (j < 16 ? 0 : j < 24 ? HATT : HATT + ENC) + 256 * (jj >> 2) + 4 * l + (jj & 3);
     float v[4];
     for (int g = 0; g < 4; ++g) {
         const int row = g * HDEC + 4 * c + uu;
@@ -696,10 +807,12 @@ size_t resident_batch_smem_bytes(int B) {
 }
 
 hipError_t resident_batch_prepare() {
-    const void* fns[] = {reinterpret_cast<const void*>(&resident_batch_kernel<2>),
-                         reinterpret_cast<const void*>(&resident_batch_kernel<4>)};
-    const int nbs[] = {2, 4};
-    for (int i = 0; i < 2; ++i) {
+    const void* fns[] = {reinterpret_cast<const void*>(&resident_batch_kernel<2, false>),
+                         reinterpret_cast<const void*>(&resident_batch_kernel<4, false>),
+                         reinterpret_cast<const void*>(&resident_batch_kernel<2, true>),
+                         reinterpret_cast<const void*>(&resident_batch_kernel<4, true>)};
+    const int nbs[] = {2, 4, 2, 4};
+    for (int i = 0; i < 4; ++i) {
         hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)resident_batch_smem_bytes(nbs[i]));
         if (e != hipSuccess) return e;
@@ -718,8 +831,11 @@ hipError_t launch_resident_batch(const ResBatchArgs& a, hipStream_t s, bool* lau
     ResBatchArgs arg = a;
     for (int b = a.B; b < RB_MAXB; ++b) arg.L[b] = 0;
     void* args[] = {&arg};
-    const void* fn = rb_nb(a.B) == 2 ? reinterpret_cast<const void*>(&resident_batch_kernel<2>)
-                                     : reinterpret_cast<const void*>(&resident_batch_kernel<4>);
+    const bool prof = a.prof != nullptr;
+    const void* fn = rb_nb(a.B) == 2 ? (prof ? reinterpret_cast<const void*>(&resident_batch_kernel<2, true>)
+                                             : reinterpret_cast<const void*>(&resident_batch_kernel<2, false>))
+                                     : (prof ? reinterpret_cast<const void*>(&resident_batch_kernel<4, true>)
+                                             : reinterpret_cast<const void*>(&resident_batch_kernel<4, false>));
     return launch_persistent(fn, dim3(RES_CUS), dim3(RB_THREADS), args, resident_batch_smem_bytes(a.B), s, launched);
 }
 
