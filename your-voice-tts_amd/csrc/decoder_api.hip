@@ -13,6 +13,7 @@
 // The host synchronises only at chunk boundaries: the first chunk is the reference's lower
 // bound on the step count (min(2L+22, max_steps) per sentence, layers/tacotron2.py:268-277).
 #include <algorithm>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -121,11 +122,13 @@ struct tts_decoder {
 
 namespace {
 
-// the largest batch the resident batch decoder takes (consecutive launches of <= RB_MAXB)
+// the largest batch the resident batch decoder takes (consecutive launches of <= RB_MAXB): two
+// launches of 4 (2 x 16.6 us per step, round 6) beat the multi-launch step (~44 us at any batch up
+// to 64); three do not.  TTS_RB_MAX overrides.
 int rb_max_batch() {
     static const int v = [] {
         const char* e = getenv("TTS_RB_MAX");
-        return e && e[0] ? std::max(0, atoi(e)) : 12;
+        return e && e[0] ? std::max(0, atoi(e)) : 2 * RB_MAXB;
     }();
     return v;
 }
@@ -878,6 +881,11 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             rb.stop_hist = d->stop_hist + (size_t)g0 * d->hist_cap;
             rb.align_hist = d->align_hist + (size_t)g0 * d->hist_cap * Lmax;
             rb.gran = d->rb_gran;
+            static const int rb_sleep = [] {
+                const char* v = getenv("TTS_RB_SLEEP");
+                return v ? atoi(v) : 0;
+            }();
+            rb.poll_sleep = rb_sleep;
             rb.status = reinterpret_cast<int*>(d->rb_gran + resident_batch_granules());
             if (rb_prof && !d->rb_prof) {
                 tts_status ps = dmalloc(d, &d->rb_prof, (size_t)RES_CUS * 4 * RB_PROF_SLOTS);
@@ -935,6 +943,27 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                     }
                     fprintf(stderr, "\n");
                 }
+                // one step (RB_PROF_T): the last publisher of an edge vs each CU's arrival (us)
+                if (pk[RB_PROF_SLOTS - 1] > RB_PROF_T) {
+                    auto at = [&](int cu, int w, int k) { return pk[((size_t)cu * 4 + w) * RB_PROF_SLOTS + k]; };
+                    const char* names[] = {"h_att", "h_dec"};
+                    const int pubk[] = {13, 16}, donek[] = {14, 17};
+                    for (int e = 0; e < 2; ++e) {
+                        long long pmin = LLONG_MAX, pmax = 0, dmin = LLONG_MAX, dmax = 0;
+                        int pmax_cu = -1;
+                        for (int cu = 0; cu < RES_CUS; ++cu)
+                            for (int w = 0; w < 4; ++w) {
+                                const long long p = at(cu, w, pubk[e]), q = at(cu, w, donek[e]);
+                                if (p < pmin) pmin = p;
+                                if (p > pmax) { pmax = p; pmax_cu = cu * 4 + w; }
+                                dmin = std::min(dmin, q);
+                                dmax = std::max(dmax, q);
+                            }
+                        fprintf(stderr, "[tts]  step %d %s: publish spread %.2f us (last: CU %d wave %d), arrival after the last publish %.2f .. %.2f us\n",
+                                RB_PROF_T, names[e], (pmax - pmin) * 0.01, pmax_cu / 4, pmax_cu % 4, (dmin - pmax) * 0.01,
+                                (dmax - pmax) * 0.01);
+                    }
+                }
             }
         }
         if (all) {
@@ -968,6 +997,20 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         ra.ta_w = d->ta_w; ra.ta_b = d->ta_b; ra.att_w0 = d->att_w; ra.att_cum0 = d->att_cum; ra.win0 = d->win_idx;
         ra.loc_conv = d->loc_conv_p; ra.loc_dense = d->loc_dense;
         ra.gran = d->gran;
+        // first-poll delays (resident.h; round 6: h_att 5 / h_dec 5 took a configs[1] sentence from
+        // 2.65 to 2.29 ms, tools/cases_sleep.txt); TTS_RES_SLEEP_* override them
+        auto knob = [](const char* name, int dflt) {
+            const char* v = getenv(name);
+            return v ? atoi(v) : dflt;
+        };
+        static const int sl_hatt = knob("TTS_RES_SLEEP_HATT", 5), sl_hdec = knob("TTS_RES_SLEEP_HDEC", 5),
+                         sl_p1 = knob("TTS_RES_SLEEP_P1", 0), sl_pre2 = knob("TTS_RES_SLEEP_PRE2", 2),
+                         sl_ctx = knob("TTS_RES_SLEEP_CTX", 0);
+        ra.sleep_hatt = sl_hatt;
+        ra.sleep_hdec = sl_hdec;
+        ra.sleep_p1 = sl_p1;
+        ra.sleep_pre2 = sl_pre2;
+        ra.sleep_ctx = sl_ctx;
         ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
         // direct (pipelined) runs skip the per-launch clear and rely on the 18-bit tag salt: on a
         // salt wrap a granule left 2^18 launches back could match a current wait, so clear then
@@ -1121,7 +1164,11 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         TTS_HIP(hipStreamWaitEvent(cs, d->ev_out, 0));
     }
     d->last_ms = 0.f;  // (pipeline mode: not timed)
-    if (timed) TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
+    if (timed) {
+        // (the resident paths record ev_t1 after their last host sync: it may still be pending)
+        TTS_HIP(hipEventSynchronize(d->ev_t1));
+        TTS_HIP(hipEventElapsedTime(&d->last_ms, d->ev_t0, d->ev_t1));
+    }
     d->last_steps = run;
     d->last_B = B;
     d->last_Lmax = Lmax;

@@ -121,6 +121,9 @@ struct ResArgs {
     float* align_hist;
     unsigned long long* gran;  // [2][GR_TOTAL], zeroed before every launch
     int* status;               // [0]: 0 ok, else the id of the wait that timed out
+    // s_sleep(4) counts (~0.12 us each) before the first poll of a gather: a poll storm from every CU
+    // slows the hand-off it waits for (device-wide h_att / h_dec; XCD-local pre1, prenet-2, context)
+    int sleep_hatt, sleep_hdec, sleep_p1, sleep_pre2, sleep_ctx;
     long long* prof;           // null, or RES_PROF_LL: [2][RES_PHASES] wall-clock ticks summed over steps
                                // per phase (CU 0, attention CU), then the event trace — measurement only
     int prof_marks;            // with prof: also the per-phase marks (they perturb the two CUs that take them)
@@ -183,9 +186,11 @@ struct ResBatchArgs {
     float* align_hist;         // [B][hist_cap][Lalign]
     unsigned long long* gran;  // resident_batch_granules() slots
     int* status;
+    int poll_sleep;            // s_sleep between device-wide polls (TTS_RB_SLEEP; 0 = none)
     long long* prof;           // [256 CU][4 waves][RB_PROF_SLOTS] phase clocks (TTS_RB_PROF=1), else null
 };
-constexpr int RB_PROF_SLOTS = 16;
+constexpr int RB_PROF_SLOTS = 20;  // [0, 13) phase sums, [13, 19) clocks at step RB_PROF_T, [19] steps
+constexpr int RB_PROF_T = 150;
 void resident_batch_weight_floats(size_t* wa, size_t* wd);
 size_t resident_batch_granules();
 hipError_t resident_batch_pack(const ResSrc& src, float4* wa, float4* wd, hipStream_t s);

@@ -155,7 +155,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // poll issues all of the thread's loads before one wait; the values go to dst[2p], dst[2p + 1]
 // once every pair of the wave carries `tag`.  false after the timeout.
 template <int NP>
-__device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base, unsigned tag, float* dst, long long tmo) {
+__device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base, unsigned tag, float* dst, long long tmo,
+                                             int sleep = 0) {
     static_assert(NP % RB_THREADS == 0, "whole pairs per thread");
     constexpr int MAXP = NP / RB_THREADS;
     const int tid = threadIdx.x;
@@ -180,6 +181,8 @@ __device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base,
         } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
             return false;
         }
+        if (sleep == 1) __builtin_amdgcn_s_sleep(1);
+        else if (sleep >= 2) __builtin_amdgcn_s_sleep(4);
     }
 }
 
@@ -207,12 +210,23 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     int* scount = ints + 24;
     // phase clocks (PROF builds): lane 0 of every wave
     long long ptk[RB_PROF_SLOTS] = {}, tprev = 0;
+    int t = 0;
     auto mark = [&](int k) {
         if constexpr (PROF) {
             if (lane == 0) {
                 const long long now = (long long)wall_clock64();
                 ptk[k] += now - tprev;
                 tprev = now;
+                // absolute clocks at one step: h_att published / gathered, ctx published, h_dec
+                // published / gathered, the step's end
+                if (t == RB_PROF_T) {
+                    if (k == 4) ptk[13] = now;
+                    if (k == 5) ptk[14] = now;
+                    if (k == 7) ptk[15] = now;
+                    if (k == 10) ptk[16] = now;
+                    if (k == 11) ptk[17] = now;
+                    if (k == 12) ptk[18] = now;
+                }
             }
         }
     };
@@ -347,7 +361,6 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     __syncthreads();
     if constexpr (PROF) tprev = (long long)wall_clock64();
 
-    int t = 0;
     for (;; ++t) {
         const int P = (t & 1) * RBG_TOTAL, Pp = ((t & 1) ^ 1) * RBG_TOTAL;
         u64* G = a.gran + P;
@@ -367,6 +380,10 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             for (int q = 0; q < 4; ++q) fma44(wa + 12 + 4 * q, ld4(xh_att + b * HATT + 256 * q + 4 * lane), ac);
             asm volatile("" ::: "memory");  // one sentence's LDS operands in flight at a time
         }
+        // the partial sums are computed HERE, off the critical path (while pre1 is in flight); without
+        // the fence the compiler sinks these FMAs past the barriers into phase 4
+#pragma unroll
+        for (int i = 0; i < V; ++i) asm volatile("" : "+v"(acc[i]));
         mark(0);
         // 2) pre1_t (+ continue flags) of this XCD's copy, gathered from the previous step's parity
         if (t == 0) {
@@ -435,10 +452,23 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 publish(G + RBG_HATT + lane * HATT + 4 * c + wave, E + 2, h_att_l);
             }
         }
+        // the decoder LSTM's h_dec_{t-1} half now: useful work before the first h_att poll (a poll
+        // storm from every CU slows the hand-off it waits for)
+        float accd[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) accd[i] = 0.f;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fma44(wd + 24 + 4 * q, ld4(xh_dec + b * HDEC + 256 * q + 4 * lane), accd + 4 * b);
+            asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) asm volatile("" : "+v"(accd[i]));
         mark(4);
         // 5) gather h_att_t
         {
-            const bool ok = gather_pairs<NB * HATT / 2>(rg, P + RBG_HATT, E + 2, xh_att, tmo);
+            const bool ok = gather_pairs<NB * HATT / 2>(rg, P + RBG_HATT, E + 2, xh_att, tmo, a.poll_sleep);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2, t); }
         }
         __syncthreads();  // P3
@@ -590,17 +620,16 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         // 8) decoder LSTM over [h_att_t | h_dec_{t-1}] (its partial sums are not held across the
         //    attention), while the other CUs' contexts arrive
 #pragma unroll
-        for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        for (int i = 0; i < V; ++i) acc[i] = accd[i];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             float* ac = acc + 4 * b;
 #pragma unroll
             for (int q = 0; q < 4; ++q) fma44(wd + 4 * q, ld4(xh_att + b * HATT + 256 * q + 4 * lane), ac);
             asm volatile("" ::: "memory");
-#pragma unroll
-            for (int q = 0; q < 4; ++q) fma44(wd + 24 + 4 * q, ld4(xh_dec + b * HDEC + 256 * q + 4 * lane), ac);
-            asm volatile("" ::: "memory");
         }
+#pragma unroll
+        for (int i = 0; i < V; ++i) asm volatile("" : "+v"(acc[i]));  // (as in phase 1: computed before the wait)
         mark(8);
         // 9) gather the NB contexts and tails
         {
@@ -650,7 +679,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             w1p[6 + i] = ld4(w1a + KF + i * 256);
         }
         {
-            const bool ok = gather_pairs<NB * HDEC / 2>(rg, P + RBG_HDEC, E + 5, xh_dec, tmo);
+            const bool ok = gather_pairs<NB * HDEC / 2>(rg, P + RBG_HDEC, E + 5, xh_dec, tmo, a.poll_sleep);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5, t); }
         }
         __syncthreads();  // P5

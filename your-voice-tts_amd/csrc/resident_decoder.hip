@@ -416,6 +416,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 }
             } else {
                 float p0 = 0.f, p1 = 0.f;
+                for (int i = 0; i < a.sleep_p1; ++i) __builtin_amdgcn_s_sleep(4);
                 if (wave < 2) {
                     ok = sweep_pair(rg, gp + 2 * pk, true, EP6, p0, p1, tmo);
                     xp1[2 * pk] = p0;
@@ -440,6 +441,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             }
             RES_MARK(1);
             if (wave < 2) {
+                for (int i = 0; i < a.sleep_pre2; ++i) __builtin_amdgcn_s_sleep(4);
                 float q0, q1;
                 const bool ok = sweep_pair(rg, s_x + (t & 1) * GR_TOTAL + 2 * pk, true, E + 1, q0, q1, tmo);
                 xpre[2 * pk] = q0;
@@ -484,6 +486,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         }
         {
             if (wave == 4 && t > 0) mel_row(t - 1);
+            for (int i = 0; i < a.sleep_hatt; ++i) __builtin_amdgcn_s_sleep(4);
             float h0, h1;
             const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HATT + 2 * pk, true, E + 2, h0, h1, tmo);
             xh_att[2 * pk] = h0;
@@ -846,6 +849,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         // 8) gather ctx_t and the tail
         if (wave < 5 && !att_cu) {  // waves 0-3: the 512 context values as pairs; wave 4, lane 0: the tail
             const int gc = s_c + (t & 1) * GR_TOTAL;
+            for (int i = 0; i < a.sleep_ctx; ++i) __builtin_amdgcn_s_sleep(4);
             float c0 = 0.f, c1 = 0.f;
             const bool ok = wave < 4 ? sweep_pair(rg, gc + 2 * pk, true, E + 4, c0, c1, tmo)
                                      : sweep_pair(rg, lane == 0 ? gc + ENC : -1, false, E + 4, c0, c1, tmo);
@@ -903,6 +907,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         }
         // 10) gather h_dec_t
         {
+            for (int i = 0; i < a.sleep_hdec; ++i) __builtin_amdgcn_s_sleep(4);
             float h0, h1;
             const bool ok = sweep_pair(rg, (t & 1) * GR_TOTAL + GR_HDEC + 2 * pk, true, E + 5, h0, h1, tmo);
             xh_dec[2 * pk] = h0;
