@@ -46,9 +46,12 @@ def main():
     ap.add_argument("--cap", type=int, default=1000)
     ap.add_argument("--batches", default="2,3,4,8,12")
     ap.add_argument("--L", type=int, default=100)
+    ap.add_argument("--mask", choices=("both", "on", "off"), default="both")
+    ap.add_argument("--quick", action="store_true", help="the resident batch decoder only")
     args = ap.parse_args()
-    for mask in (False, True):
-        rb, ml = model(mask, True, args.cap), model(mask, False, args.cap)
+    for mask in {"both": (False, True), "on": (True,), "off": (False,)}[args.mask]:
+        rb = model(mask, True, args.cap)
+        ml = None if args.quick else model(mask, False, args.cap)
         for B in [int(x) for x in args.batches.split(",")]:
             ids = [weights.synthetic_ids(args.L, 1 + b) for b in range(B)]
             rec = dict(mask=mask, B=B, L=args.L, cap=args.cap)
@@ -58,9 +61,10 @@ def main():
             steps = max(rb.inference_batch(ids)["steps"])
             rec["steps"] = steps
             rec["us_per_step"] = 1000 * rec["decoder_loop_ms"] / steps if steps else None
-            rec["multi_launch_ms"] = timed(lambda: ml.inference_batch(ids))
-            rec["multi_launch_loop_ms"] = ml.last_timing.get("decoder_loop_ms")
-            rec["serial_b1_ms"] = timed(lambda: [rb.inference_batch([x]) for x in ids], reps=1)
+            if ml is not None:
+                rec["multi_launch_ms"] = timed(lambda: ml.inference_batch(ids))
+                rec["multi_launch_loop_ms"] = ml.last_timing.get("decoder_loop_ms")
+                rec["serial_b1_ms"] = timed(lambda: [rb.inference_batch([x]) for x in ids], reps=1)
             print(json.dumps(rec), flush=True)
 
 

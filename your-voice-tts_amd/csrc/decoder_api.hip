@@ -881,11 +881,16 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
             rb.stop_hist = d->stop_hist + (size_t)g0 * d->hist_cap;
             rb.align_hist = d->align_hist + (size_t)g0 * d->hist_cap * Lmax;
             rb.gran = d->rb_gran;
-            static const int rb_sleep = [] {
-                const char* v = getenv("TTS_RB_SLEEP");
-                return v ? atoi(v) : 0;
-            }();
-            rb.poll_sleep = rb_sleep;
+            auto knob = [](const char* name, int dflt) {
+                const char* v = getenv(name);
+                return v ? atoi(v) : dflt;
+            };
+            static const int rb_hatt = knob("TTS_RB_SLEEP_HATT", 0), rb_hdec = knob("TTS_RB_SLEEP_HDEC", 0),
+                             rb_pre2 = knob("TTS_RB_SLEEP_PRE2", 0), rb_ctx = knob("TTS_RB_SLEEP_CTX", 0);
+            rb.sleep_hatt = rb_hatt;
+            rb.sleep_hdec = rb_hdec;
+            rb.sleep_pre2 = rb_pre2;
+            rb.sleep_ctx = rb_ctx;
             rb.status = reinterpret_cast<int*>(d->rb_gran + resident_batch_granules());
             if (rb_prof && !d->rb_prof) {
                 tts_status ps = dmalloc(d, &d->rb_prof, (size_t)RES_CUS * 4 * RB_PROF_SLOTS);

@@ -168,6 +168,11 @@ tts_status enqueue_encoder_resident(tts_encoder* e, int Lmax, bool zero_state, h
     e->rgran_clear = true;
     EncResArgs a{};
     a.w = e->rw;
+    static const int enc_first_sleep = [] {
+        const char* v = getenv("TTS_ENC_FIRST_SLEEP");
+        return v ? atoi(v) : 2;  // round 6: ~-9 us per configs[1] sentence (tools/cases_sleep.txt)
+    }();
+    a.first_sleep = enc_first_sleep;
     a.xi = e->xi;
     a.L = Lmax;
     a.hdir = hs;

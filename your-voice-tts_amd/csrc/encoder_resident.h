@@ -19,6 +19,7 @@ struct EncResArgs {
     unsigned long long* gran;  // encoder_resident_granules() u64, zeroed before every launch
     int* status;         // 0 ok; ENC_RES_STATUS_PLACEMENT; else a wait timed out
     long long tmo;       // wall_clock64 ticks per wait
+    int first_sleep;     // s_sleep(1) count before a step's first h poll (TTS_ENC_FIRST_SLEEP)
     unsigned salt;       // per-launch tag salt (18 bits): launched directly, never from a graph,
                          // so no granule (or stale cache line) of an earlier launch can match
 };

@@ -209,6 +209,7 @@ __global__ __launch_bounds__(ER_THREADS, 1) void encoder_resident_kernel(const E
             // (one load instruction per poll instead of four on one wave)
             float v[2];
             const int pr = wave * 64 + lane;
+            for (int i = 0; i < a.first_sleep; ++i) __builtin_amdgcn_s_sleep(1);
             const bool ok = sweep_pair(gr, ((par * 2 + dir) * H) / 2 + pr, (a.salt << 14) | (unsigned)(s + 1), v, a.tmo);
             if (!ok) {
                 if (lane == 0)

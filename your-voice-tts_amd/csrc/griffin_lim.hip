@@ -1177,6 +1177,7 @@ struct PersArgs {
     long long* prof;    // diagnostic (TTS_GL_PHASES): per-phase wall_clock64 ticks of frame prof_f, or null
     int prof_f;
     int nowait;         // measurement only (TTS_GL_NOWAIT=1): one gather sweep, tags unchecked (wrong results)
+    int first_sleep;    // s_sleep(4) count before an iteration's first gather poll (TTS_GL_FIRST_SLEEP)
     int drop_f;         // fault injection (tests, TTS_GL_INJECT_DROP): sentence 0's frame drop_f stops
                         // after its first iteration without storing it (-1: none)
 };
@@ -1410,6 +1411,8 @@ __device__ __forceinline__ void gl_persistent_body(const PersArgs& p) {
             const auto rG = buf_rsrc(src, (unsigned)(a.Fmax * g.winp * 8));
             long long t_end = 0;
             u32x4 x[GL_PAIRS];
+            // (a poll storm from every workgroup the moment it has stored slows the stores it waits for)
+            for (int i = 0; i < p.first_sleep; ++i) __builtin_amdgcn_s_sleep(4);
             for (int spin = 0;; ++spin) {
 #pragma unroll
                 for (int m = 0; m < GL_PAIRS; ++m)
@@ -2418,6 +2421,11 @@ tts_status gl_run_dev(tts_gl* g, int mode, const float* spec, const int32_t* F, 
             return v && v[0] == '1';
         }();
         pa.nowait = gl_nowait;
+        static const int gl_first_sleep = [] {
+            const char* v = getenv("TTS_GL_FIRST_SLEEP");
+            return v ? atoi(v) : 4;  // round 6: -19 us per configs[1] sentence (tools/cases_sleep.txt)
+        }();
+        pa.first_sleep = gl_first_sleep;
         long long* prof = nullptr;
         const char* phases = getenv("TTS_GL_PHASES");
         if (phases && phases[0]) {  // diagnostic: phase ticks of frame TTS_GL_PHASES (stderr)

@@ -186,7 +186,7 @@ struct ResBatchArgs {
     float* align_hist;         // [B][hist_cap][Lalign]
     unsigned long long* gran;  // resident_batch_granules() slots
     int* status;
-    int poll_sleep;            // s_sleep between device-wide polls (TTS_RB_SLEEP; 0 = none)
+    int sleep_hatt, sleep_hdec, sleep_pre2, sleep_ctx;  // s_sleep(4) counts before a gather's first poll (TTS_RB_SLEEP_*)
     long long* prof;           // [256 CU][4 waves][RB_PROF_SLOTS] phase clocks (TTS_RB_PROF=1), else null
 };
 constexpr int RB_PROF_SLOTS = 20;  // [0, 13) phase sums, [13, 19) clocks at step RB_PROF_T, [19] steps

@@ -156,11 +156,13 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // once every pair of the wave carries `tag`.  false after the timeout.
 template <int NP>
 __device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base, unsigned tag, float* dst, long long tmo,
-                                             int sleep = 0) {
+                                             int first_sleep = 0) {
     static_assert(NP % RB_THREADS == 0, "whole pairs per thread");
     constexpr int MAXP = NP / RB_THREADS;
     const int tid = threadIdx.x;
     long long t_end = 0;
+    // (a poll storm from every CU the moment it has published slows the stores it waits for)
+    for (int i = 0; i < first_sleep; ++i) __builtin_amdgcn_s_sleep(4);
     for (int spin = 0;; ++spin) {
         u32x4 x[MAXP];
 #pragma unroll
@@ -181,8 +183,6 @@ __device__ __forceinline__ bool gather_pairs(__amdgpu_buffer_rsrc_t r, int base,
         } else if ((spin & 31) == 0 && (long long)wall_clock64() > t_end) {
             return false;
         }
-        if (sleep == 1) __builtin_amdgcn_s_sleep(1);
-        else if (sleep >= 2) __builtin_amdgcn_s_sleep(4);
     }
 }
 
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         }
         mark(2);
         {
-            const bool ok = gather_pairs<NB * PRE / 2>(rg, P + xb + RBX_PRE2, E + 1, xpre, tmo);
+            const bool ok = gather_pairs<NB * PRE / 2>(rg, P + xb + RBX_PRE2, E + 1, xpre, tmo, a.sleep_pre2);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 7, t); }
         }
         __syncthreads();  // P2
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         mark(4);
         // 5) gather h_att_t
         {
-            const bool ok = gather_pairs<NB * HATT / 2>(rg, P + RBG_HATT, E + 2, xh_att, tmo, a.poll_sleep);
+            const bool ok = gather_pairs<NB * HATT / 2>(rg, P + RBG_HATT, E + 2, xh_att, tmo, a.sleep_hatt);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 2, t); }
         }
         __syncthreads();  // P3
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
         mark(8);
         // 9) gather the NB contexts and tails
         {
-            const bool ok = gather_pairs<NB * ENC / 2>(rg, P + xb + RBX_CTX, E + 4, xctx, tmo);
+            const bool ok = gather_pairs<NB * ENC / 2>(rg, P + xb + RBX_CTX, E + 4, xctx, tmo, a.sleep_ctx);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 4, t); }
             if (wave == 1) {
                 float t0 = 0.f, t1 = 0.f;
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             w1p[6 + i] = ld4(w1a + KF + i * 256);
         }
         {
-            const bool ok = gather_pairs<NB * HDEC / 2>(rg, P + RBG_HDEC, E + 5, xh_dec, tmo, a.poll_sleep);
+            const bool ok = gather_pairs<NB * HDEC / 2>(rg, P + RBG_HDEC, E + 5, xh_dec, tmo, a.sleep_hdec);
             if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 5, t); }
         }
         __syncthreads();  // P5

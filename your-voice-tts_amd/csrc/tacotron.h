@@ -109,7 +109,8 @@ struct TResArgs {
     unsigned long long* gran;  // tres_granules() granules (zeroed at create)
     int* status;               // 0 ok; TR_STATUS_PLACEMENT; else the id of the wait that timed out
     unsigned salt;             // per launch, 18 bits
-    long long timeout_ticks;   // wall_clock64 ticks per wait
+    long long timeout_ticks;
+    int first_sleep;  // s_sleep(1) count before a hand-off's first poll (TTS_TACO_FIRST_SLEEP)   // wall_clock64 ticks per wait
     long long* prof;           // null, or [2][TR_PHASES] phase ticks of CUs 0 and 1 of XCD 0 (measurement)
 };
 size_t tres_granules();

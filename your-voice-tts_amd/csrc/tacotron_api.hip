@@ -1131,6 +1131,11 @@ tts_status tts_tacotron_decode(tts_tacotron* t, const float* enc, const int32_t*
         }
         a.salt = t->res_salt;
         a.timeout_ticks = t->res_ticks;
+        static const int taco_first_sleep = [] {
+            const char* v = getenv("TTS_TACO_FIRST_SLEEP");
+            return v ? atoi(v) : 4;  // round 6: configs[4] 1.603M -> 1.615M (tools/taco_sleep_sweep.sh)
+        }();
+        a.first_sleep = taco_first_sleep;
         a.prof = nullptr;
         t->last_ra = a;
         TTS_HIP(hipMemsetAsync(a.status, 0, sizeof(int), s));

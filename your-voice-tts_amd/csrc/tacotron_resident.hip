@@ -97,8 +97,10 @@ __device__ __forceinline__ void fail(int* status, int code) {
 // One wave polls its N granules per lane (idx(i) < 0: none) until every tag equals `tag`; false
 // after `tmo` wall-clock ticks.
 template <int N, typename F>
-__device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo) {
+__device__ __forceinline__ bool sweep(u64* g, unsigned tag, float (&v)[N], F idx, long long tmo, int first_sleep = 0) {
     long long t_end = 0;
+    // (a poll storm from every CU of the XCD the moment it has published slows the stores it waits for)
+    for (int i = 0; i < first_sleep; ++i) __builtin_amdgcn_s_sleep(1);
     for (int spin = 0;; ++spin) {
         bool ok = true;
         // every load issued unconditionally (a slot with idx < 0 re-reads slot 0 and is ignored), so
@@ -193,6 +195,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
     extern __shared__ __align__(16) float sm[];
     int* ctl = reinterpret_cast<int*>(sm + L_CTL + TR_SPX * (2 + TR_CPS));  // [0] abort, [1] rank, [2] nx, [3] all done, [4..8) done
     const long long tmo = a.timeout_ticks;
+    const int fsl = a.first_sleep;
     // phase timers (measurement only, tts_tacotron_resident_phases): CUs 0 and 1 of group 0
     bool prof = false;
     long long plast = 0;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                 const bool ok = sweep<3>(Gp + G_PRE1, Ep + P_PRE1, v3, [&](int i) {
                     if (i < 2) return gs * T_PRE1 + gf * 128 + ln + 64 * i;
                     return (wave == 0 && ln < ns) ? TR_SPX * T_PRE1 + ln : -1;
-                }, tmo);
+                }, tmo, fsl);
                 pre1[gs * T_PRE1 + gf * 128 + lane] = v3[0];
                 pre1[gs * T_PRE1 + gf * 128 + 64 + lane] = v3[1];
                 if (wave == 0 && lane < ns) dn[lane] = v3[2] == 0.f ? 1 : 0;
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         }
         if (gon) {
             float v1[1];
-            const bool ok = sweep<1>(G + G_PRE2, E + P_PRE2, v1, [&](int i) { return gs * T_PRE2 + gf * 64 + ln; }, tmo);
+            const bool ok = sweep<1>(G + G_PRE2, E + P_PRE2, v1, [&](int i) { return gs * T_PRE2 + gf * 64 + ln; }, tmo, fsl);
             xa[gs * TXA + gf * 64 + lane] = v1[0];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 2); }
         }
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         MARK(12);
         if (gon) {
             float v2[2];
-            const bool ok = sweep<2>(G + G_HATT, E + P_HATT, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo);
+            const bool ok = sweep<2>(G + G_HATT, E + P_HATT, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo, fsl);
             hatt[gs * TD + gf * 128 + lane] = v2[0];
             hatt[gs * TD + gf * 128 + 64 + lane] = v2[1];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 3); }
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         }
         if (att_on && wave < 2) {
             float v1[1];
-            const bool ok = sweep<1>(G + G_Q, E + P_Q, v1, [&](int i) { return sa * ADIM + wave * 64 + ln; }, tmo);
+            const bool ok = sweep<1>(G + G_Q, E + P_Q, v1, [&](int i) { return sa * ADIM + wave * 64 + ln; }, tmo, fsl);
             q[wave * 64 + lane] = v1[0];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 4); }
         }
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                 bool ok = true;
                 if (tid < ATTP_W - 1)
                     ok = sweep<TR_CPS>(G + G_ATTP + sa * TR_CPS * ATTP_W, E + P_ATTP, v8,
-                                       [&](int i) { return i * ATTP_W + tid; }, tmo);
+                                       [&](int i) { return i * ATTP_W + tid; }, tmo, fsl);
                 __syncthreads();  // red is rewritten below
                 if (tid < ATTP_W - 1) {
                     float sum = 0.f;
@@ -573,7 +576,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             const bool ok = sweep<3>(G + G_CTXF, E + P_CTXF, v3, [&](int i) {
                 if (i < 2) return gs * CTXF_W + gf * 128 + ln + 64 * i;
                 return (gf == 1 && ln < 2 + TR_CPS) ? gs * CTXF_W + TD + ln : -1;
-            }, tmo);
+            }, tmo, fsl);
             xa[gs * TXA + T_PRE2 + gf * 128 + lane] = v3[0];
             xa[gs * TXA + T_PRE2 + gf * 128 + 64 + lane] = v3[1];
             if (gf == 1) {
@@ -612,7 +615,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
         }
         if (gon) {
             float v2[2];
-            const bool ok = sweep<2>(G + G_DIN, E + P_DIN, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo);
+            const bool ok = sweep<2>(G + G_DIN, E + P_DIN, v2, [&](int i) { return gs * TD + gf * 128 + ln + 64 * i; }, tmo, fsl);
             din[gs * TD + gf * 128 + lane] = v2[0];
             din[gs * TD + gf * 128 + 64 + lane] = v2[1];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 7); }
@@ -671,7 +674,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
                 float v4[4];
                 const bool ok = sweep<4>(gg, tg, v4, [&](int i) {
                     return (i < 2 ? 0 : TR_SPX * TD) + gs * TD + gf * 128 + ln + 64 * (i & 1);
-                }, tmo);
+                }, tmo, fsl);
                 Hn[gs * TD + gf * 128 + lane] = v4[0];
                 Hn[gs * TD + gf * 128 + 64 + lane] = v4[1];
                 Dn[gs * TD + gf * 128 + lane] = v4[2];
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(TR_THREADS, 1) void tacotron_resident_kernel(const 
             float v4[4];
             const bool ok = sweep<4>(G + G_MEL, E + P_MEL, v4, [&](int i) {
                 return gs * TR_NMEL_MAX + gf * 256 + ln + 64 * i;
-            }, tmo);
+            }, tmo, fsl);
 #pragma unroll
             for (int i = 0; i < 4; ++i) mel[gs * TR_NMEL_MAX + gf * 256 + lane + 64 * i] = v4[i];
             if (!ok && lane == 0) { ctl[0] = 1; fail(a.status, 12); }
