@@ -936,7 +936,7 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
                         pk[RB_PROF_SLOTS - 1]);
                 for (int w = 0; w < 4; ++w) {
                     fprintf(stderr, "[tts]  wave %d:", w);
-                    for (int k = 0; k < 13; ++k) {
+                    for (int k : {0, 1, 2, 3, 4, 5, 6, 20, 21, 22, 23, 7, 8, 9, 10, 11, 12}) {
                         double mn = 1e30, mx = 0, sum = 0;
                         for (int cu = 0; cu < RES_CUS; ++cu) {
                             const double v = pk[((size_t)cu * 4 + w) * RB_PROF_SLOTS + k] * 0.01 / steps;
@@ -1010,12 +1010,15 @@ tts_status decoder_run(tts_decoder* d, const float* enc, const int32_t* lens, in
         };
         static const int sl_hatt = knob("TTS_RES_SLEEP_HATT", 5), sl_hdec = knob("TTS_RES_SLEEP_HDEC", 5),
                          sl_p1 = knob("TTS_RES_SLEEP_P1", 0), sl_pre2 = knob("TTS_RES_SLEEP_PRE2", 2),
-                         sl_ctx = knob("TTS_RES_SLEEP_CTX", 0);
+                         sl_ctx = knob("TTS_RES_SLEEP_CTX", 0), sl_q = knob("TTS_RES_SLEEP_Q", 0),
+                         sl_e = knob("TTS_RES_SLEEP_E", 0);
         ra.sleep_hatt = sl_hatt;
         ra.sleep_hdec = sl_hdec;
         ra.sleep_p1 = sl_p1;
         ra.sleep_pre2 = sl_pre2;
         ra.sleep_ctx = sl_ctx;
+        ra.sleep_q = sl_q;
+        ra.sleep_e = sl_e;
         ra.status = reinterpret_cast<int*>(d->gran + 2 * GR_TOTAL);
         // direct (pipelined) runs skip the per-launch clear and rely on the 18-bit tag salt: on a
         // salt wrap a granule left 2^18 launches back could match a current wait, so clear then

@@ -124,6 +124,7 @@ struct ResArgs {
     // s_sleep(4) counts (~0.12 us each) before the first poll of a gather: a poll storm from every CU
     // slows the hand-off it waits for (device-wide h_att / h_dec; XCD-local pre1, prenet-2, context)
     int sleep_hatt, sleep_hdec, sleep_p1, sleep_pre2, sleep_ctx;
+    int sleep_q, sleep_e;  // s_sleep(1) counts: the query gather, the general form's energy gather
     long long* prof;           // null, or RES_PROF_LL: [2][RES_PHASES] wall-clock ticks summed over steps
                                // per phase (CU 0, attention CU), then the event trace — measurement only
     int prof_marks;            // with prof: also the per-phase marks (they perturb the two CUs that take them)
@@ -189,7 +190,7 @@ struct ResBatchArgs {
     int sleep_hatt, sleep_hdec, sleep_pre2, sleep_ctx;  // s_sleep(4) counts before a gather's first poll (TTS_RB_SLEEP_*)
     long long* prof;           // [256 CU][4 waves][RB_PROF_SLOTS] phase clocks (TTS_RB_PROF=1), else null
 };
-constexpr int RB_PROF_SLOTS = 20;  // [0, 13) phase sums, [13, 19) clocks at step RB_PROF_T, [19] steps
+constexpr int RB_PROF_SLOTS = 26;  // [0, 13) phase sums, [13, 19) clocks at step RB_PROF_T, [20, 24) attention sub-phases, [25] steps
 constexpr int RB_PROF_T = 150;
 void resident_batch_weight_floats(size_t* wa, size_t* wd);
 size_t resident_batch_granules();

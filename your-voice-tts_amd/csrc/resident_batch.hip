@@ -356,6 +356,17 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
     // P of sentence ab (read each step from L2, issued before the query wait)
     const auto rpt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.Pt + (size_t)(att_w ? ab : 0) * ADIM * a.Lcap),
                                                        (short)0, ADIM * a.Lcap * 4, 0x00020000);
+    // this lane's P at the wave's positions rank + 32 i (dims 2 lane, 2 lane + 1): constant over the
+    // launch, held in registers (a per-step reload held the query poll up behind ~1000 scattered
+    // cache-line reads per wave: vmcnt is in order)
+    float2 gp[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int pe = rank + 32 * i;
+        const bool on = att_w && pe < Lb;
+        gp[i].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rpt, on ? (2 * lane * a.Lcap + pe) * 4 : OOB_OFF, 0, 0));
+        gp[i].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rpt, on ? ((2 * lane + 1) * a.Lcap + pe) * 4 : OOB_OFF, 0, 0));
+    }
     const auto rg = __builtin_amdgcn_make_buffer_rsrc(a.gran, (short)0, 2 * RBG_TOTAL * 8, 0x00020000);
     const int xb = RBG_X + xcc * RBX_SIZE;  // this XCD's block (the parity offset is added per step)
     __syncthreads();
@@ -494,20 +505,12 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
             if (lane < 16) publish_xcd(G + xb + RBX_CTX + ab * ENC + 16 * rank + lane, E + 4, 0.f);
             if (rank == 0 && lane == 16) publish_xcd(G + xb + RBX_TAIL + ab, E + 4, 0.f);
         } else if (att_w) {
-            float2 gp[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int pe = rank + 32 * i;
-                gp[i].x = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    rpt, pe < Lb ? (2 * lane * a.Lcap + pe) * 4 : OOB_OFF, 0, VOLATILE_AUX));
-                gp[i].y = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                    rpt, pe < Lb ? ((2 * lane + 1) * a.Lcap + pe) * 4 : OOB_OFF, 0, VOLATILE_AUX));
-            }
             float2 q = float2{0.f, 0.f};
             {
                 const bool ok = sweep_pair(rg, P + xb + RBX_Q + ab * ADIM + 2 * lane, true, E + 3, q.x, q.y, tmo);
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 3, t); }
             }
+            mark(20);
             // the energy of positions rank + 32 i: v . tanh(q + P) + b_v (common_layers.py:178-182)
             {
                 float ev[8];
@@ -517,6 +520,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 const int pe = rank + 32 * (lane >> 3);
                 if ((lane & 7) == 0 && pe < Lb) publish_xcd(G + xb + RBX_E + ab * RES_LMAX + pe, E + 7, r + vb);
             }
+            mark(21);
             // sentence ab's energies from every CU of the XCD: positions 2 lane (+1), 128 + 2 lane (+1)
             int ps[4];
             bool in[4];
@@ -530,6 +534,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                 e[0] = e0; e[1] = e1; e[2] = e2; e[3] = e3;
                 if (!ok && lane == 0) { flags[1] = 1; fail(a.status, 8, t); }
             }
+            mark(22);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 ps[i] = (i >> 1) * 128 + 2 * lane + (i & 1);
@@ -594,6 +599,7 @@ __global__ __launch_bounds__(RB_THREADS, 1) void resident_batch_kernel(const Res
                                             ((ps[2] >= Lb - 2 && in[2] ? w[2] : 0.f) + (ps[3] >= Lb - 2 && in[3] ? w[3] : 0.f)));
             *reinterpret_cast<float2*>(wnew + 2 * lane) = float2{w[0], w[1]};
             *reinterpret_cast<float2*>(wnew + 128 + 2 * lane) = float2{w[2], w[3]};
+            mark(23);
             // the context of channels 16 rank + (lane & 15) over positions (lane >> 4) + 4 m (bmm, :217 /
             // :253) from the LDS copy; the weights were just written by this wave (in order)
             const float* es = sm + S::ENCS + ab * S::ENC_L * 16 + (lane & 15);

@@ -532,6 +532,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                     renc, ps < L ? (ps * ENC + 16 * rank + 2 * wave) * 4 : OOB_OFF, 0, VOLATILE_AUX));
             }
             if (wave < 2) {
+                for (int i = 0; i < a.sleep_q; ++i) __builtin_amdgcn_s_sleep(1);
                 float q0, q1;
                 const bool ok = sweep_pair(rg, s_q + (t & 1) * GR_TOTAL + 2 * pk, true, E + 3, q0, q1, tmo);
                 xq[pk] = q0 + q1;
@@ -552,6 +553,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             }
             // every CU gathers the XCD's L energies (waves 0-1: positions 2 pk, 2 pk + 1)
             if (wave < 2) {
+                for (int i = 0; i < a.sleep_e; ++i) __builtin_amdgcn_s_sleep(1);
                 const int p0 = 2 * pk;
                 float e0 = 0.f, e1 = 0.f;
                 const bool ok =
@@ -704,6 +706,7 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
             for (int m = 0; m < 4; ++m) xvd[m] = xv[sub + 32 * m];
             const float a_pos = pos >= 0 ? aold[pos] : 0.f, a_prev = pos > 0 ? aold[pos - 1] : 0.f;
             if (wave < 2) {  // query row pk = its two half-rows
+                for (int i = 0; i < a.sleep_q; ++i) __builtin_amdgcn_s_sleep(1);
                 float q0, q1;
                 const bool ok = sweep_pair(rg, s_q + (t & 1) * GR_TOTAL + 2 * pk, true, E + 3, q0, q1, tmo);
                 xq[pk] = q0 + q1;
