@@ -484,19 +484,6 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
                 ptc[m] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
                     rpt, pos >= 0 ? (((tid & 31) + 32 * m) * a.Lcap + pos) * 4 : OOB_OFF, 0, VOLATILE_AUX));
         }
-        // general form: this lane's encoder values of the context (channels 16 rank + 2 wave + {0, 1}
-        // at its positions), issued before the h_att poll's delay so that they have landed when the
-        // query is polled (vmcnt is in order: issued after the h_att gather, they held the query
-        // poll up by their latency)
-        float2 gen_e[4];
-        if constexpr (GEN) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int ps = (i >> 1) * 128 + 2 * lane + (i & 1);
-                gen_e[i] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
-                    renc, ps < L ? (ps * ENC + 16 * rank + 2 * wave) * 4 : OOB_OFF, 0, VOLATILE_AUX));
-            }
-        }
         {
             if (wave == 4 && t > 0) mel_row(t - 1);
             for (int i = 0; i < a.sleep_hatt; ++i) __builtin_amdgcn_s_sleep(4);
@@ -534,8 +521,16 @@ __global__ __launch_bounds__(RES_THREADS, 1) void resident_decoder_kernel(const 
         //    (<= 15 positions, duplicates harmless) whenever max over C >= 1e-8.  Step 0 (alpha
         //    initialised nonzero everywhere) and that rare case evaluate every position.
         if constexpr (GEN) {
-            // 7') general attention form (resident.h): the query of this XCD's copy (waves 0-1; the
-            // context's encoder values were issued before the h_att gather)
+            // 7') general attention form (resident.h).  This lane's encoder values of the context
+            // (channels 16 rank + 2 wave + {0, 1} at its positions; volatile: issued here, in flight
+            // across the query and energy hand-offs), then the query of this XCD's copy (waves 0-1)
+            float2 gen_e[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ps = (i >> 1) * 128 + 2 * lane + (i & 1);
+                gen_e[i] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(
+                    renc, ps < L ? (ps * ENC + 16 * rank + 2 * wave) * 4 : OOB_OFF, 0, VOLATILE_AUX));
+            }
             if (wave < 2) {
                 for (int i = 0; i < a.sleep_q; ++i) __builtin_amdgcn_s_sleep(1);
                 float q0, q1;
