@@ -42,10 +42,12 @@ sharding = importlib.import_module("your-voice-tts_amd.sharding")
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP32_MFMA_PEAK_TF = 157.3  # dense fp32 MFMA peak (same table)
-# one hand-off edge of the resident decoder in isolation (tools/microbench/edge.hip, round 4: one
-# 16-byte granule pair per lane; device-wide 1024 granules on 8 waves, XCD-local 256 on 2 waves)
-EDGE_DEVICE_US = 1.60
-EDGE_XCD_US = 0.47
+# one hand-off edge of the resident decoder in isolation (tools/microbench/edge.hip, one 16-byte
+# granule pair per lane; device-wide 1024 granules on 8 waves, XCD-local 256 on 4 waves), the best
+# over first-poll delays (round 6, profiles/r06_edge_floor.log: device-wide 1.61 us polling at once,
+# 0.98 with a ~0.36 us delay; XCD-local 0.76, no delay; round 4 had measured 1.60 / 0.47)
+EDGE_DEVICE_US = 0.98
+EDGE_XCD_US = 0.76
 FP64_VECTOR_PEAK_TF = 78.6  # fp64 vector FMA peak (same table)
 # one GL frame-iteration: forward + inverse 1024-point complex FFT (5 N log2 N each) plus the
 # real-FFT split / merge and the phase projection (~20 flops per bin each way)
@@ -750,7 +752,7 @@ def main():
                 fp32_compute_frac=flops / (dec_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF,
                 device_wide_edges_us_per_step=dev_edges, xcd_local_edges_us_per_step=xcd_edges,
                 edge_microbench_us=dict(device_wide=EDGE_DEVICE_US, xcd_local=EDGE_XCD_US,
-                                        source="tools/microbench/edge.hip (one 16-byte granule pair per lane)"),
+                                        source="tools/microbench/edge.hip (one 16-byte granule pair per lane, best first-poll delay; profiles/r06_edge_floor.log)"),
                 latency_floor_us=floor, step_over_floor=us / floor, us_per_step=us)
             # the resident decoder's weights never leave the chip (counter traffic ~1 % of the SURVEY
             # 8(d) bytes): its roofline is the hand-off latency floor, not HBM.  The

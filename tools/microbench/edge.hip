@@ -6,7 +6,10 @@
 //                       republishes it XCD-locally (sc0), then GW waves sweep the XCD's 1024 copies
 //   mode 2: XCD-local — every CU publishes 8 granules XCD-locally, GW waves sweep the XCD's 256
 //   mode 3: flat 8 KB, only the 32 CUs of one rank-class read (the other CUs publish and skip)
-// usage: edge <mode> <GW> <rounds>
+//   mode 4: flat device-wide 1024 granules as 16-byte pairs; mode 5: XCD-local 256 as pairs
+// usage: edge <mode> <GW> <rounds> [first_sleep]: first_sleep x s_sleep 4 before a round's first
+// poll (round 6: a poll storm from every CU slows the stores it waits for).  Every spin is bounded
+// (1 << 22 polls): a lost round ends the kernel with a wrong time instead of a hang.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -28,7 +31,7 @@ __device__ __forceinline__ u64 peek(u64* g) {
 }
 template <int N, typename F>
 __device__ __forceinline__ void sweep(u64* g, unsigned tag, float (&v)[N], F idx) {
-    for (;;) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
@@ -48,7 +51,7 @@ typedef __attribute__((address_space(1))) u64x2 gu64x2;
 // N 16-byte loads per lane, each = granules (2k, 2k + 1) of pair index k = idx(i)
 template <int N, typename F>
 __device__ __forceinline__ void sweep16(u64* g, unsigned tag, float (&v)[2 * N], F idx) {
-    for (;;) {
+    for (int spin = 0; spin < (1 << 22); ++spin) {
         bool ok = true;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
@@ -68,7 +71,8 @@ __device__ __forceinline__ void sweep16(u64* g, unsigned tag, float (&v)[2 * N],
 constexpr int GR_TAB = 0, GR_DEV = 512, GR_X = GR_DEV + 2 * 1024, GR_TOTAL = GR_X + 2 * 8 * 1024;
 
 template <int GW>
-__global__ __launch_bounds__(512, 1) void edge_kernel(u64* gran, int mode, int rounds, float* sink, long long* ticks) {
+__global__ __launch_bounds__(512, 1) void edge_kernel(u64* gran, int mode, int rounds, float* sink, long long* ticks,
+                                                      int first_sleep) {
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ float xs[1024];
     __shared__ int info[4];
@@ -110,6 +114,8 @@ __global__ __launch_bounds__(512, 1) void edge_kernel(u64* gran, int mode, int r
             __syncthreads();
             continue;
         }
+        if (wave < GW)
+            for (int i = 0; i < first_sleep; ++i) __builtin_amdgcn_s_sleep(4);
         if (mode >= 4 && wave < GW) {
             // 16-byte pair loads: mode 4 flat device-wide, mode 5 XCD-local 256
             constexpr int PER = 512 / (64 * GW);  // pairs per lane
@@ -149,7 +155,7 @@ __global__ __launch_bounds__(512, 1) void edge_kernel(u64* gran, int mode, int r
 
 int main(int argc, char** argv) {
     const int mode = argc > 1 ? atoi(argv[1]) : 0, gw = argc > 2 ? atoi(argv[2]) : 4,
-              rounds = argc > 3 ? atoi(argv[3]) : 2000;
+              rounds = argc > 3 ? atoi(argv[3]) : 2000, first_sleep = argc > 4 ? atoi(argv[4]) : 0;
     u64* gran;
     float* sink;
     long long* ticks;
@@ -161,7 +167,7 @@ int main(int argc, char** argv) {
     auto fn = gw == 8 ? (void*)edge_kernel<8> : gw == 2 ? (void*)edge_kernel<2> : (void*)edge_kernel<4>;
     for (int rep = 0; rep < 3; ++rep) {
         (void)hipMemset(gran, 0, sizeof(u64) * GR_TOTAL);
-        void* args[] = {&gran, (void*)&mode, (void*)&rounds, &sink, &ticks};
+        void* args[] = {&gran, (void*)&mode, (void*)&rounds, &sink, &ticks, (void*)&first_sleep};
         (void)hipLaunchKernel(fn, dim3(256), dim3(512), args, 0, 0);
         if (hipDeviceSynchronize() != hipSuccess) {
             printf("fail\n");
@@ -171,7 +177,8 @@ int main(int argc, char** argv) {
         (void)hipMemcpy(t.data(), ticks, 8 * 256, hipMemcpyDeviceToHost);
         long long mx = 0;
         for (long long v : t) mx = v > mx ? v : mx;
-        printf("mode %d GW %d rounds %d: %.3f us per round\n", mode, gw, rounds, 1e3 * (double)mx / rate / rounds);
+        printf("mode %d GW %d rounds %d first_sleep %d: %.3f us per round\n", mode, gw, rounds, first_sleep,
+               1e3 * (double)mx / rate / rounds);
     }
     return 0;
 }
